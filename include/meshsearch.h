@@ -1,0 +1,142 @@
+/*
+ * meshsearch.h — C ABI of the MI355X-native point-to-mesh spatial search engine (libmeshsearch.so).
+ *
+ * Drop-in replacement for the three CPython extensions of psbody-mesh 0.4 that wrap CGAL 4.7's
+ * AABB_tree (KanaLab/mesh: mesh/src/spatialsearchmodule.cpp, mesh/src/aabb_normals.cpp,
+ * mesh/src/py_visibility.cpp) and for the scipy KDTree behind search.ClosestPointTree.  Every entry
+ * point takes plain pointers and sizes; no Python, numpy or torch type crosses this boundary.
+ * The Python shims in mesh_amd/ (spatialsearch.py, aabb_normals.py, visibility.py, search.py) bind
+ * these functions with ctypes; INTEGRATION.md shows the binding a psbody-mesh maintainer would add.
+ *
+ * Conventions
+ *  - Arrays are C-contiguous row-major: points/normals (N,3) double, faces (T,3) uint32.
+ *  - Every function returns MSH_OK (0) or an error code; msh_last_error() gives the message of the
+ *    last failure on the calling thread.  MSH_EINVAL maps to ValueError (bad shape / index),
+ *    MSH_EDEVICE / MSH_ENOMEM to RuntimeError (HIP failure), as the reference raises
+ *    (spatialsearchmodule.cpp:82-97 ValueError; cgal_error_emulation.hpp:19-33 RuntimeError).
+ *  - Host-buffer entry points (no _device suffix) copy inputs to HBM, run the HIP kernels and copy
+ *    results back; they are synchronous.  *_device entry points take HBM pointers and a hipStream_t
+ *    (passed as void*, NULL = the handle's own stream) and are asynchronous on that stream.
+ *  - A handle owns device copies of the mesh and its BVH (the reference's TreeAndTri owns host
+ *    copies, nearest_triangle.hpp:28-32); input arrays are not retained.  Calls on one handle must be
+ *    serialised by the caller; different handles are independent.
+ *  - There is no CPU fallback: without a usable gfx950 device every compute entry point fails with
+ *    MSH_EDEVICE.
+ */
+#ifndef MESHSEARCH_H_
+#define MESHSEARCH_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSH_OK 0
+#define MSH_EINVAL 1
+#define MSH_EDEVICE 2
+#define MSH_ENOMEM 3
+
+#define MSH_NO_FACE 0xFFFFFFFFu
+
+typedef struct msh_tree msh_tree;
+
+typedef struct msh_tree_info {
+    int device;          /* HIP device ordinal holding the tree */
+    int kind;            /* 0 triangles (spatialsearch), 1 normals metric (aabb_normals), 2 points */
+    uint64_t n_points;   /* P: vertices of the main mesh */
+    uint64_t n_faces;    /* T: leaf primitives (main + extra mesh faces, or points) */
+    uint64_t n_main_faces;
+    uint64_t n_nodes;    /* internal LBVH nodes (T-1) */
+    uint64_t bytes;      /* device bytes owned by the handle (mesh + BVH) */
+    double eps;
+    float scene_lo[3], scene_hi[3];
+    double build_ms;     /* GPU time of the LBVH build (Morton + radix sort + emission + refit) */
+} msh_tree_info;
+
+/* ---- library / device ---- */
+const char* msh_last_error(void);
+int msh_version(void);
+int msh_device_count(int* n);
+/* Device used by subsequent builds on the calling thread (default: current HIP device). */
+int msh_set_device(int device);
+
+/* ---- spatialsearch (spatialsearchmodule.cpp) ---- */
+/* aabbtree_compute(v, f) -> capsule: spatialsearchmodule.cpp:74-127 (TreeAndTri build :108-123).
+ * GPU LBVH build: Morton codes of triangle centroids, LDS radix sort, Karras emission, atomic refit. */
+int msh_tree_build(const double* v, size_t P, const uint32_t* f, size_t T, msh_tree** out);
+/* visibility_compute(v=, f=, extra_v=, extra_f=) builds over main + extra triangles:
+ * py_visibility.cpp:114-163.  extra may be NULL/0. */
+int msh_tree_build_ex(const double* v, size_t P, const uint32_t* f, size_t T, const double* ev, size_t EP,
+                      const uint32_t* ef, size_t ET, msh_tree** out);
+/* capsule destructor: spatialsearchmodule.cpp:68-72 */
+void msh_tree_free(msh_tree* tree);
+int msh_tree_get_info(const msh_tree* tree, msh_tree_info* info);
+
+/* aabbtree_nearest(tree, q) -> (face (1,S) u32, part (1,S) u32, point (S,3) f64):
+ * spatialsearchmodule.cpp:165-220, per query nearest_one :129-140.  part may be NULL.
+ * Closest face = lexicographic minimum of (squared distance, face index); point = CGAL's
+ * construction for that face (project on plane, edge, vertex); part = iev::nearest_primitive code. */
+int msh_tree_nearest(msh_tree* tree, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt);
+int msh_tree_nearest_device(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part,
+                            double* d_pt, void* stream);
+/* Instrumented traversal (not timed): total internal nodes popped and leaf triangles tested over the
+ * S queries, for the algorithmic-bytes figure of the roofline. */
+int msh_tree_nearest_stats(msh_tree* tree, const double* d_q, size_t S, uint64_t* nodes, uint64_t* leaves);
+
+/* aabbtree_nearest_alongnormal(tree, p, n) -> (dist (S,) f64, face (S,) u32, point (S,3) f64):
+ * spatialsearchmodule.cpp:222-323.  Nearest hit of the rays (p, n) and (p, -n).  No hit:
+ * dist = 1e100 (as the reference), face = MSH_NO_FACE, point = NaN (reference: uninitialised). */
+int msh_tree_nearest_alongnormal(msh_tree* tree, const double* p, const double* n, size_t S, double* dist,
+                                 uint32_t* face, double* pt);
+
+/* aabbtree_intersections_indices(tree, qv, qf) -> ascending query-face indices (K,) u32 whose
+ * triangle intersects any mesh triangle: spatialsearchmodule.cpp:326-417 (unregistered there,
+ * SURVEY App. B).  out must hold Tq entries; *K receives the count. */
+int msh_tree_intersections(msh_tree* tree, const double* qv, size_t Pq, const uint32_t* qf, size_t Tq, uint32_t* out,
+                           size_t* K);
+
+/* ---- aabb_normals (aabb_normals.cpp, AABB_n_tree.h) ---- */
+/* aabbtree_n_compute(v, f, eps): aabb_normals.cpp:63-110 */
+int msh_ntree_build(const double* v, size_t P, const uint32_t* f, size_t T, double eps, msh_tree** out);
+/* aabbtree_n_nearest(tree, v, n) -> (face (1,S) u32, point (S,3) f64): aabb_normals.cpp:112-190.
+ * Metric ||q - p|| + eps (1 - n_q . n_tri) (AABB_n_tree.h:40-84); lexicographic min (metric, face). */
+int msh_ntree_nearest(msh_tree* tree, const double* q, const double* n, size_t S, uint32_t* face, double* pt);
+/* aabbtree_n_selfintersects(tree) -> int: aabb_normals.cpp:192-207; pairs sharing an exactly equal
+ * vertex coordinate are skipped (AABB_n_tree.h:107-116). */
+int msh_ntree_selfintersects(msh_tree* tree, int64_t* count);
+
+/* ---- visibility (py_visibility.cpp, visibility.cpp) ---- */
+/* visibility_compute(cams, tree|v,f, n, sensors, extra_v, extra_f, min_dist) -> (vis (C,P) u32,
+ * n_dot_cam (C,P) f64): py_visibility.cpp:81-219, VisibilityTask visibility.cpp:75-115.
+ * Visibility is computed for the tree's main-mesh vertices.  normals (P,3) and sensors (C,9) may be
+ * NULL; without normals ndc is zero-filled (reference: uninitialised).  The tree is borrowed, never
+ * freed (fixes the double free at py_visibility.cpp:212). */
+int msh_visibility(msh_tree* tree, const double* cams, size_t C, const double* normals, const double* sensors,
+                   double min_dist, uint32_t* vis, double* ndc);
+
+/* ---- ClosestPointTree (search.py:52-65, scipy.spatial.KDTree) ---- */
+int msh_points_build(const double* v, size_t P, msh_tree** out);
+/* nearest vertex: lexicographic min (squared distance, vertex index); dist = sqrt(d2) */
+int msh_points_nearest(msh_tree* tree, const double* q, size_t S, uint32_t* idx, double* dist);
+
+/* ---- multi-GPU replication (RCCL broadcast of a built BVH over xGMI) ---- */
+/* Size of the flat device blob holding the mesh + BVH of a handle. */
+int msh_tree_blob_size(const msh_tree* tree, size_t* bytes);
+/* Pack the handle's device buffers into d_dst (HBM, on the handle's device, blob_size bytes). */
+int msh_tree_blob_pack(const msh_tree* tree, void* d_dst, void* stream);
+/* Create a handle on `device` from a packed blob already resident in that device's HBM
+ * (e.g. after an RCCL broadcast).  The blob is copied; the caller keeps ownership of d_src. */
+int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stream, msh_tree** out);
+
+/* ---- kernel timing (HIP events on the launch stream; used by bench.py's roofline) ---- */
+int msh_timing_enable(int on);
+/* Total milliseconds and launch count of kernel `name` ("nearest", "sort", "morton") since reset. */
+int msh_timing_get(const char* name, double* ms, int64_t* count);
+int msh_timing_reset(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MESHSEARCH_H_ */

@@ -1,0 +1,198 @@
+"""ctypes binding of ``libmeshsearch.so`` (C ABI declared in ``include/meshsearch.h``).
+
+This is the only place that touches the native library.  There is no CPU fallback: if the library is
+missing, cannot be loaded, or no HIP device is usable, every call raises.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MESH_AMD_LIB", os.path.join(_HERE, "lib", "libmeshsearch.so"))
+
+MSH_OK, MSH_EINVAL, MSH_EDEVICE, MSH_ENOMEM = 0, 1, 2, 3
+NO_FACE = 0xFFFFFFFF
+
+_c_double_p = ctypes.POINTER(ctypes.c_double)
+_c_u32_p = ctypes.POINTER(ctypes.c_uint32)
+_c_u64_p = ctypes.POINTER(ctypes.c_uint64)
+_c_i64_p = ctypes.POINTER(ctypes.c_int64)
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_i = ctypes.c_int
+
+_lib = None
+_lock = threading.Lock()
+
+# (name, restype, argtypes) for every symbol of include/meshsearch.h
+SIGNATURES = [
+    ("msh_last_error", ctypes.c_char_p, []),
+    ("msh_version", _i, []),
+    ("msh_device_count", _i, [ctypes.POINTER(_i)]),
+    ("msh_set_device", _i, [_i]),
+    ("msh_tree_build", _i, [_c_double_p, _sz, _c_u32_p, _sz, ctypes.POINTER(_vp)]),
+    ("msh_tree_build_ex", _i, [_c_double_p, _sz, _c_u32_p, _sz, _c_double_p, _sz, _c_u32_p, _sz, ctypes.POINTER(_vp)]),
+    ("msh_tree_free", None, [_vp]),
+    ("msh_tree_get_info", _i, [_vp, _vp]),
+    ("msh_tree_nearest", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_u32_p, _c_double_p]),
+    ("msh_tree_nearest_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    ("msh_tree_nearest_stats", _i, [_vp, _vp, _sz, _c_u64_p, _c_u64_p]),
+    ("msh_tree_nearest_alongnormal", _i, [_vp, _c_double_p, _c_double_p, _sz, _c_double_p, _c_u32_p, _c_double_p]),
+    ("msh_tree_intersections", _i, [_vp, _c_double_p, _sz, _c_u32_p, _sz, _c_u32_p, ctypes.POINTER(_sz)]),
+    ("msh_ntree_build", _i, [_c_double_p, _sz, _c_u32_p, _sz, ctypes.c_double, ctypes.POINTER(_vp)]),
+    ("msh_ntree_nearest", _i, [_vp, _c_double_p, _c_double_p, _sz, _c_u32_p, _c_double_p]),
+    ("msh_ntree_selfintersects", _i, [_vp, _c_i64_p]),
+    ("msh_visibility", _i, [_vp, _c_double_p, _sz, _c_double_p, _c_double_p, ctypes.c_double, _c_u32_p, _c_double_p]),
+    ("msh_points_build", _i, [_c_double_p, _sz, ctypes.POINTER(_vp)]),
+    ("msh_points_nearest", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_double_p]),
+    ("msh_tree_blob_size", _i, [_vp, ctypes.POINTER(_sz)]),
+    ("msh_tree_blob_pack", _i, [_vp, _vp, _vp]),
+    ("msh_tree_blob_unpack", _i, [_vp, _sz, _i, _vp, ctypes.POINTER(_vp)]),
+    ("msh_timing_enable", _i, [_i]),
+    ("msh_timing_get", _i, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _c_i64_p]),
+    ("msh_timing_reset", _i, []),
+]
+
+
+class TreeInfo(ctypes.Structure):
+    _fields_ = [("device", _i), ("kind", _i), ("n_points", ctypes.c_uint64), ("n_faces", ctypes.c_uint64),
+                ("n_main_faces", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
+                ("eps", ctypes.c_double), ("scene_lo", ctypes.c_float * 3), ("scene_hi", ctypes.c_float * 3),
+                ("build_ms", ctypes.c_double)]
+
+
+def lib():
+    """Load libmeshsearch.so (raises ImportError if it is missing — no fallback)."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError("libmeshsearch.so not built (%s): run `python -c 'import __graft_entry__ as g; "
+                                      "g.build()'` or `make -C mesh_amd/csrc`" % LIB_PATH)
+                L = ctypes.CDLL(LIB_PATH)
+                for name, res, args in SIGNATURES:
+                    fn = getattr(L, name)
+                    fn.restype = res
+                    fn.argtypes = args
+                _lib = L
+    return _lib
+
+
+def check(status, exc_value=ValueError):
+    if status == MSH_OK:
+        return
+    msg = lib().msh_last_error().decode("utf-8", "replace")
+    if status == MSH_EINVAL:
+        raise exc_value(msg)
+    raise RuntimeError(msg)
+
+
+def dptr(a):
+    return a.ctypes.data_as(_c_double_p) if a is not None else None
+
+
+def uptr(a):
+    return a.ctypes.data_as(_c_u32_p) if a is not None else None
+
+
+class Handle(object):
+    """Owning reference to an ``msh_tree*`` (the reference's PyCapsule, spatialsearchmodule.cpp:125)."""
+
+    __slots__ = ("ptr", "kind", "__weakref__")
+
+    def __init__(self, ptr, kind):
+        self.ptr = ptr
+        self.kind = kind
+
+    def info(self):
+        inf = TreeInfo()
+        check(lib().msh_tree_get_info(self.ptr, ctypes.byref(inf)))
+        return inf
+
+    def free(self):
+        if self.ptr:
+            lib().msh_tree_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def __repr__(self):
+        return "<meshsearch tree kind=%s at 0x%x>" % (self.kind, self.ptr or 0)
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    st = lib().msh_device_count(ctypes.byref(n))
+    return n.value if st == MSH_OK else 0
+
+
+def set_device(device):
+    check(lib().msh_set_device(int(device)))
+
+
+def build_tree(v, f, extra_v=None, extra_f=None):
+    out = _vp()
+    if extra_v is not None and extra_f is not None:
+        check(lib().msh_tree_build_ex(dptr(v), v.shape[0], uptr(f), f.shape[0], dptr(extra_v), extra_v.shape[0],
+                                      uptr(extra_f), extra_f.shape[0], ctypes.byref(out)))
+    else:
+        check(lib().msh_tree_build(dptr(v), v.shape[0], uptr(f), f.shape[0], ctypes.byref(out)))
+    return Handle(out.value, "triangles")
+
+
+def build_ntree(v, f, eps):
+    out = _vp()
+    check(lib().msh_ntree_build(dptr(v), v.shape[0], uptr(f), f.shape[0], float(eps), ctypes.byref(out)))
+    return Handle(out.value, "normals")
+
+
+def build_points(v):
+    out = _vp()
+    check(lib().msh_points_build(dptr(v), v.shape[0], ctypes.byref(out)))
+    return Handle(out.value, "points")
+
+
+def blob_size(h):
+    n = _sz(0)
+    check(lib().msh_tree_blob_size(h.ptr, ctypes.byref(n)))
+    return n.value
+
+
+def blob_pack(h, d_dst, stream=None):
+    check(lib().msh_tree_blob_pack(h.ptr, _vp(d_dst), _vp(stream) if stream else None))
+
+
+def blob_unpack(d_src, nbytes, device, stream=None, kind="triangles"):
+    out = _vp()
+    check(lib().msh_tree_blob_unpack(_vp(d_src), nbytes, int(device), _vp(stream) if stream else None,
+                                     ctypes.byref(out)))
+    return Handle(out.value, kind)
+
+
+def timing_enable(on=True):
+    check(lib().msh_timing_enable(1 if on else 0))
+
+
+def timing_get(name):
+    ms = ctypes.c_double(0)
+    n = ctypes.c_int64(0)
+    check(lib().msh_timing_get(name.encode(), ctypes.byref(ms), ctypes.byref(n)))
+    return ms.value, n.value
+
+
+def timing_reset():
+    check(lib().msh_timing_reset())
+
+
+def as_f64_nx3(a, name="Input"):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if a.ndim != 2 or a.shape[1] != 3:
+        raise ValueError("%s must be Nx3" % name)
+    return a

@@ -1,0 +1,322 @@
+// K1 — GPU LBVH build (replaces CGAL AABB_tree::rebuild's median-split build,
+// spatialsearchmodule.cpp:122, and accelerate_distance_queries' KD hint, :123).
+//
+//   1. k_tri_bounds / k_point_bounds   fp64 bounds of every primitive
+//   2. k_reduce_box (2 stages)         scene box (fp64)
+//   3. k_morton                        30-bit Morton code of each primitive's box centre
+//   4. radix_sort_pairs (sort.hip)     stable sort (key, primitive id): duplicate codes keep id order
+//   5. k_karras                        Karras (HPG 2012) internal-node emission; codes made unique by
+//                                      augmenting them with the sorted position
+//   6. k_refit                         bottom-up AABB refit, one lane per leaf, the second arrival at
+//                                      each node continues upward (agent-scope release/acquire hand-off,
+//                                      cdna_hip_programming.md §6 Guideline 16)
+//   7. k_depth                         max leaf depth (sizes the traversal stack spill)
+// Node boxes are fp32 rounded outward (round-down lo / round-up hi, then one more ulp) so every
+// fp64 primitive lies strictly inside the box of every ancestor.
+#include <algorithm>
+#include <memory>
+
+#include "internal.h"
+
+namespace msh {
+
+__global__ __launch_bounds__(kBlock) void k_tri_bounds(const double* __restrict__ v, const uint32_t* __restrict__ f,
+                                                       size_t T, double* __restrict__ lo, double* __restrict__ hi) {
+    const size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= T) return;
+    const uint32_t i0 = f[3 * t], i1 = f[3 * t + 1], i2 = f[3 * t + 2];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double a = v[3 * (size_t)i0 + k], b = v[3 * (size_t)i1 + k], c = v[3 * (size_t)i2 + k];
+        lo[3 * t + k] = fmin(fmin(a, b), c);
+        hi[3 * t + k] = fmax(fmax(a, b), c);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_point_bounds(const double* __restrict__ v, size_t P, double* __restrict__ lo,
+                                                         double* __restrict__ hi) {
+    const size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= 3 * P) return;
+    lo[t] = v[t];
+    hi[t] = v[t];
+}
+
+// out[6*b .. 6*b+5] = (min lo xyz, max hi xyz) over the block's range
+__global__ __launch_bounds__(kBlock) void k_reduce_box(const double* __restrict__ lo, const double* __restrict__ hi,
+                                                       size_t n, double* __restrict__ out) {
+    __shared__ double sh[6][kBlock];
+    const int tid = threadIdx.x;
+    double r[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (size_t i = (size_t)blockIdx.x * kBlock + tid; i < n; i += (size_t)gridDim.x * kBlock) {
+        r[0] = fmin(r[0], lo[3 * i]); r[1] = fmin(r[1], lo[3 * i + 1]); r[2] = fmin(r[2], lo[3 * i + 2]);
+        r[3] = fmax(r[3], hi[3 * i]); r[4] = fmax(r[4], hi[3 * i + 1]); r[5] = fmax(r[5], hi[3 * i + 2]);
+    }
+    for (int k = 0; k < 6; ++k) sh[k][tid] = r[k];
+    __syncthreads();
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+        if (tid < s) {
+            for (int k = 0; k < 3; ++k) sh[k][tid] = fmin(sh[k][tid], sh[k][tid + s]);
+            for (int k = 3; k < 6; ++k) sh[k][tid] = fmax(sh[k][tid], sh[k][tid + s]);
+        }
+        __syncthreads();
+    }
+    if (tid < 6) out[6 * blockIdx.x + tid] = sh[tid][0];
+}
+
+__device__ inline uint32_t expand_bits10(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+__device__ inline uint32_t morton30(double x, double y, double z, const double* box) {
+    const double ex = box[3] - box[0], ey = box[4] - box[1], ez = box[5] - box[2];
+    double nx = ex > 0 ? (x - box[0]) / ex : 0.5, ny = ey > 0 ? (y - box[1]) / ey : 0.5, nz = ez > 0 ? (z - box[2]) / ez : 0.5;
+    nx = fmin(fmax(nx * 1024.0, 0.0), 1023.0);
+    ny = fmin(fmax(ny * 1024.0, 0.0), 1023.0);
+    nz = fmin(fmax(nz * 1024.0, 0.0), 1023.0);
+    return (expand_bits10((uint32_t)nx) << 2) | (expand_bits10((uint32_t)ny) << 1) | expand_bits10((uint32_t)nz);
+}
+
+__global__ __launch_bounds__(kBlock) void k_morton(const double* __restrict__ lo, const double* __restrict__ hi, size_t n,
+                                                   const double* __restrict__ box, uint32_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ vals) {
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const double cx = 0.5 * (lo[3 * i] + hi[3 * i]);
+    const double cy = 0.5 * (lo[3 * i + 1] + hi[3 * i + 1]);
+    const double cz = 0.5 * (lo[3 * i + 2] + hi[3 * i + 2]);
+    keys[i] = morton30(cx, cy, cz, box);
+    vals[i] = (uint32_t)i;
+}
+
+// delta(i, j): common-prefix length of the augmented keys (code, position)
+__device__ inline int lbvh_delta(const uint32_t* __restrict__ k, int n, int i, int j) {
+    if (j < 0 || j >= n) return -1;
+    const uint32_t a = k[i], b = k[j];
+    if (a != b) return __clz(a ^ b);
+    return 32 + __clz((uint32_t)i ^ (uint32_t)j);
+}
+
+// parent[c]: (parent << 1) | side for internal c in [0, n-1) and leaf l at (n-1) + l
+__global__ __launch_bounds__(kBlock) void k_karras(const uint32_t* __restrict__ keys, int n, BNode* __restrict__ nodes,
+                                                   uint32_t* __restrict__ parent) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n - 1) return;
+    const int d = (lbvh_delta(keys, n, i, i + 1) - lbvh_delta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
+    const int dmin = lbvh_delta(keys, n, i, i - d);
+    int lmax = 2;
+    while (lbvh_delta(keys, n, i, i + lmax * d) > dmin) lmax <<= 1;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (lbvh_delta(keys, n, i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = lbvh_delta(keys, n, i, j);
+    int s = 0, t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (lbvh_delta(keys, n, i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    const int gamma = i + s * d + (d < 0 ? -1 : 0);
+    const int lo = min(i, j), hi = max(i, j);
+    const int left = (lo == gamma) ? ~gamma : gamma;
+    const int right = (hi == gamma + 1) ? ~(gamma + 1) : gamma + 1;
+    nodes[i].d = make_int4(left, right, 0, 0);
+    parent[left >= 0 ? left : (n - 1) + ~left] = ((uint32_t)i << 1) | 0u;
+    parent[right >= 0 ? right : (n - 1) + ~right] = ((uint32_t)i << 1) | 1u;
+}
+
+__device__ inline float down1(float x) { return nextafterf(x, -INFINITY); }
+__device__ inline float up1(float x) { return nextafterf(x, INFINITY); }
+
+__device__ inline void store_slot(BNode* nodes, int node, int side, const float* lo, const float* hi) {
+    float* p = reinterpret_cast<float*>(nodes + node);
+    if (side == 0) {
+        *reinterpret_cast<float4*>(p) = make_float4(lo[0], lo[1], lo[2], hi[0]);
+        *reinterpret_cast<float2*>(p + 4) = make_float2(hi[1], hi[2]);
+    } else {
+        *reinterpret_cast<float2*>(p + 6) = make_float2(lo[0], lo[1]);
+        *reinterpret_cast<float4*>(p + 8) = make_float4(lo[2], hi[0], hi[1], hi[2]);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_refit(const double* __restrict__ plo, const double* __restrict__ phi,
+                                                  const uint32_t* __restrict__ order, int n, BNode* nodes,
+                                                  const uint32_t* __restrict__ parent, uint32_t* flags) {
+    const int leaf = blockIdx.x * kBlock + threadIdx.x;
+    if (leaf >= n) return;
+    const uint32_t pr = order[leaf];
+    float lo[3], hi[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = down1(__double2float_rd(plo[3 * (size_t)pr + k]));
+        hi[k] = up1(__double2float_ru(phi[3 * (size_t)pr + k]));
+    }
+    uint32_t p = parent[(n - 1) + leaf];
+    for (int guard = 0; guard < 4096; ++guard) {  // bounded: a tree is never 4096 levels deep
+        const int node = (int)(p >> 1), side = (int)(p & 1u);
+        store_slot(nodes, node, side, lo, hi);
+        // release: every store of this lane is performed and written back past this XCD's L2
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t old = __hip_atomic_fetch_add(&flags[node], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == 0u) return;  // first arrival: the sibling's lane finishes this node
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        const float* q = reinterpret_cast<const float*>(nodes + node);
+        float b[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) b[k] = q[k];
+        lo[0] = fminf(b[0], b[6]);  lo[1] = fminf(b[1], b[7]);  lo[2] = fminf(b[2], b[8]);
+        hi[0] = fmaxf(b[3], b[9]);  hi[1] = fmaxf(b[4], b[10]); hi[2] = fmaxf(b[5], b[11]);
+        if (node == 0) return;
+        p = parent[node];
+    }
+}
+
+// depth of every leaf (root = depth 1 for its children); out = max
+__global__ __launch_bounds__(kBlock) void k_depth(const uint32_t* __restrict__ parent, int n, unsigned* __restrict__ out) {
+    const int leaf = blockIdx.x * kBlock + threadIdx.x;
+    if (leaf >= n) return;
+    unsigned d = 1;
+    uint32_t p = parent[(n - 1) + leaf];
+    while ((p >> 1) != 0u && d < 4096u) {
+        p = parent[p >> 1];
+        ++d;
+    }
+    atomicMax(out, d);
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_tris(const double* __restrict__ v, const uint32_t* __restrict__ f,
+                                                      const uint32_t* __restrict__ order, size_t T, uint32_t face_base,
+                                                      TriRec* __restrict__ out) {
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= T) return;
+    const uint32_t t = order[k];
+    TriRec r;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const size_t vi = f[3 * (size_t)t + c];
+        r.v[3 * c] = v[3 * vi];
+        r.v[3 * c + 1] = v[3 * vi + 1];
+        r.v[3 * c + 2] = v[3 * vi + 2];
+    }
+    r.face = t + face_base;
+    r.pad = 0;
+    out[k] = r;
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_points(const double* __restrict__ v, const uint32_t* __restrict__ order,
+                                                        size_t P, PtRec* __restrict__ out) {
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= P) return;
+    const uint32_t i = order[k];
+    PtRec r;
+    r.x = v[3 * (size_t)i];
+    r.y = v[3 * (size_t)i + 1];
+    r.z = v[3 * (size_t)i + 2];
+    r.idx = i;
+    r.pad = 0;
+    out[k] = r;
+}
+
+static unsigned nblocks(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+int tri_bounds(const double* d_v, const uint32_t* d_f, size_t T, double* d_lo, double* d_hi, hipStream_t s) {
+    k_tri_bounds<<<nblocks(T), kBlock, 0, s>>>(d_v, d_f, T, d_lo, d_hi);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+int point_bounds(const double* d_v, size_t P, double* d_lo, double* d_hi, hipStream_t s) {
+    k_point_bounds<<<nblocks(3 * P), kBlock, 0, s>>>(d_v, P, d_lo, d_hi);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+int pack_tri_leaves(const double* d_v, const uint32_t* d_f, const uint32_t* d_order, size_t T, uint32_t face_base,
+                    TriRec* d_out, hipStream_t s) {
+    k_pack_tris<<<nblocks(T), kBlock, 0, s>>>(d_v, d_f, d_order, T, face_base, d_out);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+int pack_point_leaves(const double* d_v, const uint32_t* d_order, size_t P, PtRec* d_out, hipStream_t s) {
+    k_pack_points<<<nblocks(P), kBlock, 0, s>>>(d_v, d_order, P, d_out);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T, uint32_t* d_order) {
+    hipStream_t s = tree->stream;
+    Workspace& ws = tree->ws;
+    if (T > (size_t)0x7FFFFFFF) {
+        set_error("LBVH build: %zu primitives exceed the 31-bit node index range", T);
+        return MSH_EINVAL;
+    }
+    // scene box
+    const unsigned rb = (unsigned)std::min<size_t>(1024, std::max<size_t>(1, (T + kBlock - 1) / kBlock));
+    MSH_TRY(ws.flags.reserve(std::max<size_t>((size_t)(rb + 1) * 6 * sizeof(double), T * sizeof(uint32_t) + 64)));
+    double* part = ws.flags.as<double>();
+    k_reduce_box<<<rb, kBlock, 0, s>>>(d_lo, d_hi, T, part);
+    MSH_HIP(hipGetLastError());
+    DevBuf box;  // released at the end of the build (after its final stream sync)
+    struct Rel { DevBuf& b; ~Rel() { b.release(); } } rel{box};
+    MSH_TRY(box.reserve(6 * sizeof(double)));
+    double* d_box = box.as<double>();
+    double box_h[6];
+    {
+        // at most 1024 partial boxes: fetch and combine them on the host (the build syncs anyway
+        // to learn the scene box used by query Morton codes)
+        std::unique_ptr<double[]> hp(new double[6 * rb]);
+        MSH_HIP(hipMemcpyAsync(hp.get(), part, 6 * rb * sizeof(double), hipMemcpyDeviceToHost, s));
+        MSH_HIP(hipStreamSynchronize(s));
+        for (int k = 0; k < 3; ++k) { box_h[k] = INFINITY; box_h[3 + k] = -INFINITY; }
+        for (unsigned b = 0; b < rb; ++b)
+            for (int k = 0; k < 3; ++k) {
+                box_h[k] = std::min(box_h[k], hp[6 * b + k]);
+                box_h[3 + k] = std::max(box_h[3 + k], hp[6 * b + 3 + k]);
+            }
+        MSH_HIP(hipMemcpyAsync(d_box, box_h, sizeof(box_h), hipMemcpyHostToDevice, s));
+    }
+    for (int k = 0; k < 3; ++k) {
+        tree->scene_lo[k] = (float)box_h[k];
+        tree->scene_hi[k] = (float)box_h[3 + k];
+    }
+    // Morton codes + sort
+    MSH_TRY(ws.keys.reserve(T * sizeof(uint32_t)));
+    MSH_TRY(ws.keys_alt.reserve(T * sizeof(uint32_t)));
+    MSH_TRY(ws.vals_alt.reserve(T * sizeof(uint32_t)));
+    uint32_t* keys = ws.keys.as<uint32_t>();
+    k_morton<<<nblocks(T), kBlock, 0, s>>>(d_lo, d_hi, T, d_box, keys, d_order);
+    MSH_HIP(hipGetLastError());
+    MSH_TRY(radix_sort_pairs(keys, d_order, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), T, 30, ws, s));
+    tree->max_depth = 0;
+    if (T < 2) {
+        MSH_HIP(hipStreamSynchronize(s));
+        return MSH_OK;
+    }
+    // Karras emission
+    MSH_TRY(ws.vals.reserve((2 * T - 1) * sizeof(uint32_t)));
+    uint32_t* parent = ws.vals.as<uint32_t>();
+    k_karras<<<nblocks(T - 1), kBlock, 0, s>>>(keys, (int)T, tree->d_nodes, parent);
+    MSH_HIP(hipGetLastError());
+    // refit
+    uint32_t* flags = ws.flags.as<uint32_t>();
+    MSH_HIP(hipMemsetAsync(flags, 0, T * sizeof(uint32_t) + 64, s));
+    k_refit<<<nblocks(T), kBlock, 0, s>>>(d_lo, d_hi, d_order, (int)T, tree->d_nodes, parent, flags);
+    MSH_HIP(hipGetLastError());
+    unsigned* d_depth = flags + T;
+    MSH_HIP(hipMemsetAsync(d_depth, 0, sizeof(unsigned), s));
+    k_depth<<<nblocks(T), kBlock, 0, s>>>(parent, (int)T, d_depth);
+    MSH_HIP(hipGetLastError());
+    unsigned depth = 0;
+    MSH_HIP(hipMemcpyAsync(&depth, d_depth, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    MSH_HIP(hipStreamSynchronize(s));
+    tree->max_depth = (int)depth;
+    return MSH_OK;
+}
+
+}  // namespace msh

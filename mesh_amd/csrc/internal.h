@@ -1,0 +1,121 @@
+// Host-side internals of libmeshsearch: the handle, device buffers, error plumbing and the kernel
+// launchers implemented in the .hip translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/meshsearch.h"
+#include "common.h"
+
+namespace msh {
+
+void set_error(const char* fmt, ...);
+
+#define MSH_HIP(expr)                                                                           \
+    do {                                                                                        \
+        hipError_t _e = (expr);                                                                 \
+        if (_e != hipSuccess) {                                                                 \
+            ::msh::set_error("HIP error %s at %s:%d: %s", hipGetErrorName(_e), __FILE__, __LINE__, #expr); \
+            return (_e == hipErrorOutOfMemory) ? MSH_ENOMEM : MSH_EDEVICE;                       \
+        }                                                                                       \
+    } while (0)
+
+#define MSH_TRY(expr)               \
+    do {                            \
+        int _s = (expr);            \
+        if (_s != MSH_OK) return _s; \
+    } while (0)
+
+// Grow-only device scratch buffer.
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    int reserve(size_t need);
+    void release();
+    template <class T>
+    T* as() const { return static_cast<T*>(ptr); }
+};
+
+// Reusable per-handle scratch (query keys / permutation / sort temporaries / results).
+struct Workspace {
+    DevBuf keys, vals, keys_alt, vals_alt, hist, scan, q, out_a, out_b, out_c, flags, counters, spill, stats;
+    void release();
+};
+
+enum Kind { kTriangles = 0, kNormals = 1, kPoints = 2 };
+
+}  // namespace msh
+
+struct msh_tree {
+    int device = 0;
+    int kind = msh::kTriangles;
+    double eps = 0.0;
+    size_t P = 0;        // main-mesh vertices
+    size_t T = 0;        // leaf primitives
+    size_t T_main = 0;   // main-mesh faces (visibility: extra faces follow)
+    double* d_v = nullptr;         // (P,3) main vertices (visibility sources)
+    msh::BNode* d_nodes = nullptr; // T-1 internal nodes (nullptr when T == 1)
+    void* d_leaves = nullptr;      // T TriRec or PtRec in Morton order
+    float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};  // bbox of all primitives
+    hipStream_t stream = nullptr;
+    double build_ms = 0.0;
+    int max_depth = 0;             // deepest leaf (root children = 1)
+    msh::Workspace ws;
+};
+
+namespace msh {
+
+// ---- radix sort (sort.hip): stable LSD sort of (u32 key, u32 value) pairs on the low `bits` bits.
+// Result ends in keys/vals (the alt buffers are temporaries).
+int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, size_t n, int bits,
+                     Workspace& ws, hipStream_t s);
+// exclusive scan of u32 (in place), n elements
+int exclusive_scan_u32(uint32_t* data, size_t n, Workspace& ws, hipStream_t s);
+
+// ---- LBVH build (build.hip) ----
+// prim_lo/prim_hi: (T,3) fp64 bounds per primitive on device.  Builds nodes and the Morton order
+// `order` (sorted position -> primitive id).  scene box written to tree.
+int build_lbvh(msh_tree* tree, const double* d_prim_lo, const double* d_prim_hi, size_t T, uint32_t* d_order);
+int tri_bounds(const double* d_v, const uint32_t* d_f, size_t T, double* d_lo, double* d_hi, hipStream_t s);
+int pack_tri_leaves(const double* d_v, const uint32_t* d_f, const uint32_t* d_order, size_t T, uint32_t face_base,
+                    TriRec* d_out, hipStream_t s);
+int pack_point_leaves(const double* d_v, const uint32_t* d_order, size_t P, PtRec* d_out, hipStream_t s);
+int point_bounds(const double* d_v, size_t P, double* d_lo, double* d_hi, hipStream_t s);
+
+// ---- queries (nearest.hip) ----
+// 30-bit Morton codes of query points in the tree's scene box + iota values.
+int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* keys, uint32_t* vals, hipStream_t s);
+int launch_nearest(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S, uint32_t* d_face,
+                   uint32_t* d_part, double* d_pt, hipStream_t s);
+int launch_nearest_stats(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S,
+                         unsigned long long* d_counts, hipStream_t s);
+int launch_nnearest(const msh_tree* tree, const double* d_q, const double* d_n, const uint32_t* d_perm, size_t S,
+                    uint32_t* d_face, double* d_pt, hipStream_t s);
+int launch_points_nearest(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S,
+                          uint32_t* d_idx, double* d_dist, hipStream_t s);
+
+// ---- rays (rays.hip) ----
+int launch_alongnormal(const msh_tree* tree, const double* d_p, const double* d_n, const uint32_t* d_perm, size_t S,
+                       double* d_dist, uint32_t* d_face, double* d_pt, hipStream_t s);
+int launch_visibility(const msh_tree* tree, const double* d_cams, size_t C, const double* d_normals,
+                      const double* d_sensors, double min_dist, uint32_t* d_vis, double* d_ndc, hipStream_t s);
+
+// ---- triangle-triangle (tritri.hip) ----
+// flags[i] = 1 iff query triangle i intersects any tree triangle (self: skip shared-vertex pairs and
+// the query triangles are the tree's own leaves in face order).
+int launch_tri_intersect(const msh_tree* tree, const TriRec* d_qtris, size_t Tq, int self_mode, uint32_t* d_flags,
+                         hipStream_t s);
+
+// ---- timing ----
+struct TimedLaunch {
+    const char* name;
+    hipStream_t s;
+    hipEvent_t a = nullptr, b = nullptr;
+    TimedLaunch(const char* n, hipStream_t st);
+    ~TimedLaunch();
+};
+
+}  // namespace msh

@@ -1,0 +1,204 @@
+"""ORACLE — test infrastructure only (see oracle.cpp header).
+
+ctypes wrapper around ``oracle/_build/liboracle.so``, the CPU restatement of CGAL 4.7's
+AABB-tree algorithms used by psbody-mesh (``mesh/src/spatialsearchmodule.cpp``,
+``aabb_normals.cpp``, ``visibility.cpp``).  Only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg import this module, and only as the checker / CPU baseline.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+
+_c_double_p = ctypes.POINTER(ctypes.c_double)
+_c_u32_p = ctypes.POINTER(ctypes.c_uint32)
+_c_u64_p = ctypes.POINTER(ctypes.c_uint64)
+_lib = None
+
+
+def build():
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        sz, vp, i = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
+        L.ora_point_triangle.restype = ctypes.c_double
+        L.ora_point_triangle.argtypes = [_c_double_p] * 5 + [_c_u32_p]
+        L.ora_cgal_tree_build.restype = vp
+        L.ora_cgal_tree_build.argtypes = [_c_double_p, sz, _c_u32_p, sz, i, ctypes.c_double]
+        L.ora_cgal_tree_free.argtypes = [vp]
+        L.ora_cgal_tree_free.restype = None
+        L.ora_cgal_tree_nearest.argtypes = [vp, _c_double_p, sz, _c_u32_p, _c_u32_p, _c_double_p, i, _c_u64_p]
+        L.ora_cgal_tree_nearest.restype = None
+        L.ora_cgal_ntree_nearest.argtypes = [vp, _c_double_p, _c_double_p, sz, _c_u32_p, _c_double_p, i]
+        L.ora_cgal_ntree_nearest.restype = None
+        L.ora_brute_nearest.argtypes = [_c_double_p, sz, _c_u32_p, sz, _c_double_p, sz, _c_u32_p, _c_u32_p,
+                                        _c_double_p, _c_double_p, i]
+        L.ora_brute_nearest.restype = None
+        L.ora_brute_nnearest.argtypes = [_c_double_p, sz, _c_u32_p, sz, ctypes.c_double, _c_double_p, _c_double_p, sz,
+                                         _c_u32_p, _c_double_p, _c_double_p, i]
+        L.ora_brute_nnearest.restype = None
+        L.ora_brute_alongnormal.argtypes = [_c_double_p, sz, _c_u32_p, sz, _c_double_p, _c_double_p, sz, _c_double_p,
+                                            _c_u32_p, _c_double_p, i]
+        L.ora_brute_alongnormal.restype = None
+        L.ora_brute_visibility.argtypes = [_c_double_p, sz, _c_double_p, sz, _c_double_p, sz, _c_double_p, _c_double_p,
+                                           ctypes.c_double, _c_u32_p, _c_double_p, i]
+        L.ora_brute_visibility.restype = None
+        L.ora_tri_tri_overlap.argtypes = [_c_double_p, _c_double_p]
+        L.ora_tri_tri_overlap.restype = i
+        L.ora_brute_intersections.argtypes = [_c_double_p, sz, _c_u32_p, sz, _c_double_p, sz, _c_u32_p, sz, _c_u32_p, i]
+        L.ora_brute_intersections.restype = sz
+        L.ora_brute_selfintersects.argtypes = [_c_double_p, sz, _c_u32_p, sz, i]
+        L.ora_brute_selfintersects.restype = ctypes.c_long
+        L.ora_brute_vertex_nn.argtypes = [_c_double_p, sz, _c_double_p, sz, _c_u32_p, _c_double_p, i]
+        L.ora_brute_vertex_nn.restype = None
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _u(a):
+    return np.ascontiguousarray(a, dtype=np.uint32)
+
+
+def _pd(a):
+    return a.ctypes.data_as(_c_double_p) if a is not None else None
+
+
+def _pu(a):
+    return a.ctypes.data_as(_c_u32_p) if a is not None else None
+
+
+def point_triangle(q, a, b, c):
+    """Closest point of triangle abc to q with CGAL's construction -> (point, part, d2)."""
+    q, a, b, c = _d(q), _d(a), _d(b), _d(c)
+    pt = np.empty(3)
+    part = np.zeros(1, np.uint32)
+    d2 = lib().ora_point_triangle(_pd(q), _pd(a), _pd(b), _pd(c), _pd(pt), _pu(part))
+    return pt, int(part[0]), d2
+
+
+class CgalTree(object):
+    """CGAL 4.7 AABB_tree restatement (median split, KD hint, left-first traversal)."""
+
+    def __init__(self, v, f, hint=True, eps=0.0):
+        self.v, self.f = _d(v), _u(f)
+        self.h = lib().ora_cgal_tree_build(_pd(self.v), self.v.shape[0], _pu(self.f), self.f.shape[0],
+                                           1 if hint else 0, float(eps))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().ora_cgal_tree_free(self.h)
+            self.h = None
+
+    def nearest(self, q, threads=0, count_visits=False):
+        q = _d(q).reshape(-1, 3)
+        S = q.shape[0]
+        face = np.empty(S, np.uint32)
+        part = np.empty(S, np.uint32)
+        pt = np.empty((S, 3))
+        visits = np.zeros(1, np.uint64)
+        lib().ora_cgal_tree_nearest(self.h, _pd(q), S, _pu(face), _pu(part), _pd(pt), int(threads),
+                                    visits.ctypes.data_as(_c_u64_p) if count_visits else None)
+        if count_visits:
+            return face, part, pt, int(visits[0])
+        return face, part, pt
+
+    def nnearest(self, q, n, threads=0):
+        q, n = _d(q).reshape(-1, 3), _d(n).reshape(-1, 3)
+        S = q.shape[0]
+        face = np.empty(S, np.uint32)
+        pt = np.empty((S, 3))
+        lib().ora_cgal_ntree_nearest(self.h, _pd(q), _pd(n), S, _pu(face), _pd(pt), int(threads))
+        return face, pt
+
+
+def brute_nearest(v, f, q, threads=0):
+    """Exhaustive closest point, lexicographic min (d2, face) -> (face, part, point, d2)."""
+    v, f, q = _d(v), _u(f), _d(q).reshape(-1, 3)
+    S = q.shape[0]
+    face = np.empty(S, np.uint32)
+    part = np.empty(S, np.uint32)
+    pt = np.empty((S, 3))
+    d2 = np.empty(S)
+    lib().ora_brute_nearest(_pd(v), v.shape[0], _pu(f), f.shape[0], _pd(q), S, _pu(face), _pu(part), _pd(pt), _pd(d2),
+                            int(threads))
+    return face, part, pt, d2
+
+
+def brute_nnearest(v, f, eps, q, n, threads=0):
+    v, f, q, n = _d(v), _u(f), _d(q).reshape(-1, 3), _d(n).reshape(-1, 3)
+    S = q.shape[0]
+    face = np.empty(S, np.uint32)
+    pt = np.empty((S, 3))
+    met = np.empty(S)
+    lib().ora_brute_nnearest(_pd(v), v.shape[0], _pu(f), f.shape[0], float(eps), _pd(q), _pd(n), S, _pu(face), _pd(pt),
+                             _pd(met), int(threads))
+    return face, pt, met
+
+
+def brute_alongnormal(v, f, p, n, threads=0):
+    v, f, p, n = _d(v), _u(f), _d(p).reshape(-1, 3), _d(n).reshape(-1, 3)
+    S = p.shape[0]
+    dist = np.empty(S)
+    face = np.empty(S, np.uint32)
+    pt = np.empty((S, 3))
+    lib().ora_brute_alongnormal(_pd(v), v.shape[0], _pu(f), f.shape[0], _pd(p), _pd(n), S, _pd(dist), _pu(face),
+                                _pd(pt), int(threads))
+    return dist, face, pt
+
+
+def brute_visibility(v, f, cams, n=None, sensors=None, extra_v=None, extra_f=None, min_dist=1e-3, threads=0):
+    v, f, cams = _d(v), _u(f), _d(cams).reshape(-1, 3)
+    tris = v[f.astype(np.int64)].reshape(-1, 9)
+    if extra_v is not None and extra_f is not None:
+        ev, ef = _d(extra_v), _u(extra_f)
+        tris = np.vstack([tris, ev[ef.astype(np.int64)].reshape(-1, 9)])
+    tris = _d(tris)
+    P, C = v.shape[0], cams.shape[0]
+    vis = np.empty((C, P), np.uint32)
+    ndc = np.empty((C, P))
+    nn = _d(n) if n is not None else None
+    ss = _d(sensors) if sensors is not None else None
+    lib().ora_brute_visibility(_pd(v), P, _pd(tris), tris.shape[0], _pd(cams), C, _pd(nn), _pd(ss), float(min_dist),
+                               _pu(vis), _pd(ndc), int(threads))
+    return vis, ndc
+
+
+def tri_tri_overlap(t1, t2):
+    t1, t2 = _d(t1).reshape(9), _d(t2).reshape(9)
+    return bool(lib().ora_tri_tri_overlap(_pd(t1), _pd(t2)))
+
+
+def brute_intersections(v, f, qv, qf, threads=0):
+    v, f, qv, qf = _d(v), _u(f), _d(qv), _u(qf)
+    out = np.empty(qf.shape[0], np.uint32)
+    K = lib().ora_brute_intersections(_pd(v), v.shape[0], _pu(f), f.shape[0], _pd(qv), qv.shape[0], _pu(qf),
+                                      qf.shape[0], _pu(out), int(threads))
+    return out[:K].copy()
+
+
+def brute_selfintersects(v, f, threads=0):
+    v, f = _d(v), _u(f)
+    return int(lib().ora_brute_selfintersects(_pd(v), v.shape[0], _pu(f), f.shape[0], int(threads)))
+
+
+def brute_vertex_nn(v, q, threads=0):
+    v, q = _d(v), _d(q).reshape(-1, 3)
+    S = q.shape[0]
+    idx = np.empty(S, np.uint32)
+    dist = np.empty(S)
+    lib().ora_brute_vertex_nn(_pd(v), v.shape[0], _pd(q), S, _pu(idx), _pd(dist), int(threads))
+    return idx, dist

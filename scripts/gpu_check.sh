@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU-box session: smoke -> pytest -m gpu -> bench (small + full) -> rocprofv3 kernel stats.
+# Every GPU step has its own time limit; after a crash/abort/timeout nothing further runs.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+ST=gpurun_out/status.txt
+: > $ST
+ok() {  # rc 0 = pass, 1 = test failures (no fault) -> continue; anything else -> stop
+  local name=$1 rc=$2
+  echo "$name rc=$rc" | tee -a $ST
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "STOP after $name" | tee -a $ST; exit $rc; fi
+}
+STAGES=${STAGES:-"smoke pytest bench prof"}
+for s in $STAGES; do
+  case $s in
+    smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; ok smoke $? ;;
+    pytest) timeout -k 10 1200 python -m pytest tests -q -m gpu -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; ok pytest $? ;;
+    bench_small) timeout -k 10 600 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_small.log 2>&1; ok bench_small $? ;;
+    bench)  timeout -k 10 900 python bench.py > gpurun_out/bench.log 2>&1; ok bench $? ;;
+    prof)   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 3 --warmup 1 --no-cpu > "$OLDPWD/gpurun_out/prof.log" 2>&1); ok prof $? ;;
+  esac
+done
+echo done | tee -a $ST

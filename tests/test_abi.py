@@ -1,0 +1,113 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports every symbol the header declares,
+the ctypes table matches the header, argument validation mirrors the reference's error surface, and
+the product path fails loudly (no CPU fallback) when no HIP device is usable."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "meshsearch.h")
+
+
+def header_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(msh_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_library_exports_every_header_symbol():
+    from mesh_amd import _native
+    L = ctypes.CDLL(_native.LIB_PATH)
+    syms = header_symbols()
+    assert len(syms) >= 25
+    missing = [s for s in syms if not hasattr(L, s)]
+    assert not missing, missing
+
+
+def test_ctypes_table_matches_header():
+    from mesh_amd import _native
+    assert sorted(n for n, _, _ in _native.SIGNATURES) == header_symbols()
+
+
+def test_library_is_gfx950_hip():
+    # the shared object carries an embedded gfx950 code object bundle
+    blob = open(os.path.join(ROOT, "mesh_amd", "lib", "libmeshsearch.so"), "rb").read()
+    assert b"gfx950" in blob
+    assert b"k_knn" in blob and b"k_karras" in blob and b"k_scatter" in blob
+
+
+def test_version_and_error_string():
+    from mesh_amd import _native
+    L = _native.lib()
+    assert L.msh_version() == 1
+    assert isinstance(L.msh_last_error(), bytes)
+
+
+def _no_gpu():
+    from mesh_amd import _native
+    return _native.device_count() == 0
+
+
+@pytest.mark.skipif(not _no_gpu(), reason="a HIP device is present")
+def test_no_device_fails_loudly(meshes):
+    from mesh_amd import spatialsearch
+    with pytest.raises(RuntimeError):
+        spatialsearch.aabbtree_compute(meshes["sphere_v"], meshes["sphere_f"])
+
+
+def test_validation_mirrors_reference(meshes):
+    from mesh_amd import _native, aabb_normals, spatialsearch, visibility
+    v, f = meshes["sphere_v"], meshes["sphere_f"]
+    with pytest.raises(ValueError, match="Vertices must be of type double, and 2 dimensional"):
+        spatialsearch.aabbtree_compute(v.astype(np.float32), f)
+    with pytest.raises(ValueError, match="Faces must be of type uint32, and 2 dimensional"):
+        spatialsearch.aabbtree_compute(v, f.astype(np.int64))
+    with pytest.raises(ValueError, match="Input must be Nx3"):
+        spatialsearch.aabbtree_compute(v[:, :2].copy(), f)
+    with pytest.raises(ValueError, match="Vertices must be of type double"):
+        aabb_normals.aabbtree_n_compute(v.astype(np.float32), f, 0.1)
+    fake = _native.Handle(1, "triangles")
+    fake_n = _native.Handle(1, "normals")
+    try:
+        with pytest.raises(ValueError, match="Input must be Nx3"):
+            spatialsearch.aabbtree_nearest(fake, np.zeros((4, 2)))
+        with pytest.raises(ValueError, match="Points and normals must be Nx3"):
+            spatialsearch.aabbtree_nearest_alongnormal(fake, np.zeros((4, 3)), np.zeros((5, 3)))
+        with pytest.raises(ValueError, match="Query Faces must be of type uint32"):
+            spatialsearch.aabbtree_intersections_indices(fake, np.zeros((3, 3)), np.zeros((1, 3), np.int32))
+        with pytest.raises(ValueError, match="First argument must be a NumPy array"):
+            aabb_normals.aabbtree_n_nearest(fake_n, [[0, 0, 0]], np.zeros((1, 3)))
+        with pytest.raises(ValueError, match="Normals should have same dimensions as points"):
+            aabb_normals.aabbtree_n_nearest(fake_n, np.zeros((2, 3)), np.zeros((3, 3)))
+        with pytest.raises(ValueError, match="Array must be of a specific type"):
+            visibility.visibility_compute(cams=np.zeros((1, 3)), v=v.astype(np.float32), f=f)
+    finally:
+        fake.ptr = None
+        fake_n.ptr = None
+    assert issubclass(spatialsearch.Mesh_IntersectionsError, Exception)
+    assert issubclass(visibility.VisibilityError, Exception)
+
+
+def test_null_handles_rejected():
+    from mesh_amd import _native
+    L = _native.lib()
+    face = np.zeros(1, np.uint32)
+    pt = np.zeros(3)
+    q = np.zeros(3)
+    assert L.msh_tree_nearest(None, _native.dptr(q), 1, _native.uptr(face), None, _native.dptr(pt)) == _native.MSH_EINVAL
+    assert b"null" in L.msh_last_error()
+    assert L.msh_tree_build(_native.dptr(q), 1, _native.uptr(face), 0, ctypes.byref(ctypes.c_void_p())) == \
+        _native.MSH_EINVAL  # empty mesh
+
+
+def test_bad_face_index_rejected_before_device():
+    from mesh_amd import _native
+    L = _native.lib()
+    v = np.zeros((3, 3))
+    f = np.array([[0, 1, 7]], np.uint32)
+    out = ctypes.c_void_p()
+    assert L.msh_tree_build(_native.dptr(v), 3, _native.uptr(f), 1, ctypes.byref(out)) == _native.MSH_EINVAL
+    assert b"references vertex 7" in L.msh_last_error()

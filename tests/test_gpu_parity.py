@@ -1,0 +1,369 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and the reference's known answers.
+
+Bar (BASELINE.json north_star): closest face identical except at equidistant ties
+(|Δd| <= 1e-9 x bbox diagonal), closest point within 1e-6 x bbox diagonal.  Against the exhaustive
+oracle with the same tie rule (lexicographic min of (d², face)) and the same CGAL construction, the
+HIP results are required to be BIT-EXACT (face, part code and point); against the CGAL-tree
+restatement (whose tie rule is traversal order) they are compared tie-tolerantly.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import workloads as W
+from tests.test_oracle import check_visibility_box, cylinder_query
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    from mesh_amd import _native
+    _native.set_device(0)
+
+
+def _nearest(v, f, q):
+    from mesh_amd import spatialsearch
+    t = spatialsearch.aabbtree_compute(np.ascontiguousarray(v, np.float64), np.ascontiguousarray(f, np.uint32))
+    face, part, pt = spatialsearch.aabbtree_nearest(t, np.ascontiguousarray(q, np.float64))
+    assert face.shape == (1, q.shape[0]) and face.dtype == np.uint32
+    assert part.shape == (1, q.shape[0]) and part.dtype == np.uint32
+    assert pt.shape == (q.shape[0], 3) and pt.dtype == np.float64
+    return face[0], part[0], pt
+
+
+def _assert_bit_exact_vs_brute(oracle, v, f, q):
+    face, part, pt = _nearest(v, f, q)
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q)
+    assert np.array_equal(face, bf), "faces differ at %s" % np.nonzero(face != bf)[0][:10]
+    assert np.array_equal(part, bp)
+    assert np.array_equal(pt, bpt)
+    return face, part, pt
+
+
+# ---------------------------------------------------------------- reference known answers
+def test_aabb_tree_known_answer(ref_tests):
+    from mesh_amd.mesh import Mesh
+    t = ref_tests["test_aabb_tree"]
+    m = Mesh(v=np.array(t["v"]), f=np.array(t["f"]))
+    f_est, v_est = m.compute_aabb_tree().nearest(np.array(t["q"]))
+    assert max(abs(f_est - np.array(t["f_expected"])).flatten()) < 1e-6
+    assert max(abs(v_est - np.array(t["v_expected"])).flatten()) < 1e-6
+
+
+@pytest.mark.parametrize("name", ["test_dist_classic", "test_dist_normals"])
+def test_normals_known_answer(meshes, ref_tests, name):
+    from mesh_amd import aabb_normals
+    t = ref_tests[name]
+    v, f = meshes[t["mesh"] + "_v"], meshes[t["mesh"] + "_f"]
+    h = aabb_normals.aabbtree_n_compute(v, f.astype(np.uint32).copy(), t["eps"])
+    tri, p = aabb_normals.aabbtree_n_nearest(h, np.array(t["q"]), np.array(t["n"]))
+    assert (tri == np.array(t["f_expected"])).all()
+    assert (p == np.array(t["p_expected"])).all()
+
+
+def test_cylinders_known_answer(meshes, ref_tests):
+    from mesh_amd import aabb_normals
+    t = ref_tests["test_cylinders"]
+    v, f = meshes["cylinder_v"], meshes["cylinder_f"]
+    q, qn = cylinder_query(meshes)
+    a, _ = aabb_normals.aabbtree_n_nearest(aabb_normals.aabbtree_n_compute(v, f, t["eps_no"]), q, qn)
+    b, _ = aabb_normals.aabbtree_n_nearest(aabb_normals.aabbtree_n_compute(v, f, t["eps_yes"]), q, qn)
+    assert np.unique(a).shape[0] <= t["max_unique_no"]
+    assert np.unique(b).shape[0] >= f.shape[0] - t["min_unique_yes_slack"]
+
+
+def test_selfintersects_known_answer(meshes, ref_tests):
+    from mesh_amd import aabb_normals
+    for name, want in ref_tests["test_selfintersects"].items():
+        h = aabb_normals.aabbtree_n_compute(meshes[name + "_v"], meshes[name + "_f"], 0.5)
+        assert aabb_normals.aabbtree_n_selfintersects(h) == want
+
+
+def test_visibility_known_answer(ref_tests):
+    from mesh_amd.visibility import visibility_compute
+    check_visibility_box(visibility_compute, ref_tests["test_visibility_box"])
+
+
+def test_intersections_known_answer(meshes, ref_tests):
+    from mesh_amd.mesh import Mesh
+    t = ref_tests["test_intersections"]
+    v, f = meshes["icosphere_v"], meshes["icosphere_f"]
+    qm = Mesh(v=v * t["radius"] + np.array(t["q_center"], float), f=f)
+    m = Mesh(v=v * t["radius"] + np.array(t["m_center"], float), f=f)
+    got = m.compute_aabb_tree().intersections_indices(qm.v, qm.f)
+    assert got.dtype == np.uint32 and got.tolist() == t["expected"]
+
+
+def test_closest_point_tree_vs_scipy_golden(meshes):
+    from mesh_amd.mesh import Mesh
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "kdtree.npz"))
+    m = Mesh(v=meshes["sphere_v"], f=meshes["sphere_f"])
+    idx, dist = m.closest_vertices(g["q"])
+    assert isinstance(idx, tuple) and len(idx) == g["q"].shape[0]
+    assert (np.array(idx) == g["idx"]).all()
+    assert np.allclose(np.array(dist), g["dist"], rtol=1e-12, atol=0)
+    nv = m.compute_closest_point_tree().nearest_vertices(g["q"][:10])
+    assert (nv == meshes["sphere_v"][g["idx"][:10]]).all()
+
+
+# ---------------------------------------------------------------- randomized parity
+def test_c1_sphere_bit_exact(oracle, meshes):
+    v, f = meshes["sphere_v"], meshes["sphere_f"]
+    q = W.c1_queries(100000)
+    face, part, pt = _assert_bit_exact_vs_brute(oracle, v, f, q)
+    cf, cp, cpt = oracle.CgalTree(v, f).nearest(q)
+    diag = float(np.linalg.norm(v.max(0) - v.min(0)))
+    same = face == cf
+    assert (pt[same] == cpt[same]).all() and (part[same] == cp[same]).all()
+    dg = np.linalg.norm(pt - q, axis=1)
+    dc = np.linalg.norm(cpt - q, axis=1)
+    assert np.all(np.abs(dg - dc) <= 1e-9 * diag)
+
+
+def test_c2_near_surface_bit_exact(oracle):
+    v, f = W.c2_mesh()
+    q, _ = W.surface_samples(v, f, 20000, seed=9, sigma=0.01)
+    q = np.vstack([q, v[:500], 0.5 * (v[f[:500, 0]] + v[f[:500, 1]])])  # vertex / edge ties
+    _assert_bit_exact_vs_brute(oracle, v, f, q)
+
+
+def test_c3_full_size_properties(oracle):
+    # BASELINE C3 mesh (1,003,520 faces) with 1M queries: size-independent properties on all queries,
+    # tie-tolerant parity against the CGAL-tree restatement on a 3000-query sample.
+    v, f = W.c3_mesh()
+    q = np.random.default_rng(3).uniform(-1.1, 1.1, (1_000_000, 3))
+    face, part, pt = _nearest(v, f, q)
+    assert face.max() < f.shape[0] and part.max() <= 6
+    tri = v[f[face].astype(np.int64)]
+    # every returned point is the CGAL construction for its face
+    for i in np.random.default_rng(1).choice(q.shape[0], 300, replace=False):
+        p, pp, _ = oracle.point_triangle(q[i], tri[i, 0], tri[i, 1], tri[i, 2])
+        assert (p == pt[i]).all() and pp == part[i]
+    idx = np.random.default_rng(2).choice(q.shape[0], 3000, replace=False)
+    cf, _, cpt = oracle.CgalTree(v, f).nearest(q[idx])
+    diag = float(np.linalg.norm(v.max(0) - v.min(0)))
+    dg = np.linalg.norm(pt[idx] - q[idx], axis=1)
+    dc = np.linalg.norm(cpt - q[idx], axis=1)
+    assert np.all(np.abs(dg - dc) <= 1e-9 * diag)
+    same = face[idx] == cf
+    assert same.mean() > 0.99 and np.all(np.abs(pt[idx][same] - cpt[same]) <= 1e-6 * diag)
+
+
+def test_normals_random_bit_exact(oracle):
+    from mesh_amd import aabb_normals
+    v, f = W.c2_mesh()
+    q, fi = W.surface_samples(v, f, 5000, seed=11, sigma=0.02)
+    n = np.random.default_rng(12).normal(size=q.shape)
+    n /= np.linalg.norm(n, axis=1)[:, None]
+    for eps in [0.0, 0.1, 2.0]:
+        h = aabb_normals.aabbtree_n_compute(v, f, eps)
+        face, pt = aabb_normals.aabbtree_n_nearest(h, q, n)
+        bf, bpt, _ = oracle.brute_nnearest(v, f, eps, q, n)
+        assert np.array_equal(face[0], bf), eps
+        assert np.array_equal(pt, bpt), eps
+
+
+def test_alongnormal_bit_exact(oracle):
+    from mesh_amd.search import AabbTree
+    from mesh_amd.mesh import Mesh
+    v, f = W.c2_mesh()
+    p, fi = W.surface_samples(v, f, 5000, seed=13, sigma=0.01)
+    tri = v[f[fi].astype(np.int64)]
+    n = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
+    n /= np.linalg.norm(n, axis=1)[:, None]
+    # add rays that miss everything
+    p = np.vstack([p, [[5.0, 5.0, 5.0]] * 3])
+    n = np.vstack([n, [[1.0, 0, 0]] * 3])
+    d, face, pt = AabbTree(Mesh(v=v, f=f)).nearest_alongnormal(p, n)
+    bd, bf, bpt = oracle.brute_alongnormal(v, f, p, n)
+    assert d.shape == (p.shape[0],) and face.dtype == np.uint32
+    assert np.array_equal(d, bd)
+    assert np.array_equal(face, bf)
+    hit = bd < 1e100
+    assert np.array_equal(pt[hit], bpt[hit])
+    assert (d[~hit] == 1e100).all() and (face[~hit] == 0xFFFFFFFF).all() and np.isnan(pt[~hit]).all()
+
+
+def test_visibility_random_exact(oracle):
+    from mesh_amd.visibility import visibility_compute
+    v, f = W.geodesic_icosphere(12)
+    th = np.arccos(np.clip(v[:, 2], -1, 1))
+    ph = np.arctan2(v[:, 1], v[:, 0])
+    v = v * (1 + 0.1 * np.sin(5 * th) * np.sin(4 * ph))[:, None]  # C5-style bumps: self-occlusion
+    from mesh_amd.mesh import Mesh
+    n = Mesh(v=v, f=f).estimate_vertex_normals()
+    cams = W.uniform_in_box([-3, -3, -3], [3, 3, 3], 6, seed=14, margin=0)
+    sens = np.random.default_rng(15).normal(size=(6, 9))
+    for kw in [dict(), dict(n=n), dict(n=n, sensors=sens), dict(min_dist=0.05)]:
+        vis, ndc = visibility_compute(cams=cams, v=v, f=f, **kw)
+        bv, bn = oracle.brute_visibility(v, f, cams, **kw)
+        assert np.array_equal(vis, bv), kw
+        assert np.array_equal(ndc, bn), kw
+        assert 0 < vis.mean() < 1
+
+
+def test_visibility_borrowed_tree():
+    from mesh_amd import spatialsearch
+    from mesh_amd.visibility import visibility_compute
+    v, f = W.geodesic_icosphere(4)
+    t = spatialsearch.aabbtree_compute(v, f)
+    a, _ = visibility_compute(cams=np.array([[0, 0, 3.0]]), tree=t)
+    b, _ = visibility_compute(cams=np.array([[0, 0, 3.0]]), v=v, f=f)
+    assert np.array_equal(a, b)
+    # the borrowed handle is still usable (reference double-frees it, py_visibility.cpp:212)
+    spatialsearch.aabbtree_nearest(t, np.zeros((2, 3)))
+
+
+def test_intersections_random(oracle):
+    from mesh_amd import spatialsearch
+    v, f = W.geodesic_icosphere(6)
+    rng = np.random.default_rng(16)
+    for shift in [0.3, 1.0, 1.9, 3.0]:
+        qv = v * 0.8 + np.array([shift, 0.1, -0.05])
+        t = spatialsearch.aabbtree_compute(v, f)
+        got = spatialsearch.aabbtree_intersections_indices(t, qv, f)
+        want = oracle.brute_intersections(v, f, qv, f)
+        assert np.array_equal(got, want), shift
+    # random triangle soup
+    qv = rng.normal(size=(300, 3))
+    qf = np.arange(300, dtype=np.uint32).reshape(-1, 3)
+    got = spatialsearch.aabbtree_intersections_indices(spatialsearch.aabbtree_compute(v, f), qv, qf)
+    assert np.array_equal(got, oracle.brute_intersections(v, f, qv, qf))
+
+
+def test_selfintersects_random(oracle):
+    from mesh_amd import aabb_normals
+    rng = np.random.default_rng(17)
+    v = rng.normal(size=(600, 3))
+    f = np.arange(600, dtype=np.uint32).reshape(-1, 3)
+    f2 = np.vstack([f, np.array([[0, 1, 5], [3, 4, 200]], np.uint32)])  # shared-vertex pairs are skipped
+    for ff in [f, f2]:
+        h = aabb_normals.aabbtree_n_compute(v, ff, 0.1)
+        assert aabb_normals.aabbtree_n_selfintersects(h) == oracle.brute_selfintersects(v, ff)
+
+
+def test_points_random_exact(oracle):
+    from mesh_amd.search import ClosestPointTree
+    from mesh_amd.mesh import Mesh
+    v, f = W.c2_mesh()
+    q = W.uniform_in_box(v.min(0), v.max(0), 50000, seed=18)
+    idx, dist = ClosestPointTree(Mesh(v=v, f=f)).nearest(q)
+    bi, bd = oracle.brute_vertex_nn(v, q)
+    assert np.array_equal(np.array(idx), bi)
+    assert np.array_equal(np.array(dist), bd)
+
+
+def test_cgal_closest_point_tree(meshes, oracle):
+    from mesh_amd.mesh import Mesh
+    v = meshes["sphere_v"]
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "kdtree.npz"))
+    m = Mesh(v=v, f=meshes["sphere_f"])
+    fi, d = m.closest_vertices(g["q"], use_cgal=True)
+    assert np.array_equal(fi, g["idx"].astype(np.uint32))
+    assert np.allclose(d, g["dist"], rtol=1e-9)
+
+
+# ---------------------------------------------------------------- edge cases
+def test_empty_queries():
+    from mesh_amd import spatialsearch
+    v, f = W.geodesic_icosphere(2)
+    t = spatialsearch.aabbtree_compute(v, f)
+    face, part, pt = spatialsearch.aabbtree_nearest(t, np.zeros((0, 3)))
+    assert face.shape == (1, 0) and pt.shape == (0, 3)
+    d, fc, p = spatialsearch.aabbtree_nearest_alongnormal(t, np.zeros((0, 3)), np.zeros((0, 3)))
+    assert d.shape == (0,)
+
+
+def test_empty_mesh_rejected():
+    from mesh_amd import spatialsearch
+    with pytest.raises(ValueError):
+        spatialsearch.aabbtree_compute(np.zeros((3, 3)), np.zeros((0, 3), np.uint32))
+
+
+@pytest.mark.parametrize("T", [1, 2, 3, 5])
+def test_tiny_meshes(oracle, T):
+    rng = np.random.default_rng(T)
+    v = rng.normal(size=(3 * T, 3))
+    f = np.arange(3 * T, dtype=np.uint32).reshape(-1, 3)
+    _assert_bit_exact_vs_brute(oracle, v, f, rng.normal(size=(5000, 3)) * 2)
+
+
+def test_duplicate_and_degenerate_triangles(oracle):
+    # coincident centroids (duplicate Morton codes) and zero-area triangles
+    v, f = W.geodesic_icosphere(5)
+    f = np.vstack([f, f[:50], f[:50, [1, 2, 0]]])
+    extra = np.array([[0.1, 0.1, 0.1], [0.2, 0.2, 0.2], [0.3, 0.3, 0.3]])  # collinear
+    v2 = np.vstack([v, extra])
+    P = v.shape[0]
+    f = np.vstack([f, [[P, P + 1, P + 2], [P, P, P + 1]]]).astype(np.uint32)
+    q = W.uniform_in_box([-1, -1, -1], [1, 1, 1], 20000, seed=19)
+    _assert_bit_exact_vs_brute(oracle, v2, f, q)
+
+
+def test_far_and_offset_queries(oracle):
+    v, f = W.geodesic_icosphere(8)
+    off = np.array([1e6, -2e6, 3e5])
+    q = np.vstack([W.uniform_in_box([-1, -1, -1], [1, 1, 1], 5000, seed=20) * 1e4,
+                   W.uniform_in_box([-1, -1, -1], [1, 1, 1], 5000, seed=21)])
+    _assert_bit_exact_vs_brute(oracle, v, f, q)
+    _assert_bit_exact_vs_brute(oracle, v + off, f, q + off)
+
+
+def test_queries_on_vertices_and_edges(oracle):
+    v, f = W.geodesic_icosphere(10)
+    e = 0.5 * (v[f[:, 0]] + v[f[:, 1]])
+    q = np.vstack([v, e, np.zeros((1, 3))])  # the centre is equidistant-ish from everything
+    _assert_bit_exact_vs_brute(oracle, v, f, q)
+
+
+def test_deep_tree_spill_path(oracle):
+    # a mesh whose LBVH is deeper than the 16-entry LDS stack (clustered + spread triangles)
+    rng = np.random.default_rng(22)
+    pts = np.vstack([rng.normal(size=(3000, 3)) * 1e-4, rng.normal(size=(3000, 3)) * 100])
+    v = np.repeat(pts, 3, axis=0) + rng.normal(size=(18000, 3)) * 1e-6
+    f = np.arange(18000, dtype=np.uint32).reshape(-1, 3)
+    from mesh_amd import spatialsearch
+    t = spatialsearch.aabbtree_compute(v, f)
+    q = rng.normal(size=(20000, 3)) * 50
+    face, part, pt = spatialsearch.aabbtree_nearest(t, q)
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q)
+    assert np.array_equal(face[0], bf) and np.array_equal(pt, bpt)
+
+
+def test_build_deterministic_and_blob_roundtrip(oracle):
+    import torch
+    from mesh_amd import _native, spatialsearch
+    v, f = W.c2_mesh()
+    q = W.uniform_in_box(v.min(0), v.max(0), 30000, seed=23)
+    t1 = spatialsearch.aabbtree_compute(v, f)
+    t2 = spatialsearch.aabbtree_compute(v, f)
+    r1 = spatialsearch.aabbtree_nearest(t1, q)
+    r2 = spatialsearch.aabbtree_nearest(t2, q)
+    assert all(np.array_equal(a, b) for a, b in zip(r1, r2))
+    n = _native.blob_size(t1)
+    blob = torch.empty(n, dtype=torch.uint8, device="cuda:0")
+    _native.blob_pack(t1, blob.data_ptr())
+    t3 = _native.blob_unpack(blob.data_ptr(), n, 0)
+    r3 = spatialsearch.aabbtree_nearest(t3, q)
+    assert all(np.array_equal(a, b) for a, b in zip(r1, r3))
+
+
+def test_device_api_matches_host_api():
+    import torch
+    from mesh_amd import spatialsearch
+    from mesh_amd.distributed import nearest_device
+    v, f = W.c2_mesh()
+    q = W.uniform_in_box(v.min(0), v.max(0), 100000, seed=24)
+    t = spatialsearch.aabbtree_compute(v, f)
+    face, part, pt = spatialsearch.aabbtree_nearest(t, q)
+    dq = torch.from_numpy(q).cuda()
+    df = torch.empty(q.shape[0], dtype=torch.int32, device="cuda")
+    dp = torch.empty(q.shape[0], dtype=torch.int32, device="cuda")
+    dpt = torch.empty((q.shape[0], 3), dtype=torch.float64, device="cuda")
+    nearest_device(t, dq, df, dp, dpt)
+    torch.cuda.synchronize()
+    assert np.array_equal(df.cpu().numpy().view(np.uint32), face[0])
+    assert np.array_equal(dp.cpu().numpy().view(np.uint32), part[0])
+    assert np.array_equal(dpt.cpu().numpy(), pt)

@@ -1,0 +1,173 @@
+"""The oracle (CPU restatement of CGAL 4.7's algorithms) pinned against the reference's own known
+answers and against scipy (ClosestPointTree's third-party arithmetic).  CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+import workloads as W
+
+
+def test_aabb_tree_known_answer(oracle, ref_tests):
+    # tests/test_mesh.py:89-109
+    t = ref_tests["test_aabb_tree"]
+    v, f, q = np.array(t["v"], float), np.array(t["f"]), np.array(t["q"], float)
+    for face, part, pt in [oracle.CgalTree(v, f).nearest(q), oracle.brute_nearest(v, f, q)[:3]]:
+        assert np.max(np.abs(face.astype(int) - np.array(t["f_expected"]))) < 1e-6
+        assert np.max(np.abs(pt - np.array(t["v_expected"]))) < t["tol"]
+
+
+@pytest.mark.parametrize("name", ["test_dist_classic", "test_dist_normals"])
+def test_normals_known_answer(oracle, meshes, ref_tests, name):
+    # tests/test_aabb_n_tree.py:29-52 — exact equality of fp64 points
+    t = ref_tests[name]
+    v, f = meshes[t["mesh"] + "_v"], meshes[t["mesh"] + "_f"]
+    face, pt = oracle.CgalTree(v, f, hint=False, eps=t["eps"]).nnearest(t["q"], t["n"])
+    assert (face[None, :] == np.array(t["f_expected"])).all()
+    assert (pt == np.array(t["p_expected"])).all()
+    bface, bpt, _ = oracle.brute_nnearest(v, f, t["eps"], t["q"], t["n"])
+    assert (bface == face).all() and (bpt == pt).all()
+
+
+def _tri_normals(v, f):
+    a, b, c = v[f[:, 0]], v[f[:, 1]], v[f[:, 2]]
+    n = np.cross(b - a, c - a)
+    return n / np.linalg.norm(n, axis=1)[:, None]
+
+
+def cylinder_query(meshes):
+    tv, tf = meshes["cylinder_trans_v"], meshes["cylinder_trans_f"]
+    tn = _tri_normals(tv, tf)
+    qn = np.zeros(tv.shape)
+    for i in range(tf.shape[0]):
+        qn[tf[i]] += tn[i]
+    return tv, qn / np.linalg.norm(qn, axis=1)[:, None]
+
+
+def test_cylinders_known_answer(oracle, meshes, ref_tests):
+    # tests/test_aabb_n_tree.py:54-76
+    t = ref_tests["test_cylinders"]
+    v, f = meshes["cylinder_v"], meshes["cylinder_f"]
+    q, qn = cylinder_query(meshes)
+    a, _ = oracle.CgalTree(v, f, hint=False, eps=t["eps_no"]).nnearest(q, qn)
+    b, _ = oracle.CgalTree(v, f, hint=False, eps=t["eps_yes"]).nnearest(q, qn)
+    assert np.unique(a).shape[0] <= t["max_unique_no"]
+    assert np.unique(b).shape[0] >= f.shape[0] - t["min_unique_yes_slack"]
+
+
+def test_selfintersects_known_answer(oracle, meshes, ref_tests):
+    # tests/test_aabb_n_tree.py:78-89
+    for name, want in ref_tests["test_selfintersects"].items():
+        assert oracle.brute_selfintersects(meshes[name + "_v"], meshes[name + "_f"]) == want
+
+
+def test_intersections_known_answer(oracle, meshes, ref_tests):
+    # tests/test_intersections.py:27 (disabled in the reference)
+    t = ref_tests["test_intersections"]
+    v, f = meshes["icosphere_v"], meshes["icosphere_f"]
+    qv = v * t["radius"] + np.array(t["q_center"], float)
+    mv = v * t["radius"] + np.array(t["m_center"], float)
+    assert oracle.brute_intersections(mv, f, qv, f).tolist() == t["expected"]
+
+
+def visibility_cases(t):
+    v = np.array(t["v"])
+    f = np.array(t["f1"], dtype=np.uint32) - 1
+    ve = np.array(t["vextra"])
+    fe = np.array(t["fextra1"], dtype=np.uint32) - 1
+    n = v / np.linalg.norm(v[0])
+    return v, f, ve, fe, n
+
+
+def check_visibility_box(vis_fn, t):
+    """The five asserts of tests/test_visibility.py:13-53 against a visibility_compute-like callable."""
+    v, f, ve, fe, n = visibility_cases(t)
+    vis, _ = vis_fn(v=v, f=f, cams=np.array([[1.0, 0.0, 0.0]]))
+    assert ((v.T[0] > 0) == vis).all()
+    vis, ndc = vis_fn(v=v, f=f, n=n, cams=np.array([[1e10, 0.0, 0.0]]))
+    assert ((v.T[0] > 0) == np.logical_and(vis, ndc > .5)).all()
+    vis, _ = vis_fn(v=v, f=f, cams=np.array([[0.0, 1.0, 0.0], [0.0, 0.0, 1.0]]))
+    assert ((v.T[1:3] > 0) == vis).all()
+    vis, _ = vis_fn(v=v, f=f, cams=np.array([[0.0, 0.0, 10.0]]), extra_v=ve, extra_f=fe)
+    assert (np.zeros_like(v.T[0]) == vis).all()
+    vis, _ = vis_fn(v=v, f=f, cams=np.array([[0.0, 0.0, 10.0]]), extra_v=ve, extra_f=fe, min_dist=1.0)
+    assert ((v.T[2] > 0) == vis).all()
+
+
+def test_visibility_known_answer(oracle, ref_tests):
+    t = ref_tests["test_visibility_box"]
+
+    def fn(v, f, cams, n=None, extra_v=None, extra_f=None, min_dist=1e-3):
+        return oracle.brute_visibility(v, f, cams, n=n, extra_v=extra_v, extra_f=extra_f, min_dist=min_dist)
+
+    check_visibility_box(fn, t)
+
+
+def _tie_tolerant(oracle, v, f, q, face_a, pt_a, face_b, pt_b):
+    diag = float(np.linalg.norm(v.max(0) - v.min(0)))
+    tri = v[f.astype(np.int64)]
+    da = np.sum((pt_a - q) ** 2, axis=1) ** 0.5
+    db = np.sum((pt_b - q) ** 2, axis=1) ** 0.5
+    same = face_a == face_b
+    # identical face: identical construction
+    assert (pt_a[same] == pt_b[same]).all()
+    # different face: must be an equidistant tie (north_star: |d| <= 1e-9 diag)
+    assert np.all(np.abs(da[~same] - db[~same]) <= 1e-9 * diag)
+    return int((~same).sum())
+
+
+def test_cgal_tree_vs_brute_sphere(oracle, meshes):
+    v, f = meshes["sphere_v"], meshes["sphere_f"]
+    q = W.uniform_in_box(v.min(0), v.max(0), 20000, seed=5)
+    cf, cp, cpt = oracle.CgalTree(v, f).nearest(q)
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q)
+    _tie_tolerant(oracle, v, f, q, cf, cpt, bf, bpt)
+    assert (cp[cf == bf] == bp[cf == bf]).all()
+
+
+def test_cgal_tree_vs_brute_on_surface(oracle):
+    # queries close to the surface (C2-like), plus exact vertices and edge midpoints (tie-heavy)
+    v, f = W.c2_mesh()
+    q, _ = W.surface_samples(v, f, 5000, seed=7, sigma=0.005)
+    e = 0.5 * (v[f[:200, 0]] + v[f[:200, 1]])
+    q = np.vstack([q, v[:300], e])
+    cf, _, cpt = oracle.CgalTree(v, f).nearest(q)
+    bf, _, bpt, _ = oracle.brute_nearest(v, f, q)
+    ties = _tie_tolerant(oracle, v, f, q, cf, cpt, bf, bpt)
+    assert ties > 0  # vertices / edge midpoints are shared by several faces
+
+
+def test_kdtree_golden(oracle, meshes):
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "kdtree.npz"))
+    idx, dist = oracle.brute_vertex_nn(meshes["sphere_v"], g["q"])
+    assert (idx == g["idx"]).all()
+    assert np.allclose(dist, g["dist"], rtol=1e-12, atol=0)
+
+
+def test_part_codes(oracle):
+    a, b, c = np.array([0., 0, 0]), np.array([1., 0, 0]), np.array([0., 1, 0])
+    cases = {(0.2, 0.2, 1.0): 0, (0.5, -1.0, 0.3): 1, (1.0, 1.0, -2.0): 2, (-1.0, 0.5, 0.0): 3,
+             (-1.0, -1.0, 0.5): 4, (2.0, -0.5, 0.0): 5, (-0.5, 2.0, 1.0): 6}
+    for q, want in cases.items():
+        pt, part, _ = oracle.point_triangle(q, a, b, c)
+        assert part == want, (q, part, want)
+
+
+def test_degenerate_triangle(oracle):
+    # zero-area triangle: nearest point over its closed edges (deliberate; CGAL yields NaN)
+    a, b, c = np.array([0., 0, 0]), np.array([1., 0, 0]), np.array([2., 0, 0])
+    pt, part, d2 = oracle.point_triangle([0.5, 1.0, 0.0], a, b, c)
+    assert np.allclose(pt, [0.5, 0, 0]) and d2 == 1.0 and part in (1, 3)
+    pt, part, d2 = oracle.point_triangle([3.0, 0.0, 0.0], a, b, c)
+    assert (pt == c).all() and part == 6
+
+
+def test_tri_tri_symmetric(oracle):
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        t1, t2 = rng.normal(size=9), rng.normal(size=9)
+        assert oracle.tri_tri_overlap(t1, t2) == oracle.tri_tri_overlap(t2, t1)
+    # shared vertex touches, coplanar overlap, disjoint
+    assert oracle.tri_tri_overlap([0, 0, 0, 1, 0, 0, 0, 1, 0], [0, 0, 0, -1, 0, 0, 0, 0, 1])
+    assert oracle.tri_tri_overlap([0, 0, 0, 2, 0, 0, 0, 2, 0], [0.5, 0.5, 0, 3, 0.5, 0, 0.5, 3, 0])
+    assert not oracle.tri_tri_overlap([0, 0, 0, 1, 0, 0, 0, 1, 0], [0, 0, 1, 1, 0, 1, 0, 1, 1])
