@@ -63,6 +63,31 @@ class TreeInfo(ctypes.Structure):
                 ("build_ms", ctypes.c_double)]
 
 
+def _preload_single_hip_runtime():
+    """Keep ONE HIP runtime per process.
+
+    PyTorch-ROCm ships its own libamdhip64.so (SONAME libamdhip64.so.7, like /opt/rocm's).  If
+    libmeshsearch pulled in /opt/rocm's copy first, a later `import torch` would load a second runtime
+    that then fails to initialise ("No HIP GPUs are available").  Loading torch's copy first (without
+    importing torch) makes our NEEDED libamdhip64.so.7 resolve to it, so torch and libmeshsearch share
+    the runtime, streams and device memory whatever the import order.
+    """
+    if os.environ.get("MESH_AMD_SYSTEM_HIP"):
+        return
+    try:
+        import importlib.util
+        spec = importlib.util.find_spec("torch")
+        if spec is None or not spec.submodule_search_locations:
+            return
+        for d in spec.submodule_search_locations:
+            p = os.path.join(d, "lib", "libamdhip64.so")
+            if os.path.exists(p):
+                ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+                return
+    except OSError:
+        pass
+
+
 def lib():
     """Load libmeshsearch.so (raises ImportError if it is missing — no fallback)."""
     global _lib
@@ -72,6 +97,7 @@ def lib():
                 if not os.path.exists(LIB_PATH):
                     raise ImportError("libmeshsearch.so not built (%s): run `python -c 'import __graft_entry__ as g; "
                                       "g.build()'` or `make -C mesh_amd/csrc`" % LIB_PATH)
+                _preload_single_hip_runtime()
                 L = ctypes.CDLL(LIB_PATH)
                 for name, res, args in SIGNATURES:
                     fn = getattr(L, name)

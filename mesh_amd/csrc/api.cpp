@@ -54,7 +54,7 @@ void DevBuf::release() {
 
 void Workspace::release() {
     DevBuf* all[] = {&keys, &vals, &keys_alt, &vals_alt, &hist, &scan, &q, &out_a, &out_b, &out_c,
-                     &flags, &counters, &spill, &stats};
+                     &flags, &counters, &spill, &stats, &ranges};
     for (DevBuf* b : all) b->release();
 }
 
@@ -193,6 +193,7 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
         if ((st = pack_tri_leaves(t->d_v, dF.as<uint32_t>(), dOrder.as<uint32_t>(), T, 0u,
                                   static_cast<TriRec*>(t->d_leaves), s)) != MSH_OK)
             break;
+        if ((st = build_obb(t, true)) != MSH_OK) break;
         (void)hipEventRecord(e1, s);
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) { set_error("LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
@@ -202,6 +203,7 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
     } while (0);
     (void)hipStreamSynchronize(s);
     dF.release(); dLo.release(); dHi.release(); dOrder.release();
+    t->ws.release();  // build scratch (sort buffers, parents, ranges) is not needed by queries
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return st;
@@ -347,11 +349,13 @@ int msh_points_build(const double* v, size_t P, msh_tree** out) {
         if ((st = build_lbvh(t, dLo.as<double>(), dHi.as<double>(), P, dOrder.as<uint32_t>())) != MSH_OK) break;
         if ((st = pack_point_leaves(t->d_v, dOrder.as<uint32_t>(), P, static_cast<PtRec*>(t->d_leaves), s)) != MSH_OK)
             break;
+        if ((st = build_obb(t, false)) != MSH_OK) break;
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) { set_error("point LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
     } while (0);
     (void)hipStreamSynchronize(s);
     dLo.release(); dHi.release(); dOrder.release();
+    t->ws.release();
     if (st != MSH_OK) {
         std::string keep = g_err;
         free_tree(t);
@@ -625,8 +629,9 @@ struct BlobHeader {
     double eps;
     float scene_lo[3], scene_hi[3];
     uint64_t off_v, off_nodes, off_leaves, total;
+    double origin[3];
 };
-static const uint64_t kBlobMagic = 0x4d53484c42564831ull;  // "MSHLBVH1"
+static const uint64_t kBlobMagic = 0x4d53484c42564832ull;  // "MSHLBVH2"
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -644,6 +649,7 @@ static void blob_layout(const msh_tree* t, BlobHeader& h) {
     for (int k = 0; k < 3; ++k) {
         h.scene_lo[k] = t->scene_lo[k];
         h.scene_hi[k] = t->scene_hi[k];
+        h.origin[k] = t->origin[k];
     }
     const size_t leaf = t->kind == kPoints ? sizeof(PtRec) : sizeof(TriRec);
     h.off_v = align256(sizeof(BlobHeader));
@@ -703,6 +709,7 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
     for (int k = 0; k < 3; ++k) {
         t->scene_lo[k] = h.scene_lo[k];
         t->scene_hi[k] = h.scene_hi[k];
+        t->origin[k] = h.origin[k];
     }
     const char* src = static_cast<const char*>(d_src);
     const size_t leaf = h.kind == kPoints ? sizeof(PtRec) : sizeof(TriRec);

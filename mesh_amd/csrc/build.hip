@@ -2,17 +2,22 @@
 // spatialsearchmodule.cpp:122, and accelerate_distance_queries' KD hint, :123).
 //
 //   1. k_tri_bounds / k_point_bounds   fp64 bounds of every primitive
-//   2. k_reduce_box (2 stages)         scene box (fp64)
+//   2. k_reduce_box                    scene box (fp64); origin = its centre (fp32 bounds are relative
+//                                      to it, so meshes far from (0,0,0) keep full fp32 precision)
 //   3. k_morton                        30-bit Morton code of each primitive's box centre
-//   4. radix_sort_pairs (sort.hip)     stable sort (key, primitive id): duplicate codes keep id order
+//   4. radix_sort_pairs (sort.hip)     stable LDS radix sort (key, primitive id): equal codes keep id order
 //   5. k_karras                        Karras (HPG 2012) internal-node emission; codes made unique by
-//                                      augmenting them with the sorted position
+//                                      augmenting them with the sorted position; also records each
+//                                      node's contiguous leaf range and split
 //   6. k_refit                         bottom-up AABB refit, one lane per leaf, the second arrival at
 //                                      each node continues upward (agent-scope release/acquire hand-off,
 //                                      cdna_hip_programming.md §6 Guideline 16)
 //   7. k_depth                         max leaf depth (sizes the traversal stack spill)
-// Node boxes are fp32 rounded outward (round-down lo / round-up hi, then one more ulp) so every
-// fp64 primitive lies strictly inside the box of every ancestor.
+//   8. (after leaf packing) k_obb      one wave per node over its Morton leaf range: area-weighted
+//                                      normal -> node frame (n, t, b = n x t), then both children's vertex
+//                                      extents along the frame (oriented boxes, thin along the surface)
+// All fp32 bounds are rounded outward (round-down lo / round-up hi, then one more ulp), so every fp64
+// primitive lies inside the bounds of every ancestor.
 #include <algorithm>
 #include <memory>
 
@@ -101,8 +106,9 @@ __device__ inline int lbvh_delta(const uint32_t* __restrict__ k, int n, int i, i
 }
 
 // parent[c]: (parent << 1) | side for internal c in [0, n-1) and leaf l at (n-1) + l
+// ranges[i] = (first leaf, last leaf, split gamma, 0): left child covers [first, gamma]
 __global__ __launch_bounds__(kBlock) void k_karras(const uint32_t* __restrict__ keys, int n, BNode* __restrict__ nodes,
-                                                   uint32_t* __restrict__ parent) {
+                                                   uint32_t* __restrict__ parent, int4* __restrict__ ranges) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n - 1) return;
     const int d = (lbvh_delta(keys, n, i, i + 1) - lbvh_delta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
@@ -123,41 +129,42 @@ __global__ __launch_bounds__(kBlock) void k_karras(const uint32_t* __restrict__ 
     const int lo = min(i, j), hi = max(i, j);
     const int left = (lo == gamma) ? ~gamma : gamma;
     const int right = (hi == gamma + 1) ? ~(gamma + 1) : gamma + 1;
-    nodes[i].d = make_int4(left, right, 0, 0);
+    float* f = nodes[i].f;
+    *reinterpret_cast<float2*>(f + 6) = make_float2(__int_as_float(left), __int_as_float(right));
+    ranges[i] = make_int4(lo, hi, gamma, 0);
     parent[left >= 0 ? left : (n - 1) + ~left] = ((uint32_t)i << 1) | 0u;
     parent[right >= 0 ? right : (n - 1) + ~right] = ((uint32_t)i << 1) | 1u;
 }
 
 __device__ inline float down1(float x) { return nextafterf(x, -INFINITY); }
 __device__ inline float up1(float x) { return nextafterf(x, INFINITY); }
+__device__ inline float out_lo(double x) { return down1(__double2float_rd(x)); }
+__device__ inline float out_hi(double x) { return up1(__double2float_ru(x)); }
 
-__device__ inline void store_slot(BNode* nodes, int node, int side, const float* lo, const float* hi) {
-    float* p = reinterpret_cast<float*>(nodes + node);
-    if (side == 0) {
-        *reinterpret_cast<float4*>(p) = make_float4(lo[0], lo[1], lo[2], hi[0]);
-        *reinterpret_cast<float2*>(p + 4) = make_float2(hi[1], hi[2]);
-    } else {
-        *reinterpret_cast<float2*>(p + 6) = make_float2(lo[0], lo[1]);
-        *reinterpret_cast<float4*>(p + 8) = make_float4(lo[2], hi[0], hi[1], hi[2]);
-    }
+__device__ inline void store_aabb(BNode* nodes, int node, int side, const float* lo, const float* hi) {
+    float* p = nodes[node].f + kAabb[side];  // 8 or 20: 16-B aligned, then an 8-B aligned pair
+    *reinterpret_cast<float4*>(p) = make_float4(lo[0], lo[1], lo[2], hi[0]);
+    *reinterpret_cast<float2*>(p + 4) = make_float2(hi[1], hi[2]);
 }
 
 __global__ __launch_bounds__(kBlock) void k_refit(const double* __restrict__ plo, const double* __restrict__ phi,
                                                   const uint32_t* __restrict__ order, int n, BNode* nodes,
-                                                  const uint32_t* __restrict__ parent, uint32_t* flags) {
+                                                  const uint32_t* __restrict__ parent, uint32_t* flags, double ox,
+                                                  double oy, double oz) {
     const int leaf = blockIdx.x * kBlock + threadIdx.x;
     if (leaf >= n) return;
     const uint32_t pr = order[leaf];
+    const double org[3] = {ox, oy, oz};
     float lo[3], hi[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        lo[k] = down1(__double2float_rd(plo[3 * (size_t)pr + k]));
-        hi[k] = up1(__double2float_ru(phi[3 * (size_t)pr + k]));
+        lo[k] = out_lo(plo[3 * (size_t)pr + k] - org[k]);
+        hi[k] = out_hi(phi[3 * (size_t)pr + k] - org[k]);
     }
     uint32_t p = parent[(n - 1) + leaf];
     for (int guard = 0; guard < 4096; ++guard) {  // bounded: a tree is never 4096 levels deep
         const int node = (int)(p >> 1), side = (int)(p & 1u);
-        store_slot(nodes, node, side, lo, hi);
+        store_aabb(nodes, node, side, lo, hi);
         // release: every store of this lane is performed and written back past this XCD's L2
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -165,18 +172,19 @@ __global__ __launch_bounds__(kBlock) void k_refit(const double* __restrict__ plo
         const uint32_t old = __hip_atomic_fetch_add(&flags[node], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (old == 0u) return;  // first arrival: the sibling's lane finishes this node
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const float* q = reinterpret_cast<const float*>(nodes + node);
-        float b[12];
+        const float* a = nodes[node].f + kAabb[0];
+        const float* b = nodes[node].f + kAabb[1];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) b[k] = q[k];
-        lo[0] = fminf(b[0], b[6]);  lo[1] = fminf(b[1], b[7]);  lo[2] = fminf(b[2], b[8]);
-        hi[0] = fmaxf(b[3], b[9]);  hi[1] = fmaxf(b[4], b[10]); hi[2] = fmaxf(b[5], b[11]);
+        for (int k = 0; k < 3; ++k) {
+            lo[k] = fminf(a[k], b[k]);
+            hi[k] = fmaxf(a[3 + k], b[3 + k]);
+        }
         if (node == 0) return;
         p = parent[node];
     }
 }
 
-// depth of every leaf (root = depth 1 for its children); out = max
+// depth of every leaf (root's children = 1); out = max
 __global__ __launch_bounds__(kBlock) void k_depth(const uint32_t* __restrict__ parent, int n, unsigned* __restrict__ out) {
     const int leaf = blockIdx.x * kBlock + threadIdx.x;
     if (leaf >= n) return;
@@ -187,6 +195,101 @@ __global__ __launch_bounds__(kBlock) void k_depth(const uint32_t* __restrict__ p
         ++d;
     }
     atomicMax(out, d);
+}
+
+// ---- oriented boxes: one wave per internal node ----
+__device__ inline double wsum(double x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o, 64);
+    return x;
+}
+__device__ inline double wmin(double x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = fmin(x, __shfl_xor(x, o, 64));
+    return x;
+}
+__device__ inline double wmax(double x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = fmax(x, __shfl_xor(x, o, 64));
+    return x;
+}
+
+template <bool TRI>
+__device__ inline int leaf_points(const void* leaves, int i, D3* p) {
+    if (TRI) {
+        uint32_t face;
+        load_tri(static_cast<const TriRec*>(leaves), i, p[0], p[1], p[2], face);
+        return 3;
+    }
+    const PtRec& r = static_cast<const PtRec*>(leaves)[i];
+    p[0] = D3{r.x, r.y, r.z};
+    return 1;
+}
+
+template <bool TRI>
+__global__ __launch_bounds__(kBlock) void k_obb(const void* __restrict__ leaves, const int4* __restrict__ ranges, int nn,
+                                                BNode* __restrict__ nodes, double ox, double oy, double oz) {
+    const int lane = threadIdx.x & 63;
+    const int waves = gridDim.x * (kBlock / 64);
+    for (int node = (blockIdx.x * kBlock + threadIdx.x) >> 6; node < nn; node += waves) {
+        const int4 r = ranges[node];
+        // area-weighted normal of the node's triangles (points: no area -> axis-aligned frame)
+        double sx = 0, sy = 0, sz = 0;
+        if (TRI) {
+            for (int i = r.x + lane; i <= r.y; i += 64) {
+                D3 p[3];
+                leaf_points<TRI>(leaves, i, p);
+                const D3 c = vcross(vsub(p[1], p[0]), vsub(p[2], p[0]));
+                sx += c.x; sy += c.y; sz += c.z;
+            }
+            sx = wsum(sx); sy = wsum(sy); sz = wsum(sz);
+        }
+        const double len = sqrt(sx * sx + sy * sy + sz * sz);
+        D3 n = (len > 0.0 && len < INFINITY) ? D3{sx / len, sy / len, sz / len} : D3{1.0, 0.0, 0.0};
+        const D3 e = fabs(n.x) < 0.9 ? D3{1.0, 0.0, 0.0} : D3{0.0, 1.0, 0.0};
+        D3 t = vsub(e, vscale(vdot(e, n), n));
+        const double tl = sqrt(vdot(t, t));
+        t = D3{t.x / tl, t.y / tl, t.z / tl};
+        const float n32[3] = {(float)n.x, (float)n.y, (float)n.z};
+        const float t32[3] = {(float)t.x, (float)t.y, (float)t.z};
+        float b32[3];
+        frame_b(n32, t32, b32);
+        const double A[3][3] = {{n32[0], n32[1], n32[2]}, {t32[0], t32[1], t32[2]}, {b32[0], b32[1], b32[2]}};
+        float ext[2][6];
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const int b = side == 0 ? r.x : r.z + 1;
+            const int eidx = side == 0 ? r.z : r.y;
+            double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int i = b + lane; i <= eidx; i += 64) {
+                D3 p[3];
+                const int np = leaf_points<TRI>(leaves, i, p);
+                for (int c = 0; c < np; ++c) {
+                    const double rx = p[c].x - ox, ry = p[c].y - oy, rz = p[c].z - oz;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        const double pr = A[k][0] * rx + A[k][1] * ry + A[k][2] * rz;
+                        mn[k] = fmin(mn[k], pr);
+                        mx[k] = fmax(mx[k], pr);
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                ext[side][k] = out_lo(wmin(mn[k]));
+                ext[side][3 + k] = out_hi(wmax(mx[k]));
+            }
+        }
+        if (lane == 0) {
+            float* f = nodes[node].f;
+            *reinterpret_cast<float4*>(f) = make_float4(n32[0], n32[1], n32[2], t32[0]);
+            *reinterpret_cast<float2*>(f + 4) = make_float2(t32[1], t32[2]);
+            *reinterpret_cast<float2*>(f + kObb[0]) = make_float2(ext[0][0], ext[0][1]);  // 14: 8-B aligned
+            *reinterpret_cast<float4*>(f + kObb[0] + 2) = make_float4(ext[0][2], ext[0][3], ext[0][4], ext[0][5]);
+            *reinterpret_cast<float2*>(f + kObb[1]) = make_float2(ext[1][0], ext[1][1]);  // 26
+            *reinterpret_cast<float4*>(f + kObb[1] + 2) = make_float4(ext[1][2], ext[1][3], ext[1][4], ext[1][5]);
+        }
+    }
 }
 
 __global__ __launch_bounds__(kBlock) void k_pack_tris(const double* __restrict__ v, const uint32_t* __restrict__ f,
@@ -249,6 +352,22 @@ int pack_point_leaves(const double* d_v, const uint32_t* d_order, size_t P, PtRe
     return MSH_OK;
 }
 
+int build_obb(msh_tree* tree, bool triangles) {
+    if (tree->T < 2) return MSH_OK;
+    const int nn = (int)(tree->T - 1);
+    const unsigned blocks = (unsigned)std::min<size_t>(((size_t)nn + 3) / 4, 65536);
+    hipStream_t s = tree->stream;
+    const int4* ranges = tree->ws.ranges.as<int4>();
+    if (triangles)
+        k_obb<true><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, tree->d_nodes, tree->origin[0],
+                                              tree->origin[1], tree->origin[2]);
+    else
+        k_obb<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, tree->d_nodes, tree->origin[0],
+                                               tree->origin[1], tree->origin[2]);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
 int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T, uint32_t* d_order) {
     hipStream_t s = tree->stream;
     Workspace& ws = tree->ws;
@@ -284,6 +403,8 @@ int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T,
     for (int k = 0; k < 3; ++k) {
         tree->scene_lo[k] = (float)box_h[k];
         tree->scene_hi[k] = (float)box_h[3 + k];
+        const double c = 0.5 * (box_h[k] + box_h[3 + k]);
+        tree->origin[k] = (c == c && fabs(c) < INFINITY) ? c : 0.0;
     }
     // Morton codes + sort
     MSH_TRY(ws.keys.reserve(T * sizeof(uint32_t)));
@@ -300,13 +421,15 @@ int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T,
     }
     // Karras emission
     MSH_TRY(ws.vals.reserve((2 * T - 1) * sizeof(uint32_t)));
+    MSH_TRY(ws.ranges.reserve((T - 1) * sizeof(int4)));
     uint32_t* parent = ws.vals.as<uint32_t>();
-    k_karras<<<nblocks(T - 1), kBlock, 0, s>>>(keys, (int)T, tree->d_nodes, parent);
+    k_karras<<<nblocks(T - 1), kBlock, 0, s>>>(keys, (int)T, tree->d_nodes, parent, ws.ranges.as<int4>());
     MSH_HIP(hipGetLastError());
     // refit
     uint32_t* flags = ws.flags.as<uint32_t>();
     MSH_HIP(hipMemsetAsync(flags, 0, T * sizeof(uint32_t) + 64, s));
-    k_refit<<<nblocks(T), kBlock, 0, s>>>(d_lo, d_hi, d_order, (int)T, tree->d_nodes, parent, flags);
+    k_refit<<<nblocks(T), kBlock, 0, s>>>(d_lo, d_hi, d_order, (int)T, tree->d_nodes, parent, flags, tree->origin[0],
+                                          tree->origin[1], tree->origin[2]);
     MSH_HIP(hipGetLastError());
     unsigned* d_depth = flags + T;
     MSH_HIP(hipMemsetAsync(d_depth, 0, sizeof(unsigned), s));

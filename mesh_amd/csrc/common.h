@@ -1,9 +1,13 @@
 // Shared device-side definitions for the MI355X (gfx950) point-to-mesh search engine.
 //
 // Data layout in HBM:
-//   BNode  — one LBVH internal node, 64 B: the fp32 AABBs of BOTH children (outward-rounded, so
-//            every fp64 primitive lies inside) + both child references.  A traversal step is one
-//            coalesced 64-B read (4 x 16-B loads) that tests two children.
+//   BNode  — one LBVH internal node, 128 B = one L2 line: a node frame (unit normal n and tangent t of
+//            the node's triangles, area-weighted; b = n x t is recomputed), and for BOTH children an fp32
+//            AABB and the fp32 extents of the child's vertices along (n, t, b) — an oriented box that is
+//            thin along the surface normal — plus both child references.  All fp32 bounds are relative
+//            to the tree's fp64 `origin` (scene-box centre) and rounded outward, so every fp64 primitive
+//            lies inside every ancestor's bounds.  A traversal step is one coalesced 128-B read
+//            (8 x 16-B loads) that tests two children.
 //   TriRec — one leaf triangle, 80 B: the 9 fp64 vertex coordinates (exact copies of the input) +
 //            the original face index.  Leaves are stored in Morton order, so a subtree's
 //            triangles are contiguous.
@@ -18,16 +22,18 @@
 namespace msh {
 
 constexpr int kBlock = 256;          // 4 waves of 64 lanes
-constexpr int kStack = 16;           // per-lane LDS stack entries (ring; overflow => restart)
+constexpr int kStack = 16;           // per-lane LDS stack entries; deeper entries spill to global memory
 constexpr double kSlack = 1.0 + 9.094947017729282e-13;  // 1 + 2^-40: fp64 rounding margin for culls
 
+// float index within a node:  0-2 n | 3-5 t | 6 child0 | 7 child1 |
+//   8-13 child0 AABB (lo xyz, hi xyz) | 14-19 child0 oriented extents (lo n t b, hi n t b) |
+//  20-25 child1 AABB                  | 26-31 child1 oriented extents
 struct alignas(16) BNode {
-    float4 a;  // lo0.x lo0.y lo0.z hi0.x
-    float4 b;  // hi0.y hi0.z lo1.x lo1.y
-    float4 c;  // lo1.z hi1.x hi1.y hi1.z
-    int4 d;    // child0, child1, unused, unused
+    float f[32];
 };
-static_assert(sizeof(BNode) == 64, "BNode must be 64 B");
+static_assert(sizeof(BNode) == 128, "BNode must be 128 B");
+constexpr int kAabb[2] = {8, 20};
+constexpr int kObb[2] = {14, 26};
 
 struct alignas(16) TriRec {
     double v[9];
@@ -62,31 +68,31 @@ __host__ __device__ inline double sqdist(const D3& p, const D3& q) {
 }
 __host__ __device__ inline bool veq(const D3& a, const D3& b) { return a.x == b.x && a.y == b.y && a.z == b.z; }
 
-// Squared distance from q to an fp32 box, evaluated in fp64 (the box corners convert exactly).
-__device__ inline double box_d2(const D3& q, float lx, float ly, float lz, float hx, float hy, float hz) {
-    const double dx = fmax(fmax((double)lx - q.x, q.x - (double)hx), 0.0);
-    const double dy = fmax(fmax((double)ly - q.y, q.y - (double)hy), 0.0);
-    const double dz = fmax(fmax((double)lz - q.z, q.z - (double)hz), 0.0);
-    return dx * dx + dy * dy + dz * dz;
+// third frame axis b = n x t in fp32 — the build and every query evaluate this same expression
+__host__ __device__ inline void frame_b(const float* n, const float* t, float* b) {
+    b[0] = n[1] * t[2] - n[2] * t[1];
+    b[1] = n[2] * t[0] - n[0] * t[2];
+    b[2] = n[0] * t[1] - n[1] * t[0];
 }
 
-struct Box6 {
-    float lx, ly, lz, hx, hy, hz;
+// ---- node loads ----
+struct NodeV {
+    float4 q[8];
+    __device__ float at(int i) const { return reinterpret_cast<const float*>(q)[i]; }
+    __device__ int child(int s) const { return __float_as_int(at(6 + s)); }
 };
-
-__device__ inline void node_boxes(const BNode& n, Box6& b0, Box6& b1) {
-    b0 = Box6{n.a.x, n.a.y, n.a.z, n.a.w, n.b.x, n.b.y};
-    b1 = Box6{n.b.z, n.b.w, n.c.x, n.c.y, n.c.z, n.c.w};
-}
-
-__device__ inline BNode load_node(const BNode* __restrict__ nodes, int i) {
+__device__ inline NodeV load_node(const BNode* __restrict__ nodes, int i) {
     const float4* p = reinterpret_cast<const float4*>(nodes + i);
-    BNode n;
-    n.a = p[0];
-    n.b = p[1];
-    n.c = p[2];
-    n.d = reinterpret_cast<const int4*>(p)[3];
+    NodeV n;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) n.q[k] = p[k];
     return n;
+}
+// children and AABBs only (first 48 + 16 B are not enough: the AABBs sit at floats 8-13 and 20-25)
+__device__ inline void node_aabb(const NodeV& n, int s, float* lo, float* hi) {
+    const int o = kAabb[s];
+    lo[0] = n.at(o); lo[1] = n.at(o + 1); lo[2] = n.at(o + 2);
+    hi[0] = n.at(o + 3); hi[1] = n.at(o + 4); hi[2] = n.at(o + 5);
 }
 
 __device__ inline void load_tri(const TriRec* __restrict__ tris, int i, D3& a, D3& b, D3& c, uint32_t& face) {
@@ -96,6 +102,14 @@ __device__ inline void load_tri(const TriRec* __restrict__ tris, int i, D3& a, D
     b = D3{x1.y, x2.x, x2.y};
     c = D3{x3.x, x3.y, x4.x};
     face = (uint32_t)__double_as_longlong(x4.y);
+}
+
+// Squared distance from q to an fp64-rounded fp32 box, evaluated in fp64 (box corners convert exactly).
+__device__ inline double box_d2(const D3& q, float lx, float ly, float lz, float hx, float hy, float hz) {
+    const double dx = fmax(fmax((double)lx - q.x, q.x - (double)hx), 0.0);
+    const double dy = fmax(fmax((double)ly - q.y, q.y - (double)hy), 0.0);
+    const double dz = fmax(fmax((double)lz - q.z, q.z - (double)hz), 0.0);
+    return dx * dx + dy * dy + dz * dz;
 }
 
 // --- CGAL constructions (Simple_cartesian<double>), evaluated without FMA contraction ---
@@ -178,6 +192,122 @@ __device__ inline double closest_on_triangle(const D3& o, const D3& t0, const D3
         part = 0;
     }
     return sqdist(o, out);
+}
+
+// ---- conservative fp32 culling (never rejects what the exact fp64 test would accept) ----
+// The query relative to the tree origin, rounded to fp32; e = largest per-axis rounding error (rounded
+// up); pe = bound of the fp32 projection error onto a unit axis (2^-21 * |q|_1 + 2e, rounded up).
+struct QF {
+    float x, y, z, e, pe;
+};
+__device__ inline QF make_qf(const D3& q, const double* origin) {
+    const double rx = q.x - origin[0], ry = q.y - origin[1], rz = q.z - origin[2];
+    QF r;
+    r.x = (float)rx;
+    r.y = (float)ry;
+    r.z = (float)rz;
+    const double e = fmax(fmax(fabs(rx - (double)r.x), fabs(ry - (double)r.y)), fabs(rz - (double)r.z));
+    r.e = __double2float_ru(e);
+    r.pe = __double2float_ru(4.76837158203125e-7 * (fabs((double)r.x) + fabs((double)r.y) + fabs((double)r.z)) + 2.0 * e);
+    return r;
+}
+
+// Lower bound of the squared distance from q to an fp32 box: per-axis gaps are shrunk by the fp32
+// subtraction error (<= 2^-24 relative) and the query rounding error, the sum by 3 roundings (2^-21).
+__host__ __device__ inline float box_d2_lo(const QF& q, float lx, float ly, float lz, float hx, float hy, float hz) {
+    const float k = 0.99999988079071044921875f;  // 1 - 2^-23
+    float gx = fmaxf(fmaxf(lx - q.x, q.x - hx), 0.f);
+    float gy = fmaxf(fmaxf(ly - q.y, q.y - hy), 0.f);
+    float gz = fmaxf(fmaxf(lz - q.z, q.z - hz), 0.f);
+    gx = fmaxf(gx * k - q.e, 0.f);
+    gy = fmaxf(gy * k - q.e, 0.f);
+    gz = fmaxf(gz * k - q.e, 0.f);
+    return (gx * gx + gy * gy + gz * gz) * 0.999999523162841796875f;  // 1 - 2^-21
+}
+
+// Lower bound of the squared distance from q to the oriented box {x : lo_k <= a_k . x <= hi_k} with
+// nearly orthonormal fp32 axes (n, t, b): the projections carry an error <= q.pe, the subtraction
+// 2^-24 relative, and the sum of squared slab gaps is divided by lambda_max(A A^T) <= 1 + 1e-6 (fp32
+// axes), covered by the factor 1 - 2^-18.
+__host__ __device__ inline float obb_d2_lo(const QF& q, const float* n, const float* t, const float* b, const float* ext) {
+    const float k = 0.99999988079071044921875f;  // 1 - 2^-23
+    const float pn = n[0] * q.x + n[1] * q.y + n[2] * q.z;
+    const float pt = t[0] * q.x + t[1] * q.y + t[2] * q.z;
+    const float pb = b[0] * q.x + b[1] * q.y + b[2] * q.z;
+    float gn = fmaxf(fmaxf(ext[0] - pn, pn - ext[3]), 0.f);
+    float gt = fmaxf(fmaxf(ext[1] - pt, pt - ext[4]), 0.f);
+    float gb = fmaxf(fmaxf(ext[2] - pb, pb - ext[5]), 0.f);
+    gn = fmaxf(gn * k - q.pe, 0.f);
+    gt = fmaxf(gt * k - q.pe, 0.f);
+    gb = fmaxf(gb * k - q.pe, 0.f);
+    return (gn * gn + gt * gt + gb * gb) * 0.999996185302734375f;  // 1 - 2^-18
+}
+
+// Both children's lower bounds from one node: max(AABB bound, oriented-box bound).
+__device__ inline void node_child_bounds(const NodeV& nd, const QF& q, float& d0, float& d1) {
+    const float n[3] = {nd.at(0), nd.at(1), nd.at(2)};
+    const float t[3] = {nd.at(3), nd.at(4), nd.at(5)};
+    float b[3];
+    frame_b(n, t, b);
+    float e0[6], e1[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        e0[k] = nd.at(kObb[0] + k);
+        e1[k] = nd.at(kObb[1] + k);
+    }
+    const int a0 = kAabb[0], a1 = kAabb[1];
+    d0 = fmaxf(box_d2_lo(q, nd.at(a0), nd.at(a0 + 1), nd.at(a0 + 2), nd.at(a0 + 3), nd.at(a0 + 4), nd.at(a0 + 5)),
+               obb_d2_lo(q, n, t, b, e0));
+    d1 = fmaxf(box_d2_lo(q, nd.at(a1), nd.at(a1 + 1), nd.at(a1 + 2), nd.at(a1 + 3), nd.at(a1 + 4), nd.at(a1 + 5)),
+               obb_d2_lo(q, n, t, b, e1));
+}
+
+// Lower bound of the squared distance from the origin to triangle (A, B, C) given in fp32 coordinates
+// relative to the query (Ericson's Voronoi-region closest point, evaluated in fp32).  For a triangle
+// whose smallest angle is not tiny the rounding error of the result is O(ulp * M / sin^2(angle)),
+// M = largest |coordinate|: triangles with sin^2 < 1e-2 return 0 (no rejection), a face-region
+// result outside the triangle returns 0, and the bound subtracts 2^-12 * M (>= 40x the error bound).
+// NaN (degenerate input) also propagates, which callers treat as "cannot reject".
+__host__ __device__ inline float tri_d2_lo(float ax, float ay, float az, float bx, float by, float bz, float cx, float cy,
+                                           float cz) {
+    const float abx = bx - ax, aby = by - ay, abz = bz - az;
+    const float acx = cx - ax, acy = cy - ay, acz = cz - az;
+    {
+        const float nx = aby * acz - abz * acy, ny = abz * acx - abx * acz, nz = abx * acy - aby * acx;
+        const float n2 = nx * nx + ny * ny + nz * nz;
+        const float l2 = (abx * abx + aby * aby + abz * abz) * (acx * acx + acy * acy + acz * acz);
+        if (!(n2 >= 1e-2f * l2)) return 0.f;  // sliver or degenerate (also catches NaN / 0)
+    }
+    float px, py, pz;
+    const float d1 = -(abx * ax + aby * ay + abz * az), d2 = -(acx * ax + acy * ay + acz * az);
+    const float d3 = -(abx * bx + aby * by + abz * bz), d4 = -(acx * bx + acy * by + acz * bz);
+    const float d5 = -(abx * cx + aby * cy + abz * cz), d6 = -(acx * cx + acy * cy + acz * cz);
+    const float vc = d1 * d4 - d3 * d2, vb = d5 * d2 - d1 * d6, va = d3 * d6 - d5 * d4;
+    if (d1 <= 0.f && d2 <= 0.f) {
+        px = ax; py = ay; pz = az;
+    } else if (d3 >= 0.f && d4 <= d3) {
+        px = bx; py = by; pz = bz;
+    } else if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
+        const float t = d1 / (d1 - d3);
+        px = ax + t * abx; py = ay + t * aby; pz = az + t * abz;
+    } else if (d6 >= 0.f && d5 <= d6) {
+        px = cx; py = cy; pz = cz;
+    } else if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
+        const float t = d2 / (d2 - d6);
+        px = ax + t * acx; py = ay + t * acy; pz = az + t * acz;
+    } else if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
+        const float t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
+        px = bx + t * (cx - bx); py = by + t * (cy - by); pz = bz + t * (cz - bz);
+    } else {
+        const float den = 1.f / (va + vb + vc);
+        const float v = vb * den, w = vc * den;
+        if (!(v >= -1e-3f && w >= -1e-3f && v + w <= 1.001f)) return 0.f;
+        px = ax + abx * v + acx * w; py = ay + aby * v + acy * w; pz = az + abz * v + acz * w;
+    }
+    const float M = fmaxf(fmaxf(fmaxf(fabsf(ax), fabsf(ay)), fmaxf(fabsf(az), fabsf(bx))),
+                          fmaxf(fmaxf(fabsf(by), fabsf(bz)), fmaxf(fmaxf(fabsf(cx), fabsf(cy)), fabsf(cz))));
+    const float d = sqrtf(px * px + py * py + pz * pz) - M * 2.44140625e-4f;  // 2^-12
+    return d > 0.f ? d * d * 0.999999523162841796875f : (d <= 0.f ? 0.f : d);  // NaN propagates
 }
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):

@@ -41,7 +41,7 @@ struct DevBuf {
 
 // Reusable per-handle scratch (query keys / permutation / sort temporaries / results).
 struct Workspace {
-    DevBuf keys, vals, keys_alt, vals_alt, hist, scan, q, out_a, out_b, out_c, flags, counters, spill, stats;
+    DevBuf keys, vals, keys_alt, vals_alt, hist, scan, q, out_a, out_b, out_c, flags, counters, spill, stats, ranges;
     void release();
 };
 
@@ -60,6 +60,7 @@ struct msh_tree {
     msh::BNode* d_nodes = nullptr; // T-1 internal nodes (nullptr when T == 1)
     void* d_leaves = nullptr;      // T TriRec or PtRec in Morton order
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};  // bbox of all primitives
+    double origin[3] = {0, 0, 0};  // fp64 scene-box centre: all fp32 node bounds are relative to it
     hipStream_t stream = nullptr;
     double build_ms = 0.0;
     int max_depth = 0;             // deepest leaf (root children = 1)
@@ -79,6 +80,8 @@ int exclusive_scan_u32(uint32_t* data, size_t n, Workspace& ws, hipStream_t s);
 // prim_lo/prim_hi: (T,3) fp64 bounds per primitive on device.  Builds nodes and the Morton order
 // `order` (sorted position -> primitive id).  scene box written to tree.
 int build_lbvh(msh_tree* tree, const double* d_prim_lo, const double* d_prim_hi, size_t T, uint32_t* d_order);
+// Oriented-box pass over the packed leaves (needs the node ranges recorded by build_lbvh).
+int build_obb(msh_tree* tree, bool triangles);
 int tri_bounds(const double* d_v, const uint32_t* d_f, size_t T, double* d_lo, double* d_hi, hipStream_t s);
 int pack_tri_leaves(const double* d_v, const uint32_t* d_f, const uint32_t* d_order, size_t T, uint32_t face_base,
                     TriRec* d_out, hipStream_t s);

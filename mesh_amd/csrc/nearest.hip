@@ -4,25 +4,37 @@
 // variant (K8, search.ClosestPointTree).
 //
 // Execution shape (gfx950):
-//   * persistent grid (≈5 workgroups of 256 lanes per CU, the LDS-stack limit); each WAVE dequeues
-//     64-query tiles from one of 8 XCD-group counters (group = blockIdx % 8, which labels the blocks
-//     sharing an XCD), each counter owning a contiguous eighth of the Morton-sorted queries — an XCD's
-//     L2 then serves one spatial region of the BVH; exhausted groups steal from the others.
-//   * one lane per query, queries visited in Morton order (perm) for wave coherence;
-//   * near-child-first depth-first traversal: one 64-B node read tests both children (fp32 boxes,
-//     distance evaluated in fp64 so the cull is conservative), leaves are tested immediately in fp64
-//     with CGAL's construction, the far child is pushed with its lower-bound distance;
-//   * per-lane stack: 16 entries in LDS ([depth][lane] layout, conflict-free), deeper entries spill to
-//     a per-lane global area sized from the tree depth measured at build time;
-//   * ties: the lexicographic minimum of (squared distance, face index) — deterministic and independent
-//     of traversal order (boxes at distance <= best*(1+2^-40) are visited, so equal-distance faces are
-//     all examined).
+//   Pass 1 (k_knn): persistent grid; each WAVE dequeues 64-query tiles from one of 8 XCD-group
+//     counters (group = blockIdx % 8 labels the blocks sharing an XCD; each counter owns a contiguous
+//     eighth of the Morton-sorted queries, so an XCD's L2 serves one region of the BVH; exhausted
+//     groups steal).  One lane per query, near-child-first depth-first traversal: one 64-B node read
+//     tests both children with conservative fp32 box bounds, leaves get a conservative fp32 pretest and
+//     then CGAL's exact fp64 construction, the far child is pushed (16-entry LDS stack per lane,
+//     [depth][lane] layout, deeper entries spill to a per-lane global area sized from the tree depth).
+//     A lane that exceeds `budget` node steps stops and appends its query (with its best so far) to a
+//     deferred list: queries near the centre of a closed surface are equidistant from most of it and
+//     would otherwise hold their whole wave for ~10^6 steps.
+//   Pass 2 (k_knn_coop): one WAVE per deferred query.  The wave expands the top of the tree
+//     breadth-first into <= 512 subtrees (LDS frontier), deals them to its 64 lanes, and every lane walks
+//     its subtrees depth-first while the wave shares the best bound after every step (wave min).
+// Ties: the lexicographic minimum of (squared distance, face index) — deterministic and independent of
+// traversal order or of how the work was split (every box within best*(1+2^-40) is visited).
 #include <algorithm>
 #include <mutex>
 
 #include "internal.h"
 
 namespace msh {
+
+struct DeferRec {
+    uint32_t qi;
+    uint32_t face;
+    int32_t leaf;
+    uint32_t pad;
+    double best;
+    double pad2;
+};
+static_assert(sizeof(DeferRec) == 32, "DeferRec must be 32 B");
 
 struct KnnArgs {
     const BNode* nodes;
@@ -37,11 +49,16 @@ struct KnnArgs {
     double* out_pt;
     double* out_dist;
     double eps;
+    double org[3];  // tree origin: fp32 node bounds are relative to it
     unsigned* counters;
     unsigned ntiles;
     uint2* spill;
     int spill_depth;
     unsigned long long* stats;
+    unsigned budget;
+    DeferRec* deferred;
+    unsigned* n_deferred;
+    unsigned max_deferred;
 };
 
 __device__ inline unsigned dequeue_tile(unsigned* counters, unsigned ntiles, unsigned group) {
@@ -58,17 +75,34 @@ __device__ inline unsigned dequeue_tile(unsigned* counters, unsigned ntiles, uns
 }
 
 // ---- leaf policies ----
+// limit(): squared radius (in box-distance units) inside which a primitive can still beat or tie the
+// best.  `shared` is a bound published by other lanes working on the same query (pass 2); it is always
+// >= the final best, so pruning with min(best, shared) keeps the result exact.  Every leaf first gets
+// the conservative fp32 lower bound (tri_d2_lo); the exact fp64 CGAL construction runs only if that
+// cannot reject it.
+__device__ inline void rel_f32(const D3& a, const D3& q, float& x, float& y, float& z) {
+    x = (float)(a.x - q.x);
+    y = (float)(a.y - q.y);
+    z = (float)(a.z - q.z);
+}
+
 struct TriPol {
     const TriRec* __restrict__ tris;
     D3 q;
-    double best;
+    double best, shared;
     uint32_t best_face;
     int best_leaf;
-    __device__ double limit() const { return best * kSlack; }
+    __device__ double limit() const { return fmin(best, shared) * kSlack; }
     __device__ void test(int leaf) {
         D3 a, b, c;
         uint32_t face;
         load_tri(tris, leaf, a, b, c, face);
+        float ax, ay, az, bx, by, bz, cx, cy, cz;
+        rel_f32(a, q, ax, ay, az);
+        rel_f32(b, q, bx, by, bz);
+        rel_f32(c, q, cx, cy, cz);
+        const float lo = tri_d2_lo(ax, ay, az, bx, by, bz, cx, cy, cz);
+        if (lo > __double2float_ru(limit())) return;  // NaN never rejects
         D3 o;
         int part;
         const double d2 = closest_on_triangle(q, a, b, c, o, part);
@@ -86,13 +120,14 @@ struct NrmPol {
     const TriRec* __restrict__ tris;
     D3 q, qn;
     double eps, pmin;
-    double best;
+    double best, shared;
     uint32_t best_face;
     int best_leaf;
     __device__ double limit() const {
-        if (best == INFINITY) return INFINITY;
-        double r = best - pmin;
-        r += 1e-12 * (fabs(best) + fabs(pmin));
+        const double b = fmin(best, shared);
+        if (b == INFINITY) return INFINITY;
+        double r = b - pmin;
+        r += 1e-12 * (fabs(b) + fabs(pmin));
         if (r < 0.0) r = 0.0;
         return r * r * kSlack;
     }
@@ -100,6 +135,12 @@ struct NrmPol {
         D3 a, b, c;
         uint32_t face;
         load_tri(tris, leaf, a, b, c, face);
+        float ax, ay, az, bx, by, bz, cx, cy, cz;
+        rel_f32(a, q, ax, ay, az);
+        rel_f32(b, q, bx, by, bz);
+        rel_f32(c, q, cx, cy, cz);
+        const float lo = tri_d2_lo(ax, ay, az, bx, by, bz, cx, cy, cz);
+        if (lo > __double2float_ru(limit())) return;
         D3 o;
         int part;
         const double d2 = closest_on_triangle(q, a, b, c, o, part);
@@ -119,10 +160,10 @@ struct NrmPol {
 struct PtPol {
     const PtRec* __restrict__ pts;
     D3 q;
-    double best;
+    double best, shared;
     uint32_t best_face;
     int best_leaf;
-    __device__ double limit() const { return best * kSlack; }
+    __device__ double limit() const { return fmin(best, shared) * kSlack; }
     __device__ void test(int leaf) {
         const double2* p = reinterpret_cast<const double2*>(pts + leaf);
         const double2 x0 = p[0], x1 = p[1];
@@ -136,65 +177,121 @@ struct PtPol {
     }
 };
 
-// Near-child-first depth-first traversal.  lds: this lane's column of the LDS stack (stride kBlock).
-template <class Pol, bool STATS>
-__device__ inline void traverse(const BNode* __restrict__ nodes, size_t T, const D3& q, Pol& pol, uint2* __restrict__ lds,
-                                uint2* __restrict__ spill, unsigned& n_nodes, unsigned& n_leaves) {
-    if (T == 1) {
-        pol.test(0);
-        if (STATS) ++n_leaves;
-        return;
+// Per-lane depth-first walker.  lds: this lane's column of the LDS stack (stride kBlock).
+struct Walker {
+    int node;
+    int sp;
+    __device__ inline void push(uint2 e, uint2* __restrict__ lds, uint2* __restrict__ spill) {
+        if (sp < kStack) lds[sp * kBlock] = e;
+        else spill[sp - kStack] = e;
+        ++sp;
     }
-    int node = 0;
-    int sp = 0;
-    // every internal node is entered at most once per query; the cap only bounds a corrupt tree
-    for (size_t guard = 0; guard < T; ++guard) {
-        const BNode nd = load_node(nodes, node);
+    // pop until an entry survives the current limit; false when the stack is exhausted
+    template <class Pol>
+    __device__ inline bool pop(const Pol& pol, uint2* __restrict__ lds, uint2* __restrict__ spill) {
+        while (sp > 0) {
+            --sp;
+            const uint2 e = sp < kStack ? lds[sp * kBlock] : spill[sp - kStack];
+            if (__uint_as_float(e.y) <= __double2float_ru(pol.limit())) {
+                node = (int)e.x;
+                return true;
+            }
+        }
+        return false;
+    }
+    // Visit `node`: bound its two children (max of the fp32 AABB and oriented-box lower bounds), test
+    // leaf children, descend into the nearer internal child and push the farther one.  Returns false
+    // when the traversal is complete.
+    template <class Pol, bool STATS>
+    __device__ inline bool step(const BNode* __restrict__ nodes, const QF& qf, Pol& pol, uint2* __restrict__ lds,
+                                uint2* __restrict__ spill, unsigned& n_nodes, unsigned& n_leaves) {
+        const NodeV nd = load_node(nodes, node);
         if (STATS) ++n_nodes;
-        const double d0 = box_d2(q, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y);
-        const double d1 = box_d2(q, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w);
-        const int c0 = nd.d.x, c1 = nd.d.y;
-        double lim = pol.limit();
+        float d0, d1;
+        node_child_bounds(nd, qf, d0, d1);
+        const int c0 = nd.child(0), c1 = nd.child(1);
+        float lim = __double2float_ru(pol.limit());
         bool h0 = d0 <= lim, h1 = d1 <= lim;
         if (h0 && c0 < 0) {
             pol.test(~c0);
             if (STATS) ++n_leaves;
             h0 = false;
-            lim = pol.limit();
+            lim = __double2float_ru(pol.limit());
         }
         if (h1 && c1 < 0) {
             pol.test(~c1);
             if (STATS) ++n_leaves;
             h1 = false;
-            lim = pol.limit();
+            lim = __double2float_ru(pol.limit());
         }
         h0 = h0 && d0 <= lim;
         h1 = h1 && d1 <= lim;
         if (h0 && h1) {
             int nearc = c0, farc = c1;
-            double dfar = d1;
+            float dfar = d1;
             if (d1 < d0) { nearc = c1; farc = c0; dfar = d0; }
-            const uint2 e = make_uint2((unsigned)farc, __float_as_uint(__double2float_rd(dfar)));
-            if (sp < kStack) lds[sp * kBlock] = e;
-            else spill[sp - kStack] = e;
-            ++sp;
+            push(make_uint2((unsigned)farc, __float_as_uint(dfar)), lds, spill);
             node = nearc;
-            continue;
+            return true;
         }
-        if (h0) { node = c0; continue; }
-        if (h1) { node = c1; continue; }
-        bool found = false;
-        while (sp > 0) {
-            --sp;
-            const uint2 e = sp < kStack ? lds[sp * kBlock] : spill[sp - kStack];
-            if ((double)__uint_as_float(e.y) <= pol.limit()) {
-                node = (int)e.x;
-                found = true;
-                break;
-            }
-        }
-        if (!found) break;
+        if (h0) { node = c0; return true; }
+        if (h1) { node = c1; return true; }
+        return pop(pol, lds, spill);
     }
+};
+
+// Outputs of one query from its policy (winner's leaf -> point / part recomputed exactly).
+template <int MODE, class Pol>
+__device__ inline void write_result(const KnnArgs& a, size_t qi, const D3& q, const Pol& pol) {
+    if (MODE == 2) {
+        a.out_face[qi] = pol.best_face;
+        a.out_dist[qi] = sqrt(pol.best);
+        return;
+    }
+    const TriRec* tris = static_cast<const TriRec*>(a.leaves);
+    D3 ta, tb, tc, o = D3{NAN, NAN, NAN};
+    uint32_t face = 0xFFFFFFFFu;
+    int part = 0;
+    if (pol.best_leaf >= 0) {  // < 0 only for a non-finite query
+        load_tri(tris, pol.best_leaf, ta, tb, tc, face);
+        closest_on_triangle(q, ta, tb, tc, o, part);
+    }
+    a.out_face[qi] = face;
+    if (MODE == 0 && a.out_part) a.out_part[qi] = (uint32_t)part;
+    a.out_pt[3 * qi] = o.x;
+    a.out_pt[3 * qi + 1] = o.y;
+    a.out_pt[3 * qi + 2] = o.z;
+}
+
+template <int MODE>
+struct PolOf;
+template <>
+struct PolOf<0> { using T = TriPol; };
+template <>
+struct PolOf<1> { using T = NrmPol; };
+template <>
+struct PolOf<2> { using T = PtPol; };
+
+template <int MODE>
+__device__ inline typename PolOf<MODE>::T make_pol(const KnnArgs& a, size_t qi, const D3& q) {
+    typename PolOf<MODE>::T pol;
+    if constexpr (MODE == 2) {
+        pol.pts = static_cast<const PtRec*>(a.leaves);
+    } else {
+        pol.tris = static_cast<const TriRec*>(a.leaves);
+    }
+    pol.q = q;
+    if constexpr (MODE == 1) {
+        pol.qn = D3{a.n[3 * qi], a.n[3 * qi + 1], a.n[3 * qi + 2]};
+        const double nq = sqrt(vdot(pol.qn, pol.qn));
+        pol.eps = a.eps;
+        pol.pmin = fmin(a.eps * (1 - nq), a.eps * (1 + nq));
+    }
+    pol.best = INFINITY;
+    pol.shared = INFINITY;
+    pol.best_face = 0xFFFFFFFFu;
+    pol.best_leaf = -1;
+    return pol;
 }
 
 template <int MODE, bool STATS>
@@ -214,48 +311,155 @@ __global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
         if (i >= a.S) continue;
         const size_t qi = a.perm ? (size_t)a.perm[i] : i;
         const D3 q = D3{a.q[3 * qi], a.q[3 * qi + 1], a.q[3 * qi + 2]};
-        if (MODE == 0) {
-            TriPol pol{static_cast<const TriRec*>(a.leaves), q, INFINITY, 0xFFFFFFFFu, -1};
-            traverse<TriPol, STATS>(a.nodes, a.T, q, pol, lds, spill, n_nodes, n_leaves);
-            if (!STATS) {
-                D3 ta, tb, tc, o = D3{NAN, NAN, NAN};
-                uint32_t face = 0xFFFFFFFFu;
-                int part = 0;
-                if (pol.best_leaf >= 0) {  // < 0 only for a non-finite query
-                    load_tri(pol.tris, pol.best_leaf, ta, tb, tc, face);
-                    closest_on_triangle(q, ta, tb, tc, o, part);
-                }
-                a.out_face[qi] = face;
-                if (a.out_part) a.out_part[qi] = (uint32_t)part;
-                a.out_pt[3 * qi] = o.x;
-                a.out_pt[3 * qi + 1] = o.y;
-                a.out_pt[3 * qi + 2] = o.z;
-            }
-        } else if (MODE == 1) {
-            const D3 qn = D3{a.n[3 * qi], a.n[3 * qi + 1], a.n[3 * qi + 2]};
-            const double nq = sqrt(vdot(qn, qn));
-            const double pmin = fmin(a.eps * (1 - nq), a.eps * (1 + nq));
-            NrmPol pol{static_cast<const TriRec*>(a.leaves), q, qn, a.eps, pmin, INFINITY, 0xFFFFFFFFu, -1};
-            traverse<NrmPol, STATS>(a.nodes, a.T, q, pol, lds, spill, n_nodes, n_leaves);
-            D3 ta, tb, tc, o = D3{NAN, NAN, NAN};
-            uint32_t face = 0xFFFFFFFFu;
-            int part = 0;
-            if (pol.best_leaf >= 0) {
-                load_tri(pol.tris, pol.best_leaf, ta, tb, tc, face);
-                closest_on_triangle(q, ta, tb, tc, o, part);
-            }
-            a.out_face[qi] = face;
-            a.out_pt[3 * qi] = o.x;
-            a.out_pt[3 * qi + 1] = o.y;
-            a.out_pt[3 * qi + 2] = o.z;
+        auto pol = make_pol<MODE>(a, qi, q);
+        if (a.T == 1) {
+            pol.test(0);
+            if (STATS) ++n_leaves;
         } else {
-            PtPol pol{static_cast<const PtRec*>(a.leaves), q, INFINITY, 0xFFFFFFFFu, -1};
-            traverse<PtPol, STATS>(a.nodes, a.T, q, pol, lds, spill, n_nodes, n_leaves);
-            a.out_face[qi] = pol.best_face;
-            a.out_dist[qi] = sqrt(pol.best);
+            const QF qf = make_qf(q, a.org);
+            Walker w{0, 0};
+            bool active = true;
+            size_t steps = 0;
+            while (active) {
+                active = w.step<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, n_leaves);
+                ++steps;
+                if (!active) break;
+                if (steps >= a.T) {  // each internal node is entered at most once: corrupt tree, stop
+                    active = false;
+                    break;
+                }
+                if (steps == a.budget) {
+                    const unsigned slot = atomicAdd(a.n_deferred, 1u);
+                    if (slot < a.max_deferred) {
+                        DeferRec r;
+                        r.qi = (uint32_t)qi;
+                        r.face = pol.best_face;
+                        r.leaf = pol.best_leaf;
+                        r.pad = 0;
+                        r.best = pol.best;
+                        r.pad2 = 0;
+                        a.deferred[slot] = r;
+                        break;  // active stays true: pass 2 owns this query
+                    }
+                    // deferred list full: finish here without a budget
+                }
+            }
+            if (active) continue;  // deferred: pass 2 writes this query
         }
+        if (!STATS) write_result<MODE>(a, qi, q, pol);
     }
     if (STATS) {
+        atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
+        atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
+    }
+}
+
+// lexicographic min of (best, face) over the wave; every lane ends with the winner
+__device__ inline void wave_lexmin(double& best, uint32_t& face, int& leaf) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+        const double b2 = __shfl_xor(best, o, 64);
+        const uint32_t f2 = (uint32_t)__shfl_xor((int)face, o, 64);
+        const int l2 = __shfl_xor(leaf, o, 64);
+        if (b2 < best || (b2 == best && f2 < face)) {
+            best = b2;
+            face = f2;
+            leaf = l2;
+        }
+    }
+}
+
+__device__ inline double wave_min(double x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = fmin(x, __shfl_xor(x, o, 64));
+    return x;
+}
+
+constexpr int kFront = 512;  // frontier entries per wave in pass 2
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
+    __shared__ uint2 stk[kStack * kBlock];
+    __shared__ uint2 front[4][2][kFront];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    uint2* lds = stk + tid;
+    uint2* spill = a.spill ? a.spill + ((size_t)blockIdx.x * kBlock + tid) * (size_t)a.spill_depth : nullptr;
+    const unsigned total = min(*a.n_deferred, a.max_deferred);
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    unsigned n_nodes = 0, n_leaves = 0;
+    for (unsigned item = blockIdx.x * 4 + wv; item < total; item += gridDim.x * 4) {
+        const DeferRec r = a.deferred[item];
+        const size_t qi = r.qi;
+        const D3 q = D3{a.q[3 * qi], a.q[3 * qi + 1], a.q[3 * qi + 2]};
+        const QF qf = make_qf(q, a.org);
+        auto pol = make_pol<MODE>(a, qi, q);
+        pol.shared = r.best;  // pass-1 best: an upper bound of the final best
+        if (lane == 0) {
+            pol.best = r.best;
+            pol.best_face = r.face;
+            pol.best_leaf = r.leaf;
+        }
+        // breadth-first expansion of the top of the tree into <= kFront subtrees
+        int cur = 0, n = 1;
+        if (lane == 0) front[wv][0][0] = make_uint2(0u, 0u);
+        __builtin_amdgcn_wave_barrier();
+        while (n > 0 && n <= kFront / 2) {
+            int m = 0;
+            for (int base = 0; base < n; base += 64) {
+                const int i = base + lane;
+                bool k0 = false, k1 = false;
+                uint2 e0, e1;
+                if (i < n) {
+                    const uint2 e = front[wv][cur][i];
+                    if (__uint_as_float(e.y) <= __double2float_ru(pol.limit())) {
+                        const NodeV nd = load_node(a.nodes, (int)e.x);
+                        ++n_nodes;
+                        float d0, d1;
+                        node_child_bounds(nd, qf, d0, d1);
+                        const int c0 = nd.child(0), c1 = nd.child(1);
+                        if (d0 <= __double2float_ru(pol.limit())) {
+                            if (c0 < 0) { pol.test(~c0); ++n_leaves; }
+                            else { k0 = true; e0 = make_uint2((unsigned)c0, __float_as_uint(d0)); }
+                        }
+                        if (d1 <= __double2float_ru(pol.limit())) {
+                            if (c1 < 0) { pol.test(~c1); ++n_leaves; }
+                            else { k1 = true; e1 = make_uint2((unsigned)c1, __float_as_uint(d1)); }
+                        }
+                    }
+                }
+                const unsigned long long b0 = __ballot(k0), b1 = __ballot(k1);
+                const int p0 = m + __popcll(b0 & lt) + __popcll(b1 & lt);
+                if (k0) front[wv][cur ^ 1][p0] = e0;
+                if (k1) front[wv][cur ^ 1][p0 + (k0 ? 1 : 0)] = e1;
+                m += __popcll(b0) + __popcll(b1);
+                pol.shared = fmin(pol.shared, wave_min(pol.best));
+            }
+            __builtin_amdgcn_wave_barrier();
+            cur ^= 1;
+            n = m;
+        }
+        // deal the frontier to the lanes (entry j -> lane j % 64), then depth-first walks
+        Walker w{0, 0};
+        if (lane < n)
+            for (int j = lane + ((n - 1 - lane) / 64) * 64; j >= lane; j -= 64) w.push(front[wv][cur][j], lds, spill);
+        bool active = w.pop(pol, lds, spill);
+        while (__any(active)) {
+            if (active) active = w.step<decltype(pol), false>(a.nodes, qf, pol, lds, spill, n_nodes, n_leaves);
+            pol.shared = fmin(pol.shared, wave_min(pol.best));
+        }
+        double best = pol.best;
+        uint32_t face = pol.best_face;
+        int leaf = pol.best_leaf;
+        wave_lexmin(best, face, leaf);
+        if (lane == 0) {
+            pol.best = best;
+            pol.best_face = face;
+            pol.best_leaf = leaf;
+            write_result<MODE>(a, qi, q, pol);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (a.stats) {
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
         atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
     }
@@ -307,28 +511,48 @@ static int device_cus(int dev) {
     return cache[dev];
 }
 
-// Common launch: grid, counters, spill area.
+constexpr unsigned kBudget = 2048;  // pass-1 node steps per lane before a query is deferred
+
+// Common launch: grid, counters, spill area, deferred list; pass 1 then pass 2.
 template <int MODE, bool STATS>
 static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* timer) {
     if (a.S == 0) return MSH_OK;
+    for (int k = 0; k < 3; ++k) a.org[k] = tree->origin[k];
     const unsigned ntiles = (unsigned)((a.S + 63) / 64);
     const unsigned want = (ntiles + 3) / 4;
-    const unsigned nblk = std::min<unsigned>(want, (unsigned)device_cus(tree->device) * 5u);
+    const unsigned ncu = (unsigned)device_cus(tree->device);
+    const unsigned nblk = std::min<unsigned>(want, ncu * 4u);
     a.ntiles = ntiles;
-    // counters (8 x 128 B) + spill
-    MSH_TRY(tree->ws.counters.reserve(8 * 32 * sizeof(unsigned)));
-    a.counters = tree->ws.counters.as<unsigned>();
-    MSH_HIP(hipMemsetAsync(a.counters, 0, 8 * 32 * sizeof(unsigned), s));
+    Workspace& ws = tree->ws;
+    // counters: 8 group counters (one 128-B line each) + the deferred count
+    MSH_TRY(ws.counters.reserve(9 * 32 * sizeof(unsigned)));
+    a.counters = ws.counters.as<unsigned>();
+    a.n_deferred = a.counters + 8 * 32;
+    MSH_HIP(hipMemsetAsync(a.counters, 0, 9 * 32 * sizeof(unsigned), s));
+    // pass 2 lanes carry up to kFront/64 dealt subtrees on top of a depth-first path
+    const unsigned nblk2 = ncu * 2u;
+    const int need = tree->max_depth + 1 + kFront / 64 + 1;
     a.spill = nullptr;
     a.spill_depth = 0;
-    if (tree->max_depth + 1 > kStack) {
-        a.spill_depth = tree->max_depth + 1 - kStack + 1;
-        MSH_TRY(tree->ws.spill.reserve((size_t)nblk * kBlock * (size_t)a.spill_depth * sizeof(uint2)));
-        a.spill = tree->ws.spill.as<uint2>();
+    if (need > kStack) {
+        a.spill_depth = need - kStack + 1;
+        MSH_TRY(ws.spill.reserve((size_t)std::max(nblk, nblk2) * kBlock * (size_t)a.spill_depth * sizeof(uint2)));
+        a.spill = ws.spill.as<uint2>();
     }
-    TimedLaunch tl(timer, s);
-    k_knn<MODE, STATS><<<nblk, kBlock, 0, s>>>(a);
-    MSH_HIP(hipGetLastError());
+    a.budget = STATS ? 0xFFFFFFFFu : kBudget;
+    a.max_deferred = (unsigned)std::min<size_t>(a.S, (a.S / 16) + 65536);
+    DevBuf& dbuf = ws.flags;
+    MSH_TRY(dbuf.reserve((size_t)a.max_deferred * sizeof(DeferRec)));
+    a.deferred = dbuf.as<DeferRec>();
+    {
+        TimedLaunch tl(timer, s);
+        k_knn<MODE, STATS><<<nblk, kBlock, 0, s>>>(a);
+        MSH_HIP(hipGetLastError());
+        if (!STATS) {
+            k_knn_coop<MODE><<<nblk2, kBlock, 0, s>>>(a);
+            MSH_HIP(hipGetLastError());
+        }
+    }
     return MSH_OK;
 }
 

@@ -97,11 +97,14 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
     }
     int node = 0, sp = 0;
     for (size_t guard = 0; guard < T; ++guard) {
-        const BNode nd = load_node(nodes, node);
+        const NodeV nd = load_node(nodes, node);
         double k0, k1;
-        bool h0 = pol.box(nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y, k0);
-        bool h1 = pol.box(nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w, k1);
-        const int c0 = nd.d.x, c1 = nd.d.y;
+        float l0[3], u0[3], l1[3], u1[3];
+        node_aabb(nd, 0, l0, u0);
+        node_aabb(nd, 1, l1, u1);
+        bool h0 = pol.box(l0[0], l0[1], l0[2], u0[0], u0[1], u0[2], k0);
+        bool h1 = pol.box(l1[0], l1[1], l1[2], u1[0], u1[1], u1[2], k1);
+        const int c0 = nd.child(0), c1 = nd.child(1);
         if (h0 && c0 < 0) {
             pol.test(~c0);
             h0 = false;
@@ -145,15 +148,16 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
 struct AlongPol {
     const TriRec* __restrict__ tris;
     D3 p, dp, dm;
+    D3 pr;  // p relative to the tree origin (node bounds are origin-relative)
     double best;  // distance
     uint32_t best_face;
     D3 best_pt;
     __device__ double lim2() const { return best == INFINITY ? INFINITY : best * best * kSlack; }
     __device__ bool box(float lx, float ly, float lz, float hx, float hy, float hz, double& key) const {
-        key = box_d2(p, lx, ly, lz, hx, hy, hz);
+        key = box_d2(pr, lx, ly, lz, hx, hy, hz);
         if (key > lim2()) return false;
         double tn;
-        return slab(p, dp, lx, ly, lz, hx, hy, hz, -INFINITY, INFINITY, tn);
+        return slab(pr, dp, lx, ly, lz, hx, hy, hz, -INFINITY, INFINITY, tn);
     }
     __device__ bool keep(double key) const { return key <= lim2(); }
     __device__ bool done() const { return false; }
@@ -181,9 +185,10 @@ struct AlongPol {
 struct AnyPol {
     const TriRec* __restrict__ tris;
     D3 src, d;
+    D3 sr;  // src relative to the tree origin
     bool hit;
     __device__ bool box(float lx, float ly, float lz, float hx, float hy, float hz, double& key) const {
-        return slab(src, d, lx, ly, lz, hx, hy, hz, 0.0, INFINITY, key);
+        return slab(sr, d, lx, ly, lz, hx, hy, hz, 0.0, INFINITY, key);
     }
     __device__ bool keep(double) const { return !hit; }
     __device__ bool done() const { return hit; }
@@ -222,6 +227,7 @@ struct RayArgs {
     unsigned ntiles;
     uint2* spill;
     int spill_depth;
+    double org[3];  // tree origin
 };
 
 __device__ inline unsigned dequeue_tile_r(unsigned* counters, unsigned ntiles, unsigned group) {
@@ -256,7 +262,8 @@ __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
             const size_t qi = a.perm ? (size_t)a.perm[i] : i;
             const D3 p = D3{a.p[3 * qi], a.p[3 * qi + 1], a.p[3 * qi + 2]};
             const D3 n = D3{a.n[3 * qi], a.n[3 * qi + 1], a.n[3 * qi + 2]};
-            AlongPol pol{a.tris, p, ray_dir(p, n), ray_dir(p, D3{-n.x, -n.y, -n.z}), INFINITY, 0xFFFFFFFFu,
+            AlongPol pol{a.tris, p, ray_dir(p, n), ray_dir(p, D3{-n.x, -n.y, -n.z}),
+                         D3{p.x - a.org[0], p.y - a.org[1], p.z - a.org[2]}, INFINITY, 0xFFFFFFFFu,
                          D3{NAN, NAN, NAN}};
             traverse_rays<AlongPol>(a.nodes, a.T, pol, lds, spill);
             a.out_dist[qi] = pol.best == INFINITY ? 1e100 : pol.best;
@@ -272,7 +279,7 @@ __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
             const double len = sqrt(vdot(dir, dir));
             dir = D3{dir.x / len, dir.y / len, dir.z / len};
             const D3 src = vadd(vv, vscale(a.min_dist, dir));
-            AnyPol pol{a.tris, src, ray_dir(src, dir), false};
+            AnyPol pol{a.tris, src, ray_dir(src, dir), D3{src.x - a.org[0], src.y - a.org[1], src.z - a.org[2]}, false};
             traverse_rays<AnyPol>(a.nodes, a.T, pol, lds, spill);
             const uint32_t reach = pol.hit ? 0u : 1u;
             a.ndc[i] = a.normals ? vdot(D3{a.normals[3 * iv], a.normals[3 * iv + 1], a.normals[3 * iv + 2]}, dir) : 0.0;
@@ -308,6 +315,7 @@ static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, c
         return MSH_EINVAL;
     }
     a.S = nrays;
+    for (int k = 0; k < 3; ++k) a.org[k] = tree->origin[k];
     a.ntiles = (unsigned)((nrays + 63) / 64);
     const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, (unsigned)device_cus_r(tree->device) * 5u);
     MSH_TRY(tree->ws.counters.reserve(8 * 32 * sizeof(unsigned)));

@@ -140,6 +140,7 @@ struct TriArgs {
     uint32_t* flags;
     uint2* spill;
     int spill_depth;
+    double org[3];  // tree origin
 };
 
 __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
@@ -151,8 +152,12 @@ __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
         D3 qa, qb, qc;
         uint32_t qface;
         load_tri(a.q, (int)i, qa, qb, qc, qface);
-        const double lo[3] = {fmin(fmin(qa.x, qb.x), qc.x), fmin(fmin(qa.y, qb.y), qc.y), fmin(fmin(qa.z, qb.z), qc.z)};
-        const double hi[3] = {fmax(fmax(qa.x, qb.x), qc.x), fmax(fmax(qa.y, qb.y), qc.y), fmax(fmax(qa.z, qb.z), qc.z)};
+        // query box relative to the tree origin (node bounds are origin-relative and padded >= 1 fp32 ulp,
+        // far above the fp64 rounding of this subtraction)
+        const double lo[3] = {fmin(fmin(qa.x, qb.x), qc.x) - a.org[0], fmin(fmin(qa.y, qb.y), qc.y) - a.org[1],
+                              fmin(fmin(qa.z, qb.z), qc.z) - a.org[2]};
+        const double hi[3] = {fmax(fmax(qa.x, qb.x), qc.x) - a.org[0], fmax(fmax(qa.y, qb.y), qc.y) - a.org[1],
+                              fmax(fmax(qa.z, qb.z), qc.z) - a.org[2]};
         bool hit = false;
         auto leaf_test = [&](int leaf) {
             D3 a0, a1, a2;
@@ -170,10 +175,13 @@ __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
         } else {
             int node = 0, sp = 0;
             for (size_t guard = 0; guard < a.T; ++guard) {
-                const BNode nd = load_node(a.nodes, node);
-                bool h0 = box_overlap(lo, hi, nd.a.x, nd.a.y, nd.a.z, nd.a.w, nd.b.x, nd.b.y);
-                bool h1 = box_overlap(lo, hi, nd.b.z, nd.b.w, nd.c.x, nd.c.y, nd.c.z, nd.c.w);
-                const int c0 = nd.d.x, c1 = nd.d.y;
+                const NodeV nd = load_node(a.nodes, node);
+                float l0[3], u0[3], l1[3], u1[3];
+                node_aabb(nd, 0, l0, u0);
+                node_aabb(nd, 1, l1, u1);
+                bool h0 = box_overlap(lo, hi, l0[0], l0[1], l0[2], u0[0], u0[1], u0[2]);
+                bool h1 = box_overlap(lo, hi, l1[0], l1[1], l1[2], u1[0], u1[1], u1[2]);
+                const int c0 = nd.child(0), c1 = nd.child(1);
                 if (h0 && c0 < 0) { leaf_test(~c0); h0 = false; if (hit) break; }
                 if (h1 && c1 < 0) { leaf_test(~c1); h1 = false; if (hit) break; }
                 if (h0 && h1) {
@@ -205,6 +213,7 @@ int launch_tri_intersect(const msh_tree* tree, const TriRec* d_qtris, size_t Tq,
     a.q = d_qtris;
     a.Tq = Tq;
     a.self_mode = self_mode;
+    for (int k = 0; k < 3; ++k) a.org[k] = tree->origin[k];
     a.flags = d_flags;
     int n = 0;
     if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, tree->device) != hipSuccess || n <= 0) n = 256;

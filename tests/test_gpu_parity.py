@@ -148,7 +148,10 @@ def test_c3_full_size_properties(oracle):
     dc = np.linalg.norm(cpt - q[idx], axis=1)
     assert np.all(np.abs(dg - dc) <= 1e-9 * diag)
     same = face[idx] == cf
-    assert same.mean() > 0.99 and np.all(np.abs(pt[idx][same] - cpt[same]) <= 1e-6 * diag)
+    # the icosphere is tie-heavy: queries outside project onto shared edges / vertices
+    assert same.mean() > 0.5
+    assert (pt[idx][same] == cpt[same]).all()
+    assert np.all(np.abs(pt[idx] - cpt) <= 1e-6 * diag)
 
 
 def test_normals_random_bit_exact(oracle):
@@ -318,6 +321,21 @@ def test_queries_on_vertices_and_edges(oracle):
     _assert_bit_exact_vs_brute(oracle, v, f, q)
 
 
+def test_cooperative_pass_near_centre(oracle):
+    # queries near the centre of a closed sphere exceed the pass-1 step budget and are finished by the
+    # wave-cooperative pass 2 (bound shared across lanes); the result must still be the exact lexmin
+    v, f = W.geodesic_icosphere(40)  # 32,000 faces
+    rng = np.random.default_rng(25)
+    q = np.vstack([rng.normal(size=(3000, 3)) * 0.02, rng.uniform(-1.1, 1.1, (3000, 3)), np.zeros((1, 3))])
+    _assert_bit_exact_vs_brute(oracle, v, f, q)
+    from mesh_amd import aabb_normals
+    n = rng.normal(size=q.shape)
+    n /= np.linalg.norm(n, axis=1)[:, None]
+    face, pt = aabb_normals.aabbtree_n_nearest(aabb_normals.aabbtree_n_compute(v, f, 0.1), q, n)
+    bf, bpt, _ = oracle.brute_nnearest(v, f, 0.1, q, n)
+    assert np.array_equal(face[0], bf) and np.array_equal(pt, bpt)
+
+
 def test_deep_tree_spill_path(oracle):
     # a mesh whose LBVH is deeper than the 16-entry LDS stack (clustered + spread triangles)
     rng = np.random.default_rng(22)
@@ -367,3 +385,20 @@ def test_device_api_matches_host_api():
     assert np.array_equal(df.cpu().numpy().view(np.uint32), face[0])
     assert np.array_equal(dp.cpu().numpy().view(np.uint32), part[0])
     assert np.array_equal(dpt.cpu().numpy(), pt)
+
+
+@pytest.mark.parametrize("name", ["ico", "c2", "offset"])
+def test_tree_bounds_contain_primitives(name):
+    # every child AABB and oriented box (frame n, t, n x t) contains all vertices below it
+    from scripts.check_tree import check_mesh
+    if name == "ico":
+        v, f = W.geodesic_icosphere(20)
+    elif name == "c2":
+        v, f = W.c2_mesh()
+    else:
+        v, f = W.geodesic_icosphere(10)
+        v = v * 0.01 + np.array([1e5, -3e4, 2e5])
+    r = check_mesh(v, f)
+    assert r["aabb_containment_violations"] == 0 and r["obb_containment_violations"] == 0, r
+    assert r["reached_nodes"] == f.shape[0] - 1
+    assert r["worst_relative_aabb_looseness_first2000"] < 1e-3, r

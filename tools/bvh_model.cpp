@@ -1,0 +1,407 @@
+// Host-side performance model of the traversal (development tool, not product code): builds the same
+// Karras LBVH as mesh_amd/csrc/build.hip (30-bit Morton codes of box centres in the scene box, stable
+// sort, Karras emission, exact subtree boxes) or alternative trees, and replays the near-first
+// closest-point traversal to count node visits / leaf tests per query.  Used to choose tree layouts
+// without spending GPU time.
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <numeric>
+#include <vector>
+
+namespace {
+
+struct Node {
+    double lo[2][3], hi[2][3];
+    int c[2];
+};
+
+struct Tree {
+    std::vector<Node> nodes;
+    std::vector<int> order;  // leaf position -> face
+    int root_leaf = -1;
+};
+
+uint32_t ex10(uint32_t v) {
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+
+int delta(const std::vector<uint32_t>& k, int n, int i, int j) {
+    if (j < 0 || j >= n) return -1;
+    if (k[i] != k[j]) return __builtin_clz(k[i] ^ k[j]);
+    return 32 + __builtin_clz((uint32_t)i ^ (uint32_t)j);
+}
+
+void prim_bounds(const double* v, const uint32_t* f, int T, std::vector<double>& lo, std::vector<double>& hi) {
+    lo.resize(3 * T);
+    hi.resize(3 * T);
+    for (int t = 0; t < T; ++t)
+        for (int k = 0; k < 3; ++k) {
+            double a = v[3 * f[3 * t] + k], b = v[3 * f[3 * t + 1] + k], c = v[3 * f[3 * t + 2] + k];
+            lo[3 * t + k] = std::min(std::min(a, b), c);
+            hi[3 * t + k] = std::max(std::max(a, b), c);
+        }
+}
+
+void fill_boxes(Tree& tr, int x, const std::vector<double>& plo, const std::vector<double>& phi, double* olo, double* ohi) {
+    for (int s = 0; s < 2; ++s) {
+        int c = tr.nodes[x].c[s];
+        double clo[3], chi[3];
+        if (c >= 0) fill_boxes(tr, c, plo, phi, clo, chi);
+        else {
+            int f = tr.order[~c];
+            for (int k = 0; k < 3; ++k) { clo[k] = plo[3 * f + k]; chi[k] = phi[3 * f + k]; }
+        }
+        for (int k = 0; k < 3; ++k) { tr.nodes[x].lo[s][k] = clo[k]; tr.nodes[x].hi[s][k] = chi[k]; }
+    }
+    for (int k = 0; k < 3; ++k) {
+        olo[k] = std::min(tr.nodes[x].lo[0][k], tr.nodes[x].lo[1][k]);
+        ohi[k] = std::max(tr.nodes[x].hi[0][k], tr.nodes[x].hi[1][k]);
+    }
+}
+
+Tree build_lbvh(const double* v, const uint32_t* f, int T) {
+    std::vector<double> lo, hi;
+    prim_bounds(v, f, T, lo, hi);
+    double box[6] = {1e300, 1e300, 1e300, -1e300, -1e300, -1e300};
+    for (int t = 0; t < T; ++t)
+        for (int k = 0; k < 3; ++k) { box[k] = std::min(box[k], lo[3 * t + k]); box[3 + k] = std::max(box[3 + k], hi[3 * t + k]); }
+    std::vector<uint32_t> key(T);
+    for (int t = 0; t < T; ++t) {
+        uint32_t c[3];
+        for (int k = 0; k < 3; ++k) {
+            double e = box[3 + k] - box[k];
+            double m = 0.5 * (lo[3 * t + k] + hi[3 * t + k]);
+            double nrm = e > 0 ? (m - box[k]) / e : 0.5;
+            nrm = std::min(std::max(nrm * 1024.0, 0.0), 1023.0);
+            c[k] = (uint32_t)nrm;
+        }
+        key[t] = (ex10(c[0]) << 2) | (ex10(c[1]) << 1) | ex10(c[2]);
+    }
+    Tree tr;
+    tr.order.resize(T);
+    std::iota(tr.order.begin(), tr.order.end(), 0);
+    std::stable_sort(tr.order.begin(), tr.order.end(), [&](int a, int b) { return key[a] < key[b]; });
+    std::vector<uint32_t> sk(T);
+    for (int i = 0; i < T; ++i) sk[i] = key[tr.order[i]];
+    if (T == 1) { tr.root_leaf = 0; return tr; }
+    tr.nodes.resize(T - 1);
+    for (int i = 0; i < T - 1; ++i) {
+        int d = (delta(sk, T, i, i + 1) - delta(sk, T, i, i - 1)) >= 0 ? 1 : -1;
+        int dmin = delta(sk, T, i, i - d);
+        int lmax = 2;
+        while (delta(sk, T, i, i + lmax * d) > dmin) lmax <<= 1;
+        int l = 0;
+        for (int t = lmax >> 1; t >= 1; t >>= 1)
+            if (delta(sk, T, i, i + (l + t) * d) > dmin) l += t;
+        int j = i + l * d;
+        int dn = delta(sk, T, i, j);
+        int s = 0, t = l;
+        do {
+            t = (t + 1) >> 1;
+            if (delta(sk, T, i, i + (s + t) * d) > dn) s += t;
+        } while (t > 1);
+        int g = i + s * d + (d < 0 ? -1 : 0);
+        tr.nodes[i].c[0] = (std::min(i, j) == g) ? ~g : g;
+        tr.nodes[i].c[1] = (std::max(i, j) == g + 1) ? ~(g + 1) : g + 1;
+    }
+    double a[3], b[3];
+    fill_boxes(tr, 0, lo, hi, a, b);
+    return tr;
+}
+
+// median split on the longest axis of the centroid box (CGAL-like), leaves are single triangles
+int build_median_rec(Tree& tr, std::vector<int>& idx, int b, int e, const std::vector<double>& lo,
+                     const std::vector<double>& hi) {
+    if (e - b == 1) return ~b;
+    int node = (int)tr.nodes.size();
+    tr.nodes.push_back(Node{});
+    double cl[3] = {1e300, 1e300, 1e300}, ch[3] = {-1e300, -1e300, -1e300};
+    for (int i = b; i < e; ++i)
+        for (int k = 0; k < 3; ++k) {
+            double c = 0.5 * (lo[3 * idx[i] + k] + hi[3 * idx[i] + k]);
+            cl[k] = std::min(cl[k], c);
+            ch[k] = std::max(ch[k], c);
+        }
+    int ax = 0;
+    for (int k = 1; k < 3; ++k) if (ch[k] - cl[k] > ch[ax] - cl[ax]) ax = k;
+    int m = (b + e) / 2;
+    std::nth_element(idx.begin() + b, idx.begin() + m, idx.begin() + e, [&](int x, int y) {
+        return lo[3 * x + ax] + hi[3 * x + ax] < lo[3 * y + ax] + hi[3 * y + ax];
+    });
+    int l = build_median_rec(tr, idx, b, m, lo, hi);
+    int r = build_median_rec(tr, idx, m, e, lo, hi);
+    tr.nodes[node].c[0] = l;
+    tr.nodes[node].c[1] = r;
+    return node;
+}
+
+Tree build_median(const double* v, const uint32_t* f, int T) {
+    std::vector<double> lo, hi;
+    prim_bounds(v, f, T, lo, hi);
+    Tree tr;
+    std::vector<int> idx(T);
+    std::iota(idx.begin(), idx.end(), 0);
+    if (T == 1) { tr.order = idx; tr.root_leaf = 0; return tr; }
+    build_median_rec(tr, idx, 0, T, lo, hi);
+    tr.order = idx;
+    double a[3], b[3];
+    fill_boxes(tr, 0, lo, hi, a, b);
+    return tr;
+}
+
+double box_d2(const double* q, const double* lo, const double* hi) {
+    double s = 0;
+    for (int k = 0; k < 3; ++k) {
+        double g = std::max(std::max(lo[k] - q[k], q[k] - hi[k]), 0.0);
+        s += g * g;
+    }
+    return s;
+}
+
+double seg_d2(const double* p, const double* a, const double* b) {
+    double ab[3], ap[3];
+    for (int k = 0; k < 3; ++k) { ab[k] = b[k] - a[k]; ap[k] = p[k] - a[k]; }
+    double den = ab[0] * ab[0] + ab[1] * ab[1] + ab[2] * ab[2];
+    double t = den > 0 ? (ap[0] * ab[0] + ap[1] * ab[1] + ap[2] * ab[2]) / den : 0;
+    t = std::min(std::max(t, 0.0), 1.0);
+    double d = 0;
+    for (int k = 0; k < 3; ++k) { double x = a[k] + t * ab[k] - p[k]; d += x * x; }
+    return d;
+}
+
+double tri_d2(const double* p, const double* a, const double* b, const double* c) {
+    double ab[3], ac[3], n[3];
+    for (int k = 0; k < 3; ++k) { ab[k] = b[k] - a[k]; ac[k] = c[k] - a[k]; }
+    n[0] = ab[1] * ac[2] - ab[2] * ac[1]; n[1] = ab[2] * ac[0] - ab[0] * ac[2]; n[2] = ab[0] * ac[1] - ab[1] * ac[0];
+    double nn = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+    double best = std::min(seg_d2(p, a, b), std::min(seg_d2(p, b, c), seg_d2(p, c, a)));
+    if (nn > 0) {
+        double ap[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+        double s = (ap[0] * n[0] + ap[1] * n[1] + ap[2] * n[2]) / nn;
+        double pr[3] = {p[0] - s * n[0] - a[0], p[1] - s * n[1] - a[1], p[2] - s * n[2] - a[2]};
+        double d00 = ab[0] * ab[0] + ab[1] * ab[1] + ab[2] * ab[2], d01 = ab[0] * ac[0] + ab[1] * ac[1] + ab[2] * ac[2];
+        double d11 = ac[0] * ac[0] + ac[1] * ac[1] + ac[2] * ac[2];
+        double d20 = pr[0] * ab[0] + pr[1] * ab[1] + pr[2] * ab[2], d21 = pr[0] * ac[0] + pr[1] * ac[1] + pr[2] * ac[2];
+        double den = d00 * d11 - d01 * d01;
+        double vv = (d11 * d20 - d01 * d21) / den, w = (d00 * d21 - d01 * d20) / den;
+        if (vv >= 0 && w >= 0 && vv + w <= 1) best = std::min(best, s * s * nn);
+    }
+    return best;
+}
+
+}  // namespace
+
+extern "C" {
+
+// kind 0 = LBVH (as built on the GPU), 1 = median split.  Outputs per-query node visits and leaf tests.
+void model_counts(const double* v, const uint32_t* f, int T, const double* q, long S, int kind, uint32_t* nodes_out,
+                  uint32_t* leaves_out, int* depth_out) {
+    Tree tr = kind == 0 ? build_lbvh(v, f, T) : build_median(v, f, T);
+    // depth
+    int maxd = 0;
+    {
+        std::vector<std::pair<int, int>> st{{0, 1}};
+        while (!st.empty()) {
+            auto [x, d] = st.back();
+            st.pop_back();
+            for (int s = 0; s < 2; ++s) {
+                int c = tr.nodes[x].c[s];
+                if (c >= 0) st.push_back({c, d + 1});
+                else maxd = std::max(maxd, d);
+            }
+        }
+    }
+    *depth_out = maxd;
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long i = 0; i < S; ++i) {
+        const double* qq = q + 3 * i;
+        double best = std::numeric_limits<double>::infinity();
+        uint32_t nn = 0, nl = 0;
+        std::vector<std::pair<int, double>> st;
+        int node = 0;
+        for (;;) {
+            const Node& n = tr.nodes[node];
+            ++nn;
+            double d[2];
+            bool h[2];
+            for (int s = 0; s < 2; ++s) {
+                d[s] = box_d2(qq, n.lo[s], n.hi[s]);
+                h[s] = d[s] <= best;
+                if (h[s] && n.c[s] < 0) {
+                    int fc = tr.order[~n.c[s]];
+                    const uint32_t* ff = f + 3 * fc;
+                    best = std::min(best, tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                    ++nl;
+                    h[s] = false;
+                }
+            }
+            h[0] = h[0] && d[0] <= best;
+            h[1] = h[1] && d[1] <= best;
+            if (h[0] && h[1]) {
+                int nr = d[1] < d[0] ? 1 : 0;
+                st.push_back({n.c[1 - nr], d[1 - nr]});
+                node = n.c[nr];
+                continue;
+            }
+            if (h[0]) { node = n.c[0]; continue; }
+            if (h[1]) { node = n.c[1]; continue; }
+            bool found = false;
+            while (!st.empty()) {
+                auto e = st.back();
+                st.pop_back();
+                if (e.second <= best) { node = e.first; found = true; break; }
+            }
+            if (!found) break;
+        }
+        nodes_out[i] = nn;
+        leaves_out[i] = nl;
+    }
+}
+}
+
+// ---- OBB experiment: per child an oriented box aligned with the area-weighted normal of its triangles
+namespace {
+struct OBB {
+    double ax[3][3];  // rows: unit axes
+    double lo[3], hi[3];
+};
+void range_of(const Tree& tr, int c, int& b, int& e) {
+    // leaves of the subtree rooted at c are contiguous in Morton order for the LBVH: find extremes
+    if (c < 0) { b = e = ~c; return; }
+    int lb, le, rb, re;
+    range_of(tr, tr.nodes[c].c[0], lb, le);
+    range_of(tr, tr.nodes[c].c[1], rb, re);
+    b = std::min(lb, rb);
+    e = std::max(le, re);
+}
+OBB make_obb(const Tree& tr, const double* v, const uint32_t* f, int b, int e, int mode) {
+    OBB o;
+    double n[3] = {0, 0, 0};
+    for (int i = b; i <= e; ++i) {
+        const uint32_t* ff = f + 3 * tr.order[i];
+        const double *A = v + 3 * ff[0], *B = v + 3 * ff[1], *C = v + 3 * ff[2];
+        double ab[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, ac[3] = {C[0] - A[0], C[1] - A[1], C[2] - A[2]};
+        n[0] += ab[1] * ac[2] - ab[2] * ac[1]; n[1] += ab[2] * ac[0] - ab[0] * ac[2]; n[2] += ab[0] * ac[1] - ab[1] * ac[0];
+    }
+    double nl = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    if (mode == 0 || !(nl > 0)) { n[0] = 1; n[1] = 0; n[2] = 0; nl = 1; }
+    for (int k = 0; k < 3; ++k) o.ax[0][k] = n[k] / nl;
+    double t[3] = {0, 0, 0};
+    int m = std::fabs(o.ax[0][0]) < 0.9 ? 0 : 1;
+    t[m] = 1;
+    // t1 = normalize(t - (t.n) n)
+    double d = t[0] * o.ax[0][0] + t[1] * o.ax[0][1] + t[2] * o.ax[0][2];
+    for (int k = 0; k < 3; ++k) t[k] -= d * o.ax[0][k];
+    double tl = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+    for (int k = 0; k < 3; ++k) o.ax[1][k] = t[k] / tl;
+    o.ax[2][0] = o.ax[0][1] * o.ax[1][2] - o.ax[0][2] * o.ax[1][1];
+    o.ax[2][1] = o.ax[0][2] * o.ax[1][0] - o.ax[0][0] * o.ax[1][2];
+    o.ax[2][2] = o.ax[0][0] * o.ax[1][1] - o.ax[0][1] * o.ax[1][0];
+    for (int a = 0; a < 3; ++a) { o.lo[a] = 1e300; o.hi[a] = -1e300; }
+    for (int i = b; i <= e; ++i) {
+        const uint32_t* ff = f + 3 * tr.order[i];
+        for (int c = 0; c < 3; ++c) {
+            const double* P = v + 3 * ff[c];
+            for (int a = 0; a < 3; ++a) {
+                double p = P[0] * o.ax[a][0] + P[1] * o.ax[a][1] + P[2] * o.ax[a][2];
+                o.lo[a] = std::min(o.lo[a], p);
+                o.hi[a] = std::max(o.hi[a], p);
+            }
+        }
+    }
+    return o;
+}
+double obb_d2(const double* q, const OBB& o) {
+    double s = 0;
+    for (int a = 0; a < 3; ++a) {
+        double p = q[0] * o.ax[a][0] + q[1] * o.ax[a][1] + q[2] * o.ax[a][2];
+        double g = std::max(std::max(o.lo[a] - p, p - o.hi[a]), 0.0);
+        s += g * g;
+    }
+    return s;
+}
+}  // namespace
+
+extern "C" void model_counts_obb(const double* v, const uint32_t* f, int T, const double* q, long S, int mode,
+                                 uint32_t* nodes_out, uint32_t* leaves_out) {
+    Tree tr = build_lbvh(v, f, T);
+    std::vector<OBB> ob(2 * (T - 1));
+    for (int x = 0; x < T - 1; ++x) {
+        int pb, pe;
+        range_of(tr, x, pb, pe);
+        OBB parent = make_obb(tr, v, f, pb, pe, 1);
+        for (int s = 0; s < 2; ++s) {
+            int b, e;
+            range_of(tr, tr.nodes[x].c[s], b, e);
+            if (mode == 3 || mode == 4) {
+                OBB o = parent;
+                for (int a = 0; a < 3; ++a) { o.lo[a] = 1e300; o.hi[a] = -1e300; }
+                for (int i = b; i <= e; ++i) {
+                    const uint32_t* ff = f + 3 * tr.order[i];
+                    for (int c = 0; c < 3; ++c) {
+                        const double* P = v + 3 * ff[c];
+                        for (int a = 0; a < 3; ++a) {
+                            double pp = P[0] * o.ax[a][0] + P[1] * o.ax[a][1] + P[2] * o.ax[a][2];
+                            o.lo[a] = std::min(o.lo[a], pp); o.hi[a] = std::max(o.hi[a], pp);
+                        }
+                    }
+                }
+                ob[2 * x + s] = o;
+            } else {
+                ob[2 * x + s] = make_obb(tr, v, f, b, e, 1);
+            }
+        }
+    }
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long i = 0; i < S; ++i) {
+        const double* qq = q + 3 * i;
+        double best = std::numeric_limits<double>::infinity();
+        uint32_t nn = 0, nl = 0;
+        std::vector<std::pair<int, double>> st;
+        int node = 0;
+        for (;;) {
+            const Node& n = tr.nodes[node];
+            ++nn;
+            double d[2];
+            bool h[2];
+            for (int s = 0; s < 2; ++s) {
+                d[s] = (mode == 1 || mode == 4) ? std::max(box_d2(qq, n.lo[s], n.hi[s]), obb_d2(qq, ob[2 * node + s]))
+                                                 : obb_d2(qq, ob[2 * node + s]);
+                h[s] = d[s] <= best;
+                if (h[s] && n.c[s] < 0) {
+                    int fc = tr.order[~n.c[s]];
+                    const uint32_t* ff = f + 3 * fc;
+                    best = std::min(best, tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                    ++nl;
+                    h[s] = false;
+                }
+            }
+            h[0] = h[0] && d[0] <= best;
+            h[1] = h[1] && d[1] <= best;
+            if (h[0] && h[1]) {
+                int nr = d[1] < d[0] ? 1 : 0;
+                st.push_back({n.c[1 - nr], d[1 - nr]});
+                node = n.c[nr];
+                continue;
+            }
+            if (h[0]) { node = n.c[0]; continue; }
+            if (h[1]) { node = n.c[1]; continue; }
+            bool found = false;
+            while (!st.empty()) {
+                auto e = st.back();
+                st.pop_back();
+                if (e.second <= best) { node = e.first; found = true; break; }
+            }
+            if (!found) break;
+        }
+        nodes_out[i] = nn;
+        leaves_out[i] = nl;
+    }
+}
