@@ -238,6 +238,40 @@ struct Walker {
         if (h1) { node = c1; return true; }
         return pop(pol, lds, spill);
     }
+    // As step(), but leaf children that survive the bound are handed back in p0/p1 instead of being
+    // tested here, so the caller can run leaf tests for many lanes of the wave at once.
+    template <class Pol, bool STATS>
+    __device__ inline bool step_collect(const BNode* __restrict__ nodes, const QF& qf, const Pol& pol,
+                                        uint2* __restrict__ lds, uint2* __restrict__ spill, unsigned& n_nodes, int& p0,
+                                        int& p1) {
+        const NodeV nd = load_node(nodes, node);
+        if (STATS) ++n_nodes;
+        float d0, d1;
+        node_child_bounds(nd, qf, d0, d1);
+        const int c0 = nd.child(0), c1 = nd.child(1);
+        const float lim = __double2float_ru(pol.limit());
+        bool h0 = d0 <= lim, h1 = d1 <= lim;
+        if (h0 && c0 < 0) {
+            p0 = ~c0;
+            h0 = false;
+        }
+        if (h1 && c1 < 0) {
+            if (p0 < 0) p0 = ~c1;
+            else p1 = ~c1;
+            h1 = false;
+        }
+        if (h0 && h1) {
+            int nearc = c0, farc = c1;
+            float dfar = d1;
+            if (d1 < d0) { nearc = c1; farc = c0; dfar = d0; }
+            push(make_uint2((unsigned)farc, __float_as_uint(dfar)), lds, spill);
+            node = nearc;
+            return true;
+        }
+        if (h0) { node = c0; return true; }
+        if (h1) { node = c1; return true; }
+        return pop(pol, lds, spill);
+    }
 };
 
 // Outputs of one query from its policy (winner's leaf -> point / part recomputed exactly).
@@ -318,33 +352,57 @@ __global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
         } else {
             const QF qf = make_qf(q, a.org);
             Walker w{0, 0};
-            bool active = true;
+            bool active = true, deferred = false;
+            int p0 = -1, p1 = -1;  // leaf children waiting for a wave-wide leaf phase
             size_t steps = 0;
-            while (active) {
-                active = w.step<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, n_leaves);
-                ++steps;
-                if (!active) break;
-                if (steps >= a.T) {  // each internal node is entered at most once: corrupt tree, stop
-                    active = false;
-                    break;
-                }
-                if (steps == a.budget) {
-                    const unsigned slot = atomicAdd(a.n_deferred, 1u);
-                    if (slot < a.max_deferred) {
-                        DeferRec r;
-                        r.qi = (uint32_t)qi;
-                        r.face = pol.best_face;
-                        r.leaf = pol.best_leaf;
-                        r.pad = 0;
-                        r.best = pol.best;
-                        r.pad2 = 0;
-                        a.deferred[slot] = r;
-                        break;  // active stays true: pass 2 owns this query
+            // Wave-synchronous loop.  Lanes that reach leaves park them; leaf tests run when the
+            // parked lanes are at least a third of the busy ones (or nobody can traverse), so the
+            // expensive fp64 leaf path executes for many lanes at once instead of stalling the wave
+            // on one lane every iteration (Aila & Laine 2009, "postponed leaf" while-while).
+            for (;;) {
+                const bool parked = p0 >= 0;
+                const unsigned long long bp = __ballot(parked);
+                const unsigned long long bt = __ballot(active && !parked);
+                if ((bp | bt) == 0ull) break;
+                const int np = __popcll(bp), nt = __popcll(bt);
+                if (np > 0 && (nt == 0 || 2 * np >= nt)) {
+                    if (parked) {
+                        pol.test(p0);
+                        if (STATS) ++n_leaves;
+                        if (p1 >= 0) {
+                            pol.test(p1);
+                            if (STATS) ++n_leaves;
+                        }
+                        p0 = p1 = -1;
                     }
-                    // deferred list full: finish here without a budget
+                    continue;
+                }
+                if (active && !parked) {
+                    active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, p0, p1);
+                    ++steps;
+                    if (active && steps >= a.T) active = false;  // each node is entered once: corrupt tree
+                    if (active && steps == a.budget) {
+                        const unsigned slot = atomicAdd(a.n_deferred, 1u);
+                        if (slot < a.max_deferred) {
+                            if (p0 >= 0) pol.test(p0);
+                            if (p1 >= 0) pol.test(p1);
+                            p0 = p1 = -1;
+                            DeferRec r;
+                            r.qi = (uint32_t)qi;
+                            r.face = pol.best_face;
+                            r.leaf = pol.best_leaf;
+                            r.pad = 0;
+                            r.best = pol.best;
+                            r.pad2 = 0;
+                            a.deferred[slot] = r;
+                            active = false;
+                            deferred = true;  // pass 2 owns this query
+                        }
+                        // deferred list full: finish here without a budget
+                    }
                 }
             }
-            if (active) continue;  // deferred: pass 2 writes this query
+            if (deferred) continue;
         }
         if (!STATS) write_result<MODE>(a, qi, q, pol);
     }

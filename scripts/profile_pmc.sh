@@ -1,0 +1,23 @@
+#!/bin/bash
+# rocprofv3 passes on the bench (C3 workload): kernel-trace --stats (CSV), then one PMC pass per counter
+# group (FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum+TCC_MISS_sum cannot share a pass on gfx950).  Run on the
+# GPU box from the repo root; outputs under gpurun_out/pmc/.  Stops at the first failing step.
+set -u
+R=$(cd "$(dirname "$0")/.." && pwd)
+OUT=$R/gpurun_out/pmc
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+Q=${Q:-100000000}
+run() {
+  local name=$1; shift
+  timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 "$R/bench.py" --queries $Q --steps 2 --warmup 1 --no-cpu > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc" | tee -a "$OUT/status.txt"
+  [ $rc -eq 0 ] || exit $rc
+}
+: > "$OUT/status.txt"
+run stats --kernel-trace --stats
+run fetch --kernel-trace --pmc FETCH_SIZE
+run write --kernel-trace --pmc WRITE_SIZE
+run tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum
+echo done | tee -a "$OUT/status.txt"
