@@ -144,6 +144,7 @@ static void free_tree(msh_tree* t) {
     t->ws.release();
     if (t->d_v) (void)hipFree(t->d_v);
     if (t->d_nodes) (void)hipFree(t->d_nodes);
+    if (t->d_nodes4) (void)hipFree(t->d_nodes4);
     if (t->d_leaves) (void)hipFree(t->d_leaves);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
@@ -194,6 +195,7 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
                                   static_cast<TriRec*>(t->d_leaves), s)) != MSH_OK)
             break;
         if ((st = build_obb(t, true)) != MSH_OK) break;
+        if ((st = build_bvh4(t)) != MSH_OK) break;
         (void)hipEventRecord(e1, s);
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) { set_error("LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
@@ -350,6 +352,7 @@ int msh_points_build(const double* v, size_t P, msh_tree** out) {
         if ((st = pack_point_leaves(t->d_v, dOrder.as<uint32_t>(), P, static_cast<PtRec*>(t->d_leaves), s)) != MSH_OK)
             break;
         if ((st = build_obb(t, false)) != MSH_OK) break;
+        if ((st = build_bvh4(t)) != MSH_OK) break;
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) { set_error("point LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
     } while (0);
@@ -426,14 +429,17 @@ int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* n
     hipStream_t s = t->stream;
     const uint32_t* perm = nullptr;
     MSH_TRY(sort_queries(t, d_q, S, s, &perm));
-    MSH_TRY(t->ws.stats.reserve(2 * sizeof(unsigned long long)));
-    MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, 2 * sizeof(unsigned long long), s));
+    MSH_TRY(t->ws.stats.reserve(8 * sizeof(unsigned long long)));
+    MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, 8 * sizeof(unsigned long long), s));
     MSH_TRY(launch_nearest_stats(t, d_q, perm, S, t->ws.stats.as<unsigned long long>(), s));
-    unsigned long long h[2] = {0, 0};
+    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     MSH_HIP(hipMemcpyAsync(h, t->ws.stats.ptr, sizeof(h), hipMemcpyDeviceToHost, s));
     MSH_HIP(hipStreamSynchronize(s));
     *nodes = h[0];
     *leaves = h[1];
+    if (getenv("MESH_AMD_STATS_DUMP"))  // development: wave-iteration utilisation of pass 1
+        fprintf(stderr, "[msh stats] S=%zu nodes=%llu leaves=%llu trav_it=%llu trav_lanes=%llu leaf_it=%llu "
+                        "leaf_lanes=%llu exact=%llu\n", S, h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
     return MSH_OK;
 }
 
@@ -727,7 +733,14 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
         if (e != hipSuccess) {
             set_error("blob unpack: %s", hipGetErrorString(e));
             st = MSH_EDEVICE;
+            break;
         }
+        st = build_bvh4(t);  // the 4-wide nearest-query nodes are derived, not shipped
+        if (st == MSH_OK && hipStreamSynchronize(t->stream) != hipSuccess) {
+            set_error("blob unpack: 4-wide node build failed");
+            st = MSH_EDEVICE;
+        }
+        t->ws.release();
     } while (0);
     if (st != MSH_OK) {
         std::string keep = g_err;

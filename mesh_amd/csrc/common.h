@@ -22,7 +22,10 @@
 namespace msh {
 
 constexpr int kBlock = 256;          // 4 waves of 64 lanes
-constexpr int kStack = 16;           // per-lane LDS stack entries; deeper entries spill to global memory
+#ifndef MSH_STACK
+#define MSH_STACK 16
+#endif
+constexpr int kStack = MSH_STACK;           // per-lane LDS stack entries; deeper entries spill to global memory
 constexpr double kSlack = 1.0 + 9.094947017729282e-13;  // 1 + 2^-40: fp64 rounding margin for culls
 
 // float index within a node:  0-2 n | 3-5 t | 6 child0 | 7 child1 |
@@ -32,6 +35,7 @@ struct alignas(16) BNode {
     float f[32];
 };
 static_assert(sizeof(BNode) == 128, "BNode must be 128 B");
+constexpr int kEmpty4 = 0x7FFFFFFF;  // empty slot of a 4-wide node half
 constexpr int kAabb[2] = {8, 20};
 constexpr int kObb[2] = {14, 26};
 
@@ -215,6 +219,9 @@ __device__ inline QF make_qf(const D3& q, const double* origin) {
 // Lower bound of the squared distance from q to an fp32 box: per-axis gaps are shrunk by the fp32
 // subtraction error (<= 2^-24 relative) and the query rounding error, the sum by 3 roundings (2^-21).
 __host__ __device__ inline float box_d2_lo(const QF& q, float lx, float ly, float lz, float hx, float hy, float hz) {
+#ifdef MSH_FP32_CONTRACT
+#pragma clang fp contract(fast)
+#endif
     const float k = 0.99999988079071044921875f;  // 1 - 2^-23
     float gx = fmaxf(fmaxf(lx - q.x, q.x - hx), 0.f);
     float gy = fmaxf(fmaxf(ly - q.y, q.y - hy), 0.f);
@@ -230,6 +237,9 @@ __host__ __device__ inline float box_d2_lo(const QF& q, float lx, float ly, floa
 // 2^-24 relative, and the sum of squared slab gaps is divided by lambda_max(A A^T) <= 1 + 1e-6 (fp32
 // axes), covered by the factor 1 - 2^-18.
 __host__ __device__ inline float obb_d2_lo(const QF& q, const float* n, const float* t, const float* b, const float* ext) {
+#ifdef MSH_FP32_CONTRACT
+#pragma clang fp contract(fast)
+#endif
     const float k = 0.99999988079071044921875f;  // 1 - 2^-23
     const float pn = n[0] * q.x + n[1] * q.y + n[2] * q.z;
     const float pt = t[0] * q.x + t[1] * q.y + t[2] * q.z;
@@ -266,15 +276,15 @@ __device__ inline void node_child_bounds(const NodeV& nd, const QF& q, float& d0
 // relative to the query (Ericson's Voronoi-region closest point, evaluated in fp32).  For a triangle
 // whose smallest angle is not tiny the rounding error of the result is O(ulp * M / sin^2(angle)),
 // M = largest |coordinate|: triangles with sin^2 < 1e-2 return 0 (no rejection), a face-region
-// result outside the triangle returns 0, and the bound subtracts 2^-12 * M (>= 40x the error bound).
+// result outside the triangle returns 0, and the bound subtracts 2^-15 * M (see the margin note).
 // NaN (degenerate input) also propagates, which callers treat as "cannot reject".
 __host__ __device__ inline float tri_d2_lo(float ax, float ay, float az, float bx, float by, float bz, float cx, float cy,
                                            float cz) {
     const float abx = bx - ax, aby = by - ay, abz = bz - az;
     const float acx = cx - ax, acy = cy - ay, acz = cz - az;
+    const float nx = aby * acz - abz * acy, ny = abz * acx - abx * acz, nz = abx * acy - aby * acx;
+    const float n2 = nx * nx + ny * ny + nz * nz;
     {
-        const float nx = aby * acz - abz * acy, ny = abz * acx - abx * acz, nz = abx * acy - aby * acx;
-        const float n2 = nx * nx + ny * ny + nz * nz;
         const float l2 = (abx * abx + aby * aby + abz * abz) * (acx * acx + acy * acy + acz * acz);
         if (!(n2 >= 1e-2f * l2)) return 0.f;  // sliver or degenerate (also catches NaN / 0)
     }
@@ -299,14 +309,21 @@ __host__ __device__ inline float tri_d2_lo(float ax, float ay, float az, float b
         const float t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
         px = bx + t * (cx - bx); py = by + t * (cy - by); pz = bz + t * (cz - bz);
     } else {
-        const float den = 1.f / (va + vb + vc);
-        const float v = vb * den, w = vc * den;
+        // face region: the distance to the supporting plane, |n . a| / |n|, is a lower bound of the
+        // distance to the triangle whatever the true region, and it avoids the cancellation of the
+        // barycentric reconstruction (2^-15 M observed there vs 2^-22 M for the plane distance)
+        const float den = va + vb + vc;
+        const float v = vb / den, w = vc / den;
         if (!(v >= -1e-3f && w >= -1e-3f && v + w <= 1.001f)) return 0.f;
-        px = ax + abx * v + acx * w; py = ay + aby * v + acy * w; pz = az + abz * v + acz * w;
+        const float h = fabsf(nx * ax + ny * ay + nz * az) / sqrtf(n2);
+        px = h; py = 0.f; pz = 0.f;
     }
     const float M = fmaxf(fmaxf(fmaxf(fabsf(ax), fabsf(ay)), fmaxf(fabsf(az), fabsf(bx))),
                           fmaxf(fmaxf(fabsf(by), fabsf(bz)), fmaxf(fmaxf(fabsf(cx), fabsf(cy)), fabsf(cz))));
-    const float d = sqrtf(px * px + py * py + pz * pz) - M * 2.44140625e-4f;  // 2^-12
+    // Margin: region classification and the vertex/edge constructions err by <= ~2^-24 M times the
+    // conditioning 1/sin^2 <= 100 (sliver guard above), i.e. ~2^-17.4 M; 2^-15 M leaves a 5x cushion
+    // (measured worst case over 10^7 random/adversarial cases: 2^-22 M, tests/csrc/pretest_check.cpp).
+    const float d = sqrtf(px * px + py * py + pz * pz) - M * 3.0517578125e-5f;  // 2^-15
     return d > 0.f ? d * d * 0.999999523162841796875f : (d <= 0.f ? 0.f : d);  // NaN propagates
 }
 

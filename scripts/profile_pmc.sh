@@ -16,8 +16,15 @@ run() {
   [ $rc -eq 0 ] || exit $rc
 }
 : > "$OUT/status.txt"
-run stats --kernel-trace --stats
-run fetch --kernel-trace --pmc FETCH_SIZE
-run write --kernel-trace --pmc WRITE_SIZE
-run tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum
+PASSES=${PASSES:-"stats fetch write tcc"}
+for p in $PASSES; do
+  case $p in
+    stats) run stats --kernel-trace --stats ;;
+    fetch) run fetch --kernel-trace --pmc FETCH_SIZE ;;
+    write) run write --kernel-trace --pmc WRITE_SIZE ;;
+    tcc)   run tcc --kernel-trace --pmc TCC_HIT_sum TCC_MISS_sum ;;
+    sq)    run sq --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_VALU ;;
+    sq2)   run sq2 --kernel-trace --pmc SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_BRANCH SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM ;;
+  esac
+done
 echo done | tee -a "$OUT/status.txt"

@@ -3,6 +3,8 @@
 // the exact fp64 squared distance (CGAL construction, mesh_amd/csrc/common.h closest_on_triangle is
 // device-only, so the exact value here comes from the oracle's formulas re-derived in long double).
 // Built with hipcc as host code; prints "violations=<n> checked=<m> rejected=<r>".
+// Kinds: random, sliver, near a vertex, near an edge, on the face, large offset, and above the
+// face/edge (6) and face/vertex (7) region boundaries, where a misclassified region matters most.
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -51,7 +53,7 @@ int main(int argc, char** argv) {
     std::uniform_real_distribution<double> U(0.0, 1.0);
     long viol = 0, rej = 0;
     for (long it = 0; it < n; ++it) {
-        const int kind = it % 6;
+        const int kind = it % 8;
         double scale = std::pow(10.0, -3 + 6 * U(rng));  // triangle size
         double off = std::pow(10.0, -4 + 8 * U(rng));    // query distance
         double q[3], t[9];
@@ -62,6 +64,18 @@ int main(int argc, char** argv) {
         if (kind == 3) for (int k = 0; k < 3; ++k) q[k] = 0.5 * (t[k] + t[3 + k]) + N(rng) * scale * 0.1;  // near an edge
         if (kind == 4) { double s = U(rng), r = U(rng) * (1 - s); for (int k = 0; k < 3; ++k) q[k] = t[k] + s * (t[3+k]-t[k]) + r * (t[6+k]-t[k]); }  // on face
         if (kind == 5) for (int k = 0; k < 9; ++k) t[k] += 1e6;  // large offset
+        if (kind == 6 || kind == 7) {
+            // above a point of the face/edge boundary (kind 6: on edge ab; kind 7: at vertex a) along the
+            // normal, with a lateral jitter around the region boundary: the misclassification case
+            double ab[3], ac[3], n[3];
+            for (int k = 0; k < 3; ++k) { ab[k] = t[3 + k] - t[k]; ac[k] = t[6 + k] - t[k]; }
+            n[0] = ab[1] * ac[2] - ab[2] * ac[1]; n[1] = ab[2] * ac[0] - ab[0] * ac[2]; n[2] = ab[0] * ac[1] - ab[1] * ac[0];
+            const double nl = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+            const double s = kind == 6 ? U(rng) : 0.0;
+            const double h = off * (U(rng) < 0.5 ? 1 : -1);
+            for (int k = 0; k < 3; ++k)
+                q[k] = t[k] + s * ab[k] + h * n[k] / nl + N(rng) * scale * std::pow(10.0, -7 + 6 * U(rng));
+        }
         float f[9];
         for (int c = 0; c < 3; ++c)
             for (int k = 0; k < 3; ++k) f[3 * c + k] = (float)(t[3 * c + k] - q[k]);

@@ -331,7 +331,8 @@ double obb_d2(const double* q, const OBB& o) {
 
 extern "C" void model_counts_obb(const double* v, const uint32_t* f, int T, const double* q, long S, int mode,
                                  uint32_t* nodes_out, uint32_t* leaves_out) {
-    Tree tr = build_lbvh(v, f, T);
+    Tree tr = mode >= 10 ? build_median(v, f, T) : build_lbvh(v, f, T);  // mode + 10: median-split tree
+    mode %= 10;
     std::vector<OBB> ob(2 * (T - 1));
     for (int x = 0; x < T - 1; ++x) {
         int pb, pe;
@@ -393,6 +394,193 @@ extern "C" void model_counts_obb(const double* v, const uint32_t* f, int T, cons
             }
             if (h[0]) { node = n.c[0]; continue; }
             if (h[1]) { node = n.c[1]; continue; }
+            bool found = false;
+            while (!st.empty()) {
+                auto e = st.back();
+                st.pop_back();
+                if (e.second <= best) { node = e.first; found = true; break; }
+            }
+            if (!found) break;
+        }
+        nodes_out[i] = nn;
+        leaves_out[i] = nl;
+    }
+}
+
+// ---- packet (wave-uniform) traversal experiment: 64 queries share one node stack; a child is entered
+// when any lane's bound passes.  Outputs per packet: uniform node visits, uniform leaf visits and the
+// per-lane leaf tests summed over the packet.  mode as model_counts_obb (1 = max(AABB, OBB)).
+extern "C" void model_packets(const double* v, const uint32_t* f, int T, const double* q, long npk, int mode,
+                              uint32_t* steps_out, uint32_t* leafv_out, uint32_t* leaft_out) {
+    Tree tr = build_lbvh(v, f, T);
+    std::vector<OBB> ob(2 * (T - 1));
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int x = 0; x < T - 1; ++x) {
+        for (int s = 0; s < 2; ++s) {
+            int b, e;
+            range_of(tr, tr.nodes[x].c[s], b, e);
+            ob[2 * x + s] = make_obb(tr, v, f, b, e, 1);
+        }
+    }
+#pragma omp parallel for schedule(dynamic, 4)
+    for (long p = 0; p < npk; ++p) {
+        const double* qq = q + 3 * 64 * p;
+        double best[64];
+        for (int l = 0; l < 64; ++l) best[l] = std::numeric_limits<double>::infinity();
+        uint32_t ns = 0, nlv = 0, nlt = 0;
+        struct E { int node; double d[64]; };
+        std::vector<E> st;
+        int node = 0;
+        for (;;) {
+            const Node& n = tr.nodes[node];
+            ++ns;
+            double d[2][64];
+            bool need[2] = {false, false};
+            for (int s = 0; s < 2; ++s) {
+                for (int l = 0; l < 64; ++l) {
+                    const double* ql = qq + 3 * l;
+                    d[s][l] = mode == 1 ? std::max(box_d2(ql, n.lo[s], n.hi[s]), obb_d2(ql, ob[2 * node + s]))
+                                        : box_d2(ql, n.lo[s], n.hi[s]);
+                }
+                if (n.c[s] < 0) {
+                    int fc = tr.order[~n.c[s]];
+                    const uint32_t* ff = f + 3 * fc;
+                    bool any = false;
+                    for (int l = 0; l < 64; ++l)
+                        if (d[s][l] <= best[l]) {
+                            any = true;
+                            ++nlt;
+                            best[l] = std::min(best[l], tri_d2(qq + 3 * l, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                        }
+                    if (any) ++nlv;
+                }
+            }
+            int cnt[2] = {0, 0}, nearer0 = 0;
+            for (int s = 0; s < 2; ++s) {
+                if (n.c[s] < 0) continue;
+                for (int l = 0; l < 64; ++l)
+                    if (d[s][l] <= best[l]) { need[s] = true; ++cnt[s]; }
+            }
+            for (int l = 0; l < 64; ++l) nearer0 += d[0][l] <= d[1][l];
+            if (need[0] && need[1]) {
+                int nr = nearer0 >= 32 ? 0 : 1;
+                E e;
+                e.node = n.c[1 - nr];
+                for (int l = 0; l < 64; ++l) e.d[l] = d[1 - nr][l];
+                st.push_back(e);
+                node = n.c[nr];
+                continue;
+            }
+            if (need[0]) { node = n.c[0]; continue; }
+            if (need[1]) { node = n.c[1]; continue; }
+            bool found = false;
+            while (!st.empty()) {
+                E e = st.back();
+                st.pop_back();
+                bool any = false;
+                for (int l = 0; l < 64; ++l) any |= e.d[l] <= best[l];
+                if (any) { node = e.node; found = true; break; }
+            }
+            if (!found) break;
+        }
+        steps_out[p] = ns;
+        leafv_out[p] = nlv;
+        leaft_out[p] = nlt;
+    }
+}
+
+// ---- BVH4 experiment: collapse the binary LBVH (node x -> grandchildren), oriented boxes of slots
+// (0,1) in the frame of binary child A's range and slots (2,3) in child B's.  Per-lane depth-first,
+// nearest child first.  Outputs per query: BVH4 nodes visited and leaf tests.
+extern "C" void model_counts_bvh4(const double* v, const uint32_t* f, int T, const double* q, long S,
+                                  uint32_t* nodes_out, uint32_t* leaves_out) {
+    Tree tr = build_lbvh(v, f, T);
+    struct Slot { int c; double lo[3], hi[3]; OBB o; };
+    struct N4 { Slot s[4]; int n; };
+    std::vector<int> map(T - 1, -1);
+    std::vector<N4> n4;
+    std::vector<int> todo{0};
+    map[0] = 0;
+    n4.push_back({});
+    auto box_of = [&](int parent, int side, double* lo, double* hi) {
+        for (int k = 0; k < 3; ++k) { lo[k] = tr.nodes[parent].lo[side][k]; hi[k] = tr.nodes[parent].hi[side][k]; }
+    };
+    while (!todo.empty()) {
+        int x = todo.back();
+        todo.pop_back();
+        N4 nd{};
+        nd.n = 0;
+        for (int side = 0; side < 2; ++side) {
+            int a = tr.nodes[x].c[side];
+            int gb, ge;
+            range_of(tr, a, gb, ge);
+            OBB frame = make_obb(tr, v, f, gb, ge, 1);
+            auto add = [&](int c, int par, int sd) {
+                Slot s;
+                s.c = c;
+                box_of(par, sd, s.lo, s.hi);
+                int b, e;
+                range_of(tr, c, b, e);
+                s.o = frame;
+                for (int k = 0; k < 3; ++k) { s.o.lo[k] = 1e300; s.o.hi[k] = -1e300; }
+                for (int i = b; i <= e; ++i) {
+                    const uint32_t* ff = f + 3 * tr.order[i];
+                    for (int cc = 0; cc < 3; ++cc) {
+                        const double* P = v + 3 * ff[cc];
+                        for (int k = 0; k < 3; ++k) {
+                            double pp = P[0] * s.o.ax[k][0] + P[1] * s.o.ax[k][1] + P[2] * s.o.ax[k][2];
+                            s.o.lo[k] = std::min(s.o.lo[k], pp); s.o.hi[k] = std::max(s.o.hi[k], pp);
+                        }
+                    }
+                }
+                nd.s[nd.n++] = s;
+            };
+            if (a < 0) add(a, x, side);
+            else { add(tr.nodes[a].c[0], a, 0); add(tr.nodes[a].c[1], a, 1); }
+        }
+        for (int k = 0; k < nd.n; ++k) {
+            int c = nd.s[k].c;
+            if (c >= 0) {
+                map[c] = (int)n4.size();
+                n4.push_back({});
+                todo.push_back(c);
+                nd.s[k].c = map[c];
+            }
+        }
+        n4[map[x]] = nd;
+    }
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long i = 0; i < S; ++i) {
+        const double* qq = q + 3 * i;
+        double best = std::numeric_limits<double>::infinity();
+        uint32_t nn = 0, nl = 0;
+        std::vector<std::pair<int, double>> st;
+        int node = 0;
+        for (;;) {
+            const N4& n = n4[node];
+            ++nn;
+            std::pair<double, int> h[4];
+            int nh = 0;
+            double dd[4];
+            for (int s = 0; s < n.n; ++s) {
+                dd[s] = std::max(box_d2(qq, n.s[s].lo, n.s[s].hi), obb_d2(qq, n.s[s].o));
+            }
+            for (int s = 0; s < n.n; ++s) {
+                if (dd[s] <= best && n.s[s].c < 0) {
+                    int fc = tr.order[~n.s[s].c];
+                    const uint32_t* ff = f + 3 * fc;
+                    best = std::min(best, tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                    ++nl;
+                }
+            }
+            for (int s = 0; s < n.n; ++s)
+                if (n.s[s].c >= 0 && dd[s] <= best) h[nh++] = {dd[s], n.s[s].c};
+            std::sort(h, h + nh);
+            if (nh > 0) {
+                for (int k = nh - 1; k >= 1; --k) st.push_back({h[k].second, h[k].first});
+                node = h[0].second;
+                continue;
+            }
             bool found = false;
             while (!st.empty()) {
                 auto e = st.back();
