@@ -7,13 +7,17 @@
 //   Pass 1 (k_knn): persistent grid; each WAVE dequeues 64-query tiles from one of 8 XCD-group
 //     counters (group = blockIdx % 8 labels the blocks sharing an XCD; each counter owns a contiguous
 //     eighth of the Morton-sorted queries, so an XCD's L2 serves one region of the BVH; exhausted
-//     groups steal).  One lane per query, near-child-first depth-first traversal: one 64-B node read
-//     tests both children with conservative fp32 box bounds, leaves get a conservative fp32 pretest and
-//     then CGAL's exact fp64 construction, the far child is pushed (16-entry LDS stack per lane,
-//     [depth][lane] layout, deeper entries spill to a per-lane global area sized from the tree depth).
-//     A lane that exceeds `budget` node steps stops and appends its query (with its best so far) to a
-//     deferred list: queries near the centre of a closed surface are equidistant from most of it and
-//     would otherwise hold their whole wave for ~10^6 steps.
+//     groups steal).  One lane per query, near-child-first depth-first traversal: one 128-B node read
+//     (one L2 line) bounds both children by max(fp32 AABB bound, fp32 oriented-box bound); the far
+//     child is pushed (16-entry LDS stack per lane, [depth][lane] layout, deeper entries spill to a
+//     per-lane global area sized from the tree depth).  Leaf children are parked and tested in
+//     wave-wide leaf phases (Aila & Laine's postponed leaves).  A leaf test is fp32 only: lower and
+//     upper bounds of its distance (tri_d2_bounds); the upper bound tightens the pruning limit, the
+//     leaf stays a candidate, and CGAL's exact fp64 construction runs at the end of the query on the
+//     candidates that can still win (TriCandPol; the normals metric and points test exactly).
+//     A lane that exceeds `budget` node steps stops and appends its query (with its exact best so far)
+//     to a deferred list: queries near the centre of a closed surface are equidistant from most of it
+//     and would otherwise hold their whole wave for ~10^6 steps.
 //   Pass 2 (k_knn_coop): one WAVE per deferred query.  The wave expands the top of the tree
 //     breadth-first into <= 512 subtrees (LDS frontier), deals them to its 64 lanes, and every lane walks
 //     its subtrees depth-first while the wave shares the best bound after every step (wave min).
@@ -25,6 +29,13 @@
 #include <mutex>
 
 #include "internal.h"
+
+// MSH_WAVES (tuning): force the pass-1 kernel's occupancy (waves per SIMD) through its register budget.
+#ifdef MSH_WAVES
+#define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MSH_WAVES, MSH_WAVES)))
+#else
+#define MSH_KNN_ATTR
+#endif
 
 namespace msh {
 
@@ -97,6 +108,7 @@ struct TriPol {
     int best_leaf;
     unsigned n_exact;  // exact constructions run (statistics only)
     __device__ double limit() const { return fmin(best, shared) * kSlack; }
+    __device__ void flush() {}
     __device__ void test(int leaf) {
         D3 a, b, c;
         uint32_t face;
@@ -123,6 +135,79 @@ struct TriPol {
     }
 };
 
+// Pass-1 triangle policy with deferred exact tests.  A leaf first gets both fp32 bounds
+// (tri_d2_bounds: lo <= d2 <= hi for the fp64 CGAL value).  Its upper bound tightens the pruning
+// limit at once, and the leaf is kept as a candidate (lo) instead of running the fp64 construction;
+// candidates whose lo exceeds the limit later are dropped, and flush() runs the exact construction
+// on the survivors only.  Exactness: the winning leaf, and every leaf tied with it, has
+// lo <= d2* <= limit at all times, so it is never dropped.  Leaves without fp32 information
+// (slivers, degenerate, non-finite) and candidates that find the list full are tested exactly on
+// the spot.
+struct TriCandPol {
+    const TriRec* __restrict__ tris;
+    D3 q;
+    double best, shared;  // exact part (as TriPol)
+    uint32_t best_face;
+    int best_leaf;
+    unsigned n_exact;
+    float hi;              // smallest fp32 upper bound among the candidates seen
+    int c0, c1, c2, c3;    // candidate leaves (-1 = free slot)
+    float l0, l1, l2, l3;  // their lower bounds
+    __device__ double limit() const { return fmin(fmin(best, shared), (double)hi) * kSlack; }
+    __device__ void exact(int leaf) {
+        D3 a, b, c, o;
+        uint32_t face;
+        int part;
+        load_tri(tris, leaf, a, b, c, face);
+        ++n_exact;
+        const double d2 = closest_on_triangle(q, a, b, c, o, part);
+        if (d2 < best || (d2 == best && face < best_face)) {
+            best = d2;
+            best_face = face;
+            best_leaf = leaf;
+        }
+    }
+    __device__ void test(int leaf) {
+        D3 a, b, c;
+        uint32_t face;
+        load_tri(tris, leaf, a, b, c, face);
+        float ax, ay, az, bx, by, bz, cx, cy, cz;
+        rel_f32(a, q, ax, ay, az);
+        rel_f32(b, q, bx, by, bz);
+        rel_f32(c, q, cx, cy, cz);
+        float lo, h;
+        tri_d2_bounds(ax, ay, az, bx, by, bz, cx, cy, cz, lo, h);
+        if (lo > __double2float_ru(limit())) return;  // NaN never rejects
+        if (!(h < INFINITY)) {                          // no fp32 information: exact now
+            exact(leaf);
+            return;
+        }
+        hi = fminf(hi, h);
+        const float lim = __double2float_ru(limit());
+        if (l0 > lim) c0 = -1;
+        if (l1 > lim) c1 = -1;
+        if (l2 > lim) c2 = -1;
+        if (l3 > lim) c3 = -1;
+        if (c0 < 0) { c0 = leaf; l0 = lo; }
+        else if (c1 < 0) { c1 = leaf; l1 = lo; }
+        else if (c2 < 0) { c2 = leaf; l2 = lo; }
+        else if (c3 < 0) { c3 = leaf; l3 = lo; }
+        else exact(leaf);
+    }
+    // exact constructions for the surviving candidates; afterwards best/best_face/best_leaf are final
+    __device__ void flush() {
+        const float lim = __double2float_ru(limit());
+#pragma unroll 1
+        while (max(max(c0, c1), max(c2, c3)) >= 0) {  // rotate through one exact() call site
+            if (c0 >= 0 && l0 <= lim) exact(c0);
+            c0 = c1; l0 = l1;
+            c1 = c2; l1 = l2;
+            c2 = c3; l2 = l3;
+            c3 = -1;
+        }
+    }
+};
+
 // metric = ||q - p|| + eps (1 - n_q . n_tri)  (AABB_n_tree.h:40-84).  The penalty is bounded below by
 // pmin = min(eps(1-|n_q|), eps(1+|n_q|)), so a face can only win inside the ball of radius best - pmin.
 struct NrmPol {
@@ -140,6 +225,7 @@ struct NrmPol {
         if (r < 0.0) r = 0.0;
         return r * r * kSlack;
     }
+    __device__ void flush() {}
     __device__ void test(int leaf) {
         D3 a, b, c;
         uint32_t face;
@@ -173,6 +259,7 @@ struct PtPol {
     uint32_t best_face;
     int best_leaf;
     __device__ double limit() const { return fmin(best, shared) * kSlack; }
+    __device__ void flush() {}
     __device__ void test(int leaf) {
         const double2* p = reinterpret_cast<const double2*>(pts + leaf);
         const double2 x0 = p[0], x1 = p[1];
@@ -383,8 +470,43 @@ __device__ inline typename PolOf<MODE>::T make_pol(const KnnArgs& a, size_t qi, 
     return pol;
 }
 
+// Test the parked leaves p0..p3 (-1 = empty) through ONE call site: the registers rotate, so the
+// (large, fp64) leaf test is instantiated once instead of once per slot.
+template <class Pol>
+__device__ inline void test_pending(Pol& pol, int& p0, int& p1, int& p2, int& p3) {
+#pragma unroll 1
+    while (max(max(p0, p1), max(p2, p3)) >= 0) {
+        if (p0 >= 0) pol.test(p0);
+        p0 = p1;
+        p1 = p2;
+        p2 = p3;
+        p3 = -1;
+    }
+}
+
+// pass-1 policy: candidate-deferring triangles for plain closest point, the exact policies otherwise
+template <int MODE>
+__device__ inline auto make_pol1(const KnnArgs& a, size_t qi, const D3& q) {
+    if constexpr (MODE == 0) {
+        TriCandPol pol;
+        pol.tris = static_cast<const TriRec*>(a.leaves);
+        pol.q = q;
+        pol.best = INFINITY;
+        pol.shared = INFINITY;
+        pol.best_face = 0xFFFFFFFFu;
+        pol.best_leaf = -1;
+        pol.n_exact = 0;
+        pol.hi = INFINITY;
+        pol.c0 = pol.c1 = pol.c2 = pol.c3 = -1;
+        pol.l0 = pol.l1 = pol.l2 = pol.l3 = 0.f;
+        return pol;
+    } else {
+        return make_pol<MODE>(a, qi, q);
+    }
+}
+
 template <int MODE, bool STATS>
-__global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
+__global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
     const int tid = threadIdx.x, lane = tid & 63;
     uint2* lds = stk + tid;
@@ -402,7 +524,7 @@ __global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
         if (i >= a.S) continue;
         const size_t qi = a.perm ? (size_t)a.perm[i] : i;
         const D3 q = D3{a.q[3 * qi], a.q[3 * qi + 1], a.q[3 * qi + 2]};
-        auto pol = make_pol<MODE>(a, qi, q);
+        auto pol = make_pol1<MODE>(a, qi, q);
         if (a.T == 1) {
             pol.test(0);
             if (STATS) ++n_leaves;
@@ -429,12 +551,8 @@ __global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
                         u_leaf_lanes += np;
                     }
                     if (parked) {
-                        if (p0 >= 0) pol.test(p0);
-                        if (p1 >= 0) pol.test(p1);
-                        if (p2 >= 0) pol.test(p2);
-                        if (p3 >= 0) pol.test(p3);
                         if (STATS) n_leaves += (p0 >= 0) + (p1 >= 0) + (p2 >= 0) + (p3 >= 0);
-                        p0 = p1 = p2 = p3 = -1;
+                        test_pending(pol, p0, p1, p2, p3);
                     }
                     continue;
                 }
@@ -451,11 +569,8 @@ __global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
                     if (active && steps == a.budget) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
                         if (slot < a.max_deferred) {
-                            if (p0 >= 0) pol.test(p0);
-                            if (p1 >= 0) pol.test(p1);
-                            if (p2 >= 0) pol.test(p2);
-                            if (p3 >= 0) pol.test(p3);
-                            p0 = p1 = p2 = p3 = -1;
+                            test_pending(pol, p0, p1, p2, p3);
+                            pol.flush();
                             DeferRec r;
                             r.qi = (uint32_t)qi;
                             r.face = pol.best_face;
@@ -473,6 +588,7 @@ __global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
             }
             if (deferred) continue;
         }
+        pol.flush();
         if (!STATS) write_result<MODE>(a, qi, q, pol);
         if constexpr (STATS && MODE == 0) n_exact += pol.n_exact;
     }

@@ -1,8 +1,8 @@
 // Host-side property check of the conservative fp32 culling bounds in mesh_amd/csrc/common.h
-// (tri_d2_lo, box_d2_lo): on random and adversarial triangles the fp32 lower bound must never exceed
-// the exact fp64 squared distance (CGAL construction, mesh_amd/csrc/common.h closest_on_triangle is
-// device-only, so the exact value here comes from the oracle's formulas re-derived in long double).
-// Built with hipcc as host code; prints "violations=<n> checked=<m> rejected=<r>".
+// (tri_d2_bounds, box_d2_lo): on random and adversarial triangles the fp32 lower bound must never
+// exceed, and the upper bound never undercut, the exact squared distance (closest_on_triangle in
+// common.h is device-only, so the exact value here is re-derived in long double).  Built with hipcc
+// as host code; prints "violations=<n> checked=<m> rejected=<r> upper=<u>".
 // Kinds: random, sliver, near a vertex, near an edge, on the face, large offset, and above the
 // face/edge (6) and face/vertex (7) region boundaries, where a misclassified region matters most.
 #include <cmath>
@@ -51,7 +51,7 @@ int main(int argc, char** argv) {
     std::mt19937_64 rng(12345);
     std::normal_distribution<double> N(0.0, 1.0);
     std::uniform_real_distribution<double> U(0.0, 1.0);
-    long viol = 0, rej = 0;
+    long viol = 0, rej = 0, pruned = 0;
     for (long it = 0; it < n; ++it) {
         const int kind = it % 8;
         double scale = std::pow(10.0, -3 + 6 * U(rng));  // triangle size
@@ -79,7 +79,8 @@ int main(int argc, char** argv) {
         float f[9];
         for (int c = 0; c < 3; ++c)
             for (int k = 0; k < 3; ++k) f[3 * c + k] = (float)(t[3 * c + k] - q[k]);
-        const float lo = msh::tri_d2_lo(f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7], f[8]);
+        float lo, hi;
+        msh::tri_d2_bounds(f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7], f[8], lo, hi);
         long double P[3] = {q[0], q[1], q[2]}, A[3] = {t[0], t[1], t[2]}, B[3] = {t[3], t[4], t[5]}, C[3] = {t[6], t[7], t[8]};
         const long double ex = tri_d2(P, A, B, C);
         if (lo > 0) ++rej;
@@ -87,7 +88,12 @@ int main(int argc, char** argv) {
             if (viol < 5) fprintf(stderr, "violation kind=%d lo=%.9g exact=%.17Lg\n", kind, lo, ex);
             ++viol;
         }
+        if ((long double)hi < ex * (1 - 1e-12L)) {  // the upper bound may not undercut either
+            if (viol < 5) fprintf(stderr, "violation kind=%d hi=%.9g exact=%.17Lg\n", kind, hi, ex);
+            ++viol;
+        }
+        if (hi < INFINITY) ++pruned;
     }
-    printf("violations=%ld checked=%ld rejected=%ld\n", viol, n, rej);
+    printf("violations=%ld checked=%ld rejected=%ld upper=%ld\n", viol, n, rej, pruned);
     return viol != 0;
 }
