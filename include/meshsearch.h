@@ -53,6 +53,7 @@ typedef struct msh_tree_info {
     double eps;
     float scene_lo[3], scene_hi[3];
     double build_ms;     /* GPU time of the LBVH build (Morton + radix sort + emission + refit) */
+    uint64_t n_meshes;   /* meshes in a batched tree (msh_batch_build), 1 otherwise */
 } msh_tree_info;
 
 /* ---- library / device ---- */
@@ -115,6 +116,19 @@ int msh_ntree_selfintersects(msh_tree* tree, int64_t* count);
  * freed (fixes the double free at py_visibility.cpp:212). */
 int msh_visibility(msh_tree* tree, const double* cams, size_t C, const double* normals, const double* sensors,
                    double min_dist, uint32_t* vis, double* ndc);
+
+/* ---- batched trees: scan-to-mesh registration over many meshes (BASELINE configs[3], C4) ----
+ * The reference answers this with one AabbTree per mesh (search.py:21-30, one aabbtree_compute +
+ * aabbtree_nearest per mesh).  Here B meshes sharing one topology are built in ONE batched LBVH build
+ * (per-mesh Morton order, Karras emission and refit in single launches over all B*T faces) and queried
+ * in one launch.  v: (B,P,3) f64, f: (T,3) u32 shared by all meshes, T >= 2.  Face indices returned
+ * are mesh-local (as a per-mesh AabbTree would return). */
+int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size_t T, msh_tree** out);
+/* q: (B,S,3) f64, S queries per mesh -> face (B,S) u32, part (B,S) u32 (may be NULL), point (B,S,3) f64;
+ * per mesh identical to msh_tree_nearest on that mesh alone. */
+int msh_batch_nearest(msh_tree* tree, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt);
+int msh_batch_nearest_device(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part,
+                             double* d_pt, void* stream);
 
 /* ---- ClosestPointTree (search.py:52-65, scipy.spatial.KDTree) ---- */
 int msh_points_build(const double* v, size_t P, msh_tree** out);

@@ -50,6 +50,9 @@ SIGNATURES = [
     ("msh_tree_blob_size", _i, [_vp, ctypes.POINTER(_sz)]),
     ("msh_tree_blob_pack", _i, [_vp, _vp, _vp]),
     ("msh_tree_blob_unpack", _i, [_vp, _sz, _i, _vp, ctypes.POINTER(_vp)]),
+    ("msh_batch_build", _i, [_c_double_p, _sz, _sz, _c_u32_p, _sz, ctypes.POINTER(_vp)]),
+    ("msh_batch_nearest", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_u32_p, _c_double_p]),
+    ("msh_batch_nearest_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     ("msh_timing_enable", _i, [_i]),
     ("msh_timing_get", _i, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _c_i64_p]),
     ("msh_timing_reset", _i, []),
@@ -60,7 +63,7 @@ class TreeInfo(ctypes.Structure):
     _fields_ = [("device", _i), ("kind", _i), ("n_points", ctypes.c_uint64), ("n_faces", ctypes.c_uint64),
                 ("n_main_faces", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
                 ("eps", ctypes.c_double), ("scene_lo", ctypes.c_float * 3), ("scene_hi", ctypes.c_float * 3),
-                ("build_ms", ctypes.c_double)]
+                ("build_ms", ctypes.c_double), ("n_meshes", ctypes.c_uint64)]
 
 
 def _preload_single_hip_runtime():
@@ -177,6 +180,13 @@ def build_ntree(v, f, eps):
     out = _vp()
     check(lib().msh_ntree_build(dptr(v), v.shape[0], uptr(f), f.shape[0], float(eps), ctypes.byref(out)))
     return Handle(out.value, "normals")
+
+
+def build_batch(v, f):
+    """B meshes sharing the faces f: v (B,P,3) float64 C-contiguous, f (T,3) uint32."""
+    out = _vp()
+    check(lib().msh_batch_build(dptr(v), v.shape[0], v.shape[1], uptr(f), f.shape[0], ctypes.byref(out)))
+    return Handle(out.value, "batch")
 
 
 def build_points(v):

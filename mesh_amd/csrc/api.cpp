@@ -145,6 +145,8 @@ static void free_tree(msh_tree* t) {
     if (t->d_v) (void)hipFree(t->d_v);
     if (t->d_nodes) (void)hipFree(t->d_nodes);
     if (t->d_nodes4) (void)hipFree(t->d_nodes4);
+    if (t->d_orgs) (void)hipFree(t->d_orgs);
+    if (t->d_boxes) (void)hipFree(t->d_boxes);
     if (t->d_leaves) (void)hipFree(t->d_leaves);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
@@ -236,6 +238,22 @@ static int check_tree(const msh_tree* t, int want_kind, const char* fn) {
     }
     if (want_kind == kPoints ? t->kind != kPoints : t->kind == kPoints) {
         set_error("%s: wrong handle kind %d", fn, t->kind);
+        return MSH_EINVAL;
+    }
+    if (t->B != 1) {
+        set_error("%s: batched tree handle (use the msh_batch_* entry points)", fn);
+        return MSH_EINVAL;
+    }
+    return use_device(t->device);
+}
+
+static int check_batch(const msh_tree* t, const char* fn) {
+    if (!t) {
+        set_error("%s: null tree handle", fn);
+        return MSH_EINVAL;
+    }
+    if (!t->d_boxes) {
+        set_error("%s: not a batched tree handle (build it with msh_batch_build)", fn);
         return MSH_EINVAL;
     }
     return use_device(t->device);
@@ -378,11 +396,12 @@ int msh_tree_get_info(const msh_tree* t, msh_tree_info* info) {
     info->n_points = t->P;
     info->n_faces = t->T;
     info->n_main_faces = t->T_main;
-    info->n_nodes = t->T > 0 ? t->T - 1 : 0;
+    info->n_nodes = t->T > 0 ? t->B * (t->T - 1) : 0;
+    info->n_meshes = t->B;
     const size_t leaf = t->kind == kPoints ? sizeof(PtRec) : sizeof(TriRec);
     const size_t vrows = t->kind == kPoints ? t->P : t->P;  // main vertices (extra mesh rows follow)
     (void)vrows;
-    info->bytes = info->n_nodes * sizeof(BNode) + t->T * leaf;
+    info->bytes = info->n_nodes * sizeof(BNode) + t->B * t->T * leaf;
     info->eps = t->eps;
     for (int k = 0; k < 3; ++k) {
         info->scene_lo[k] = t->scene_lo[k];
@@ -666,6 +685,7 @@ static void blob_layout(const msh_tree* t, BlobHeader& h) {
 
 int msh_tree_blob_size(const msh_tree* t, size_t* bytes) {
     if (!t || !bytes) { set_error("null argument"); return MSH_EINVAL; }
+    if (t->B != 1) { set_error("msh_tree_blob_size: batched trees are not serialisable"); return MSH_EINVAL; }
     BlobHeader h;
     blob_layout(t, h);
     *bytes = h.total;
@@ -674,6 +694,7 @@ int msh_tree_blob_size(const msh_tree* t, size_t* bytes) {
 
 int msh_tree_blob_pack(const msh_tree* t, void* d_dst, void* stream) {
     if (!t || !d_dst) { set_error("null argument"); return MSH_EINVAL; }
+    if (t->B != 1) { set_error("msh_tree_blob_pack: batched trees are not serialisable"); return MSH_EINVAL; }
     MSH_TRY(use_device(t->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : t->stream;
     BlobHeader h;
@@ -735,6 +756,7 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
             st = MSH_EDEVICE;
             break;
         }
+        if ((st = upload_origin(t, t->stream)) != MSH_OK) break;
         st = build_bvh4(t);  // the 4-wide nearest-query nodes are derived, not shipped
         if (st == MSH_OK && hipStreamSynchronize(t->stream) != hipSuccess) {
             set_error("blob unpack: 4-wide node build failed");
@@ -772,6 +794,122 @@ int msh_timing_reset(void) {
     resolve_pending();
     std::lock_guard<std::mutex> g(g_tmu);
     g_times.clear();
+    return MSH_OK;
+}
+
+// ---- batched trees (C4: B meshes sharing one topology) ----
+int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size_t T, msh_tree** out) {
+    if (!out) { set_error("msh_batch_build: null output"); return MSH_EINVAL; }
+    *out = nullptr;
+    if (!v || !f || B == 0 || P == 0 || T < 2) {
+        set_error("msh_batch_build: need B >= 1 meshes of P >= 1 vertices and T >= 2 faces (got B=%zu P=%zu T=%zu)",
+                  B, P, T);
+        return MSH_EINVAL;
+    }
+    if (B * T > (size_t)0x7FFFFFFF) {
+        set_error("msh_batch_build: %zu x %zu faces exceed the 31-bit leaf index range", B, T);
+        return MSH_EINVAL;
+    }
+    MSH_TRY(check_faces(f, T, P, "msh_batch_build"));
+    msh_tree* t = nullptr;
+    MSH_TRY(new_tree(kTriangles, &t));
+    t->B = B;
+    t->P = P;
+    t->T = T;
+    t->T_main = T;
+    hipStream_t s = t->stream;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    DevBuf dF, dLo, dHi, dOrder;
+    int st = MSH_OK;
+    do {
+        hipError_t e = hipEventCreate(&e0);
+        if (e == hipSuccess) e = hipEventCreate(&e1);
+        if (e == hipSuccess) e = hipMalloc(&t->d_v, B * P * 3 * sizeof(double));
+        if (e == hipSuccess) e = hipMalloc(&t->d_nodes, B * (T - 1) * sizeof(BNode));
+        if (e == hipSuccess) e = hipMalloc(&t->d_leaves, B * T * sizeof(TriRec));
+        if (e != hipSuccess) { set_error("msh_batch_build: %s", hipGetErrorString(e)); st = MSH_ENOMEM; break; }
+        e = hipMemcpyAsync(t->d_v, v, B * P * 3 * sizeof(double), hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) { set_error("msh_batch_build: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
+        if ((st = upload(dF, f, 3 * T, s)) != MSH_OK) break;
+        if ((st = dLo.reserve(3 * B * T * sizeof(double))) != MSH_OK) break;
+        if ((st = dHi.reserve(3 * B * T * sizeof(double))) != MSH_OK) break;
+        if ((st = dOrder.reserve(B * T * sizeof(uint32_t))) != MSH_OK) break;
+        (void)hipEventRecord(e0, s);
+        if ((st = tri_bounds_batch(t->d_v, P, dF.as<uint32_t>(), B, T, dLo.as<double>(), dHi.as<double>(), s)) != MSH_OK)
+            break;
+        if ((st = build_lbvh_batch(t, dLo.as<double>(), dHi.as<double>(), T, dOrder.as<uint32_t>())) != MSH_OK) break;
+        if ((st = pack_tri_leaves_batch(t->d_v, P, dF.as<uint32_t>(), dOrder.as<uint32_t>(), B, T,
+                                        static_cast<TriRec*>(t->d_leaves), s)) != MSH_OK)
+            break;
+        if ((st = build_obb(t, true)) != MSH_OK) break;
+        (void)hipEventRecord(e1, s);
+        e = hipStreamSynchronize(s);
+        if (e != hipSuccess) { set_error("batched LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        t->build_ms = ms;
+    } while (0);
+    (void)hipStreamSynchronize(s);
+    dF.release(); dLo.release(); dHi.release(); dOrder.release();
+    t->ws.release();
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (st != MSH_OK) {
+        std::string keep = g_err;
+        free_tree(t);
+        g_err = keep;
+        return st;
+    }
+    *out = t;
+    return MSH_OK;
+}
+
+int msh_batch_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part, double* d_pt,
+                             void* stream) {
+    MSH_TRY(check_batch(t, "msh_batch_nearest_device"));
+    const size_t n = t->B * S;
+    if (n == 0) return MSH_OK;
+    if (n > (size_t)0xFFFFFFFFu) { set_error("msh_batch_nearest: %zu queries exceed 2^32", n); return MSH_EINVAL; }
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : t->stream;
+    Workspace& ws = t->ws;
+    const uint32_t* perm = nullptr;
+    if (n >= kSortMin) {  // Morton order inside each mesh, meshes in order (two stable passes)
+        MSH_TRY(ws.keys.reserve(n * sizeof(uint32_t)));
+        MSH_TRY(ws.vals.reserve(n * sizeof(uint32_t)));
+        MSH_TRY(ws.keys_alt.reserve(n * sizeof(uint32_t)));
+        MSH_TRY(ws.vals_alt.reserve(n * sizeof(uint32_t)));
+        uint32_t* keys = ws.keys.as<uint32_t>();
+        uint32_t* vals = ws.vals.as<uint32_t>();
+        MSH_TRY(query_morton_batch(t, d_q, n, S, keys, vals, s));
+        MSH_TRY(radix_sort_pairs(keys, vals, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n, 30, ws, s));
+        if (t->B > 1) {
+            MSH_TRY(mesh_keys(vals, n, S, keys, s));
+            int bits = 0;
+            while (bits < 32 && ((size_t)1 << bits) < t->B) ++bits;
+            MSH_TRY(radix_sort_pairs(keys, vals, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n, bits, ws, s));
+        }
+        perm = vals;
+    }
+    return launch_nearest_batch(t, d_q, perm, n, S, d_face, d_part, d_pt, s);
+}
+
+int msh_batch_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
+    MSH_TRY(check_batch(t, "msh_batch_nearest"));
+    const size_t n = t->B * S;
+    if (n == 0) return MSH_OK;
+    if (!q || !face || !pt) { set_error("msh_batch_nearest: null argument"); return MSH_EINVAL; }
+    hipStream_t s = t->stream;
+    Workspace& ws = t->ws;
+    MSH_TRY(upload(ws.q, q, 3 * n, s));
+    MSH_TRY(ws.out_a.reserve(n * sizeof(uint32_t)));
+    MSH_TRY(ws.out_b.reserve(n * sizeof(uint32_t)));
+    MSH_TRY(ws.out_c.reserve(3 * n * sizeof(double)));
+    MSH_TRY(msh_batch_nearest_device(t, ws.q.as<double>(), S, ws.out_a.as<uint32_t>(),
+                                     part ? ws.out_b.as<uint32_t>() : nullptr, ws.out_c.as<double>(), s));
+    MSH_HIP(hipMemcpyAsync(face, ws.out_a.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    if (part) MSH_HIP(hipMemcpyAsync(part, ws.out_b.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+    MSH_HIP(hipMemcpyAsync(pt, ws.out_c.ptr, 3 * n * sizeof(double), hipMemcpyDeviceToHost, s));
+    MSH_HIP(hipStreamSynchronize(s));
     return MSH_OK;
 }
 

@@ -25,16 +25,20 @@
 
 namespace msh {
 
-__global__ __launch_bounds__(kBlock) void k_tri_bounds(const double* __restrict__ v, const uint32_t* __restrict__ f,
-                                                       size_t T, double* __restrict__ lo, double* __restrict__ hi) {
-    const size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    if (t >= T) return;
+// Batched kernels: B meshes of P vertices / T primitives each, stored back to back (primitive
+// g = b*T + t of mesh b = g / T); the single-mesh build is B = 1.
+__global__ __launch_bounds__(kBlock) void k_tri_bounds(const double* __restrict__ v, size_t P, const uint32_t* __restrict__ f,
+                                                       size_t n, size_t T, double* __restrict__ lo, double* __restrict__ hi) {
+    const size_t g = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (g >= n) return;
+    const size_t b = g / T, t = g - b * T;
+    const double* vb = v + 3 * P * b;
     const uint32_t i0 = f[3 * t], i1 = f[3 * t + 1], i2 = f[3 * t + 2];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const double a = v[3 * (size_t)i0 + k], b = v[3 * (size_t)i1 + k], c = v[3 * (size_t)i2 + k];
-        lo[3 * t + k] = fmin(fmin(a, b), c);
-        hi[3 * t + k] = fmax(fmax(a, b), c);
+        const double a = vb[3 * (size_t)i0 + k], bb = vb[3 * (size_t)i1 + k], c = vb[3 * (size_t)i2 + k];
+        lo[3 * g + k] = fmin(fmin(a, bb), c);
+        hi[3 * g + k] = fmax(fmax(a, bb), c);
     }
 }
 
@@ -68,6 +72,34 @@ __global__ __launch_bounds__(kBlock) void k_reduce_box(const double* __restrict_
     if (tid < 6) out[6 * blockIdx.x + tid] = sh[tid][0];
 }
 
+// one block per mesh: box of mesh b over its T primitives -> boxes[6b..6b+5], origin (box centre)
+// -> orgs[3b..3b+2]
+__global__ __launch_bounds__(kBlock) void k_mesh_boxes(const double* __restrict__ lo, const double* __restrict__ hi,
+                                                       size_t T, double* __restrict__ boxes, double* __restrict__ orgs) {
+    __shared__ double sh[6][kBlock];
+    const int tid = threadIdx.x;
+    const size_t base = (size_t)blockIdx.x * T;
+    double r[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+    for (size_t i = base + tid; i < base + T; i += kBlock) {
+        r[0] = fmin(r[0], lo[3 * i]); r[1] = fmin(r[1], lo[3 * i + 1]); r[2] = fmin(r[2], lo[3 * i + 2]);
+        r[3] = fmax(r[3], hi[3 * i]); r[4] = fmax(r[4], hi[3 * i + 1]); r[5] = fmax(r[5], hi[3 * i + 2]);
+    }
+    for (int k = 0; k < 6; ++k) sh[k][tid] = r[k];
+    __syncthreads();
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+        if (tid < s) {
+            for (int k = 0; k < 3; ++k) sh[k][tid] = fmin(sh[k][tid], sh[k][tid + s]);
+            for (int k = 3; k < 6; ++k) sh[k][tid] = fmax(sh[k][tid], sh[k][tid + s]);
+        }
+        __syncthreads();
+    }
+    if (tid < 6) boxes[6 * blockIdx.x + tid] = sh[tid][0];
+    if (tid < 3) {
+        const double c = 0.5 * (sh[tid][0] + sh[3 + tid][0]);
+        orgs[3 * blockIdx.x + tid] = (c == c && fabs(c) < INFINITY) ? c : 0.0;
+    }
+}
+
 __device__ inline uint32_t expand_bits10(uint32_t v) {
     v = (v * 0x00010001u) & 0xFF0000FFu;
     v = (v * 0x00000101u) & 0x0F00F00Fu;
@@ -85,16 +117,39 @@ __device__ inline uint32_t morton30(double x, double y, double z, const double* 
     return (expand_bits10((uint32_t)nx) << 2) | (expand_bits10((uint32_t)ny) << 1) | expand_bits10((uint32_t)nz);
 }
 
-__global__ __launch_bounds__(kBlock) void k_morton(const double* __restrict__ lo, const double* __restrict__ hi, size_t n,
-                                                   const double* __restrict__ box, uint32_t* __restrict__ keys,
-                                                   uint32_t* __restrict__ vals) {
-    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
+__device__ inline uint32_t prim_morton(const double* __restrict__ lo, const double* __restrict__ hi, size_t i,
+                                       const double* box) {
     const double cx = 0.5 * (lo[3 * i] + hi[3 * i]);
     const double cy = 0.5 * (lo[3 * i + 1] + hi[3 * i + 1]);
     const double cz = 0.5 * (lo[3 * i + 2] + hi[3 * i + 2]);
-    keys[i] = morton30(cx, cy, cz, box);
+    return morton30(cx, cy, cz, box);
+}
+
+// key = Morton code of the primitive's box centre in its mesh's box (boxes + 6 * (i / T))
+__global__ __launch_bounds__(kBlock) void k_morton(const double* __restrict__ lo, const double* __restrict__ hi, size_t n,
+                                                   size_t T, const double* __restrict__ boxes, uint32_t* __restrict__ keys,
+                                                   uint32_t* __restrict__ vals) {
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = prim_morton(lo, hi, i, boxes + 6 * (i / T));
     vals[i] = (uint32_t)i;
+}
+
+// batched build, between the two sort phases: key = mesh of the primitive
+__global__ __launch_bounds__(kBlock) void k_mesh_key(const uint32_t* __restrict__ vals, size_t n, size_t T,
+                                                     uint32_t* __restrict__ keys) {
+    const size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j < n) keys[j] = (uint32_t)(vals[j] / T);
+}
+
+// batched build, after the sort: Morton codes in sorted order (for node emission)
+__global__ __launch_bounds__(kBlock) void k_sorted_morton(const double* __restrict__ lo, const double* __restrict__ hi,
+                                                          const uint32_t* __restrict__ vals, size_t n, size_t T,
+                                                          const double* __restrict__ boxes, uint32_t* __restrict__ keys) {
+    const size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= n) return;
+    const size_t i = vals[j];
+    keys[j] = prim_morton(lo, hi, i, boxes + 6 * (i / T));
 }
 
 // delta(i, j): common-prefix length of the augmented keys (code, position)
@@ -105,12 +160,18 @@ __device__ inline int lbvh_delta(const uint32_t* __restrict__ k, int n, int i, i
     return 32 + __clz((uint32_t)i ^ (uint32_t)j);
 }
 
-// parent[c]: (parent << 1) | side for internal c in [0, n-1) and leaf l at (n-1) + l
-// ranges[i] = (first leaf, last leaf, split gamma, 0): left child covers [first, gamma]
-__global__ __launch_bounds__(kBlock) void k_karras(const uint32_t* __restrict__ keys, int n, BNode* __restrict__ nodes,
-                                                   uint32_t* __restrict__ parent, int4* __restrict__ ranges) {
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n - 1) return;
+// Mesh b owns internal nodes [b(n-1), (b+1)(n-1)) and leaves [bn, (b+1)n); child references are
+// global (internal >= 0, leaf = ~global leaf).  parent[c]: (parent << 1) | side for internal c in
+// [0, B(n-1)) and global leaf l at B(n-1) + l.  ranges[g] = (first leaf, last leaf, split gamma, 0),
+// global leaf positions: the left child covers [first, gamma].
+__global__ __launch_bounds__(kBlock) void k_karras(const uint32_t* __restrict__ all_keys, int B, int n,
+                                                   BNode* __restrict__ nodes, uint32_t* __restrict__ parent,
+                                                   int4* __restrict__ ranges) {
+    const long long gi = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (gi >= (long long)B * (n - 1)) return;
+    const int mb = (int)(gi / (n - 1)), i = (int)(gi - (long long)mb * (n - 1));
+    const uint32_t* keys = all_keys + (size_t)mb * n;
+    const int nb = mb * (n - 1), lb = mb * n;  // node / leaf base of this mesh
     const int d = (lbvh_delta(keys, n, i, i + 1) - lbvh_delta(keys, n, i, i - 1)) >= 0 ? 1 : -1;
     const int dmin = lbvh_delta(keys, n, i, i - d);
     int lmax = 2;
@@ -127,13 +188,15 @@ __global__ __launch_bounds__(kBlock) void k_karras(const uint32_t* __restrict__ 
     } while (t > 1);
     const int gamma = i + s * d + (d < 0 ? -1 : 0);
     const int lo = min(i, j), hi = max(i, j);
-    const int left = (lo == gamma) ? ~gamma : gamma;
-    const int right = (hi == gamma + 1) ? ~(gamma + 1) : gamma + 1;
-    float* f = nodes[i].f;
+    const int left = (lo == gamma) ? ~(lb + gamma) : nb + gamma;
+    const int right = (hi == gamma + 1) ? ~(lb + gamma + 1) : nb + gamma + 1;
+    const int g = nb + i;
+    float* f = nodes[g].f;
     *reinterpret_cast<float2*>(f + 6) = make_float2(__int_as_float(left), __int_as_float(right));
-    ranges[i] = make_int4(lo, hi, gamma, 0);
-    parent[left >= 0 ? left : (n - 1) + ~left] = ((uint32_t)i << 1) | 0u;
-    parent[right >= 0 ? right : (n - 1) + ~right] = ((uint32_t)i << 1) | 1u;
+    ranges[g] = make_int4(lb + lo, lb + hi, lb + gamma, 0);
+    const size_t leaf0 = (size_t)B * (n - 1);
+    parent[left >= 0 ? (size_t)left : leaf0 + ~left] = ((uint32_t)g << 1) | 0u;
+    parent[right >= 0 ? (size_t)right : leaf0 + ~right] = ((uint32_t)g << 1) | 1u;
 }
 
 __device__ inline float down1(float x) { return nextafterf(x, -INFINITY); }
@@ -148,20 +211,22 @@ __device__ inline void store_aabb(BNode* nodes, int node, int side, const float*
 }
 
 __global__ __launch_bounds__(kBlock) void k_refit(const double* __restrict__ plo, const double* __restrict__ phi,
-                                                  const uint32_t* __restrict__ order, int n, BNode* nodes,
-                                                  const uint32_t* __restrict__ parent, uint32_t* flags, double ox,
-                                                  double oy, double oz) {
-    const int leaf = blockIdx.x * kBlock + threadIdx.x;
-    if (leaf >= n) return;
+                                                  const uint32_t* __restrict__ order, int B, int n, BNode* nodes,
+                                                  const uint32_t* __restrict__ parent, uint32_t* flags,
+                                                  const double* __restrict__ orgs) {
+    const long long leaf = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (leaf >= (long long)B * n) return;
+    const int mb = (int)(leaf / n);
+    const int root = mb * (n - 1);
     const uint32_t pr = order[leaf];
-    const double org[3] = {ox, oy, oz};
+    const double org[3] = {orgs[3 * mb], orgs[3 * mb + 1], orgs[3 * mb + 2]};
     float lo[3], hi[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         lo[k] = out_lo(plo[3 * (size_t)pr + k] - org[k]);
         hi[k] = out_hi(phi[3 * (size_t)pr + k] - org[k]);
     }
-    uint32_t p = parent[(n - 1) + leaf];
+    uint32_t p = parent[(size_t)B * (n - 1) + leaf];
     for (int guard = 0; guard < 4096; ++guard) {  // bounded: a tree is never 4096 levels deep
         const int node = (int)(p >> 1), side = (int)(p & 1u);
         store_aabb(nodes, node, side, lo, hi);
@@ -179,18 +244,20 @@ __global__ __launch_bounds__(kBlock) void k_refit(const double* __restrict__ plo
             lo[k] = fminf(a[k], b[k]);
             hi[k] = fmaxf(a[3 + k], b[3 + k]);
         }
-        if (node == 0) return;
+        if (node == root) return;
         p = parent[node];
     }
 }
 
 // depth of every leaf (root's children = 1); out = max
-__global__ __launch_bounds__(kBlock) void k_depth(const uint32_t* __restrict__ parent, int n, unsigned* __restrict__ out) {
-    const int leaf = blockIdx.x * kBlock + threadIdx.x;
-    if (leaf >= n) return;
+__global__ __launch_bounds__(kBlock) void k_depth(const uint32_t* __restrict__ parent, int B, int n,
+                                                  unsigned* __restrict__ out) {
+    const long long leaf = (long long)blockIdx.x * kBlock + threadIdx.x;
+    if (leaf >= (long long)B * n) return;
+    const uint32_t root = (uint32_t)((leaf / n) * (n - 1));
     unsigned d = 1;
-    uint32_t p = parent[(n - 1) + leaf];
-    while ((p >> 1) != 0u && d < 4096u) {
+    uint32_t p = parent[(size_t)B * (n - 1) + leaf];
+    while ((p >> 1) != root && d < 4096u) {
         p = parent[p >> 1];
         ++d;
     }
@@ -228,10 +295,12 @@ __device__ inline int leaf_points(const void* leaves, int i, D3* p) {
 
 template <bool TRI>
 __global__ __launch_bounds__(kBlock) void k_obb(const void* __restrict__ leaves, const int4* __restrict__ ranges, int nn,
-                                                BNode* __restrict__ nodes, double ox, double oy, double oz) {
+                                                int npm, BNode* __restrict__ nodes, const double* __restrict__ orgs) {
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (kBlock / 64);
     for (int node = (blockIdx.x * kBlock + threadIdx.x) >> 6; node < nn; node += waves) {
+        const int mb = node / npm;  // mesh of the node (npm internal nodes per mesh)
+        const double ox = orgs[3 * mb], oy = orgs[3 * mb + 1], oz = orgs[3 * mb + 2];
         const int4 r = ranges[node];
         // area-weighted normal of the node's triangles (points: no area -> axis-aligned frame)
         double sx = 0, sy = 0, sz = 0;
@@ -292,21 +361,23 @@ __global__ __launch_bounds__(kBlock) void k_obb(const void* __restrict__ leaves,
     }
 }
 
-__global__ __launch_bounds__(kBlock) void k_pack_tris(const double* __restrict__ v, const uint32_t* __restrict__ f,
-                                                      const uint32_t* __restrict__ order, size_t T, uint32_t face_base,
-                                                      TriRec* __restrict__ out) {
+// leaf k holds primitive order[k] = b*T + t of mesh b; its face id is the mesh-local t (+ face_base)
+__global__ __launch_bounds__(kBlock) void k_pack_tris(const double* __restrict__ v, size_t P, const uint32_t* __restrict__ f,
+                                                      const uint32_t* __restrict__ order, size_t n, size_t T,
+                                                      uint32_t face_base, TriRec* __restrict__ out) {
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k >= T) return;
-    const uint32_t t = order[k];
+    if (k >= n) return;
+    const size_t g = order[k], b = g / T, t = g - b * T;
+    const double* vb = v + 3 * P * b;
     TriRec r;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-        const size_t vi = f[3 * (size_t)t + c];
-        r.v[3 * c] = v[3 * vi];
-        r.v[3 * c + 1] = v[3 * vi + 1];
-        r.v[3 * c + 2] = v[3 * vi + 2];
+        const size_t vi = f[3 * t + c];
+        r.v[3 * c] = vb[3 * vi];
+        r.v[3 * c + 1] = vb[3 * vi + 1];
+        r.v[3 * c + 2] = vb[3 * vi + 2];
     }
-    r.face = t + face_base;
+    r.face = (uint32_t)t + face_base;
     r.pad = 0;
     out[k] = r;
 }
@@ -328,7 +399,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_points(const double* __restrict
 static unsigned nblocks(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 int tri_bounds(const double* d_v, const uint32_t* d_f, size_t T, double* d_lo, double* d_hi, hipStream_t s) {
-    k_tri_bounds<<<nblocks(T), kBlock, 0, s>>>(d_v, d_f, T, d_lo, d_hi);
+    k_tri_bounds<<<nblocks(T), kBlock, 0, s>>>(d_v, 0, d_f, T, T, d_lo, d_hi);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }
@@ -341,7 +412,7 @@ int point_bounds(const double* d_v, size_t P, double* d_lo, double* d_hi, hipStr
 
 int pack_tri_leaves(const double* d_v, const uint32_t* d_f, const uint32_t* d_order, size_t T, uint32_t face_base,
                     TriRec* d_out, hipStream_t s) {
-    k_pack_tris<<<nblocks(T), kBlock, 0, s>>>(d_v, d_f, d_order, T, face_base, d_out);
+    k_pack_tris<<<nblocks(T), kBlock, 0, s>>>(d_v, 0, d_f, d_order, T, T, face_base, d_out);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }
@@ -354,16 +425,15 @@ int pack_point_leaves(const double* d_v, const uint32_t* d_order, size_t P, PtRe
 
 int build_obb(msh_tree* tree, bool triangles) {
     if (tree->T < 2) return MSH_OK;
-    const int nn = (int)(tree->T - 1);
+    const int nn = (int)(tree->B * (tree->T - 1));
     const unsigned blocks = (unsigned)std::min<size_t>(((size_t)nn + 3) / 4, 65536);
     hipStream_t s = tree->stream;
     const int4* ranges = tree->ws.ranges.as<int4>();
+    const int npm = (int)(tree->T - 1);  // internal nodes per mesh
     if (triangles)
-        k_obb<true><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, tree->d_nodes, tree->origin[0],
-                                              tree->origin[1], tree->origin[2]);
+        k_obb<true><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
     else
-        k_obb<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, tree->d_nodes, tree->origin[0],
-                                               tree->origin[1], tree->origin[2]);
+        k_obb<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }
@@ -474,6 +544,13 @@ int build_bvh4(msh_tree* tree) {
     return MSH_OK;
 }
 
+// device copy of the single-mesh origin (kernels read per-mesh origins from tree->d_orgs)
+int upload_origin(msh_tree* tree, hipStream_t s) {
+    if (!tree->d_orgs) MSH_HIP(hipMalloc(&tree->d_orgs, 3 * sizeof(double)));
+    MSH_HIP(hipMemcpyAsync(tree->d_orgs, tree->origin, 3 * sizeof(double), hipMemcpyHostToDevice, s));
+    return MSH_OK;
+}
+
 int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T, uint32_t* d_order) {
     hipStream_t s = tree->stream;
     Workspace& ws = tree->ws;
@@ -512,12 +589,13 @@ int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T,
         const double c = 0.5 * (box_h[k] + box_h[3 + k]);
         tree->origin[k] = (c == c && fabs(c) < INFINITY) ? c : 0.0;
     }
+    MSH_TRY(upload_origin(tree, s));
     // Morton codes + sort
     MSH_TRY(ws.keys.reserve(T * sizeof(uint32_t)));
     MSH_TRY(ws.keys_alt.reserve(T * sizeof(uint32_t)));
     MSH_TRY(ws.vals_alt.reserve(T * sizeof(uint32_t)));
     uint32_t* keys = ws.keys.as<uint32_t>();
-    k_morton<<<nblocks(T), kBlock, 0, s>>>(d_lo, d_hi, T, d_box, keys, d_order);
+    k_morton<<<nblocks(T), kBlock, 0, s>>>(d_lo, d_hi, T, T, d_box, keys, d_order);
     MSH_HIP(hipGetLastError());
     MSH_TRY(radix_sort_pairs(keys, d_order, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), T, 30, ws, s));
     tree->max_depth = 0;
@@ -529,22 +607,129 @@ int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T,
     MSH_TRY(ws.vals.reserve((2 * T - 1) * sizeof(uint32_t)));
     MSH_TRY(ws.ranges.reserve((T - 1) * sizeof(int4)));
     uint32_t* parent = ws.vals.as<uint32_t>();
-    k_karras<<<nblocks(T - 1), kBlock, 0, s>>>(keys, (int)T, tree->d_nodes, parent, ws.ranges.as<int4>());
+    k_karras<<<nblocks(T - 1), kBlock, 0, s>>>(keys, 1, (int)T, tree->d_nodes, parent, ws.ranges.as<int4>());
     MSH_HIP(hipGetLastError());
     // refit
     uint32_t* flags = ws.flags.as<uint32_t>();
     MSH_HIP(hipMemsetAsync(flags, 0, T * sizeof(uint32_t) + 64, s));
-    k_refit<<<nblocks(T), kBlock, 0, s>>>(d_lo, d_hi, d_order, (int)T, tree->d_nodes, parent, flags, tree->origin[0],
-                                          tree->origin[1], tree->origin[2]);
+    k_refit<<<nblocks(T), kBlock, 0, s>>>(d_lo, d_hi, d_order, 1, (int)T, tree->d_nodes, parent, flags, tree->d_orgs);
     MSH_HIP(hipGetLastError());
     unsigned* d_depth = flags + T;
     MSH_HIP(hipMemsetAsync(d_depth, 0, sizeof(unsigned), s));
-    k_depth<<<nblocks(T), kBlock, 0, s>>>(parent, (int)T, d_depth);
+    k_depth<<<nblocks(T), kBlock, 0, s>>>(parent, 1, (int)T, d_depth);
     MSH_HIP(hipGetLastError());
     unsigned depth = 0;
     MSH_HIP(hipMemcpyAsync(&depth, d_depth, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     MSH_HIP(hipStreamSynchronize(s));
     tree->max_depth = (int)depth;
+    return MSH_OK;
+}
+
+
+// ---- batched build (C4: many meshes sharing one topology) ----
+int tri_bounds_batch(const double* d_v, size_t P, const uint32_t* d_f, size_t B, size_t T, double* d_lo, double* d_hi,
+                     hipStream_t s) {
+    k_tri_bounds<<<nblocks(B * T), kBlock, 0, s>>>(d_v, P, d_f, B * T, T, d_lo, d_hi);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+int pack_tri_leaves_batch(const double* d_v, size_t P, const uint32_t* d_f, const uint32_t* d_order, size_t B, size_t T,
+                          TriRec* d_out, hipStream_t s) {
+    k_pack_tris<<<nblocks(B * T), kBlock, 0, s>>>(d_v, P, d_f, d_order, B * T, T, 0u, d_out);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+static int bits_for(size_t n) {  // bits needed for values in [0, n)
+    int b = 0;
+    while (b < 32 && ((size_t)1 << b) < n) ++b;
+    return b;
+}
+
+int build_lbvh_batch(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T, uint32_t* d_order) {
+    hipStream_t s = tree->stream;
+    Workspace& ws = tree->ws;
+    const size_t B = tree->B, n = B * T;
+    if (n > (size_t)0x7FFFFFFF || B * (T - 1) > (size_t)0x7FFFFFFF) {
+        set_error("batched LBVH build: %zu primitives exceed the 31-bit node index range", n);
+        return MSH_EINVAL;
+    }
+    MSH_HIP(hipMalloc(&tree->d_boxes, 6 * B * sizeof(double)));
+    MSH_HIP(hipMalloc(&tree->d_orgs, 3 * B * sizeof(double)));
+    k_mesh_boxes<<<(unsigned)B, kBlock, 0, s>>>(d_lo, d_hi, T, tree->d_boxes, tree->d_orgs);
+    MSH_HIP(hipGetLastError());
+    // Morton codes in each mesh's own box; sort by code, then (stable) by mesh: order = (mesh, code, id)
+    MSH_TRY(ws.keys.reserve(n * sizeof(uint32_t)));
+    MSH_TRY(ws.keys_alt.reserve(n * sizeof(uint32_t)));
+    MSH_TRY(ws.vals_alt.reserve(n * sizeof(uint32_t)));
+    uint32_t* keys = ws.keys.as<uint32_t>();
+    k_morton<<<nblocks(n), kBlock, 0, s>>>(d_lo, d_hi, n, T, tree->d_boxes, keys, d_order);
+    MSH_HIP(hipGetLastError());
+    MSH_TRY(radix_sort_pairs(keys, d_order, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n, 30, ws, s));
+    if (B > 1) {
+        k_mesh_key<<<nblocks(n), kBlock, 0, s>>>(d_order, n, T, keys);
+        MSH_HIP(hipGetLastError());
+        MSH_TRY(radix_sort_pairs(keys, d_order, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n,
+                                 bits_for(B), ws, s));
+        k_sorted_morton<<<nblocks(n), kBlock, 0, s>>>(d_lo, d_hi, d_order, n, T, tree->d_boxes, keys);
+        MSH_HIP(hipGetLastError());
+    }
+    const size_t nn = B * (T - 1);
+    MSH_TRY(ws.vals.reserve((nn + n) * sizeof(uint32_t)));
+    MSH_TRY(ws.ranges.reserve(nn * sizeof(int4)));
+    uint32_t* parent = ws.vals.as<uint32_t>();
+    k_karras<<<nblocks(nn), kBlock, 0, s>>>(keys, (int)B, (int)T, tree->d_nodes, parent, ws.ranges.as<int4>());
+    MSH_HIP(hipGetLastError());
+    MSH_TRY(ws.flags.reserve(nn * sizeof(uint32_t) + 64));
+    uint32_t* flags = ws.flags.as<uint32_t>();
+    MSH_HIP(hipMemsetAsync(flags, 0, nn * sizeof(uint32_t) + 64, s));
+    k_refit<<<nblocks(n), kBlock, 0, s>>>(d_lo, d_hi, d_order, (int)B, (int)T, tree->d_nodes, parent, flags,
+                                          tree->d_orgs);
+    MSH_HIP(hipGetLastError());
+    unsigned* d_depth = flags + nn;
+    MSH_HIP(hipMemsetAsync(d_depth, 0, sizeof(unsigned), s));
+    k_depth<<<nblocks(n), kBlock, 0, s>>>(parent, (int)B, (int)T, d_depth);
+    MSH_HIP(hipGetLastError());
+    unsigned depth = 0;
+    MSH_HIP(hipMemcpyAsync(&depth, d_depth, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    // overall scene box (informational: msh_tree_get_info)
+    std::unique_ptr<double[]> hb(new double[6 * B]);
+    MSH_HIP(hipMemcpyAsync(hb.get(), tree->d_boxes, 6 * B * sizeof(double), hipMemcpyDeviceToHost, s));
+    MSH_HIP(hipStreamSynchronize(s));
+    for (int k = 0; k < 3; ++k) {
+        double lo = INFINITY, hi = -INFINITY;
+        for (size_t b = 0; b < B; ++b) {
+            lo = std::min(lo, hb[6 * b + k]);
+            hi = std::max(hi, hb[6 * b + 3 + k]);
+        }
+        tree->scene_lo[k] = (float)lo;
+        tree->scene_hi[k] = (float)hi;
+    }
+    tree->max_depth = (int)depth;
+    return MSH_OK;
+}
+
+// query i of mesh i / S: 30-bit Morton code in that mesh's box
+__global__ __launch_bounds__(kBlock) void k_query_morton_batch(const double* __restrict__ q, size_t n, size_t S,
+                                                               const double* __restrict__ boxes,
+                                                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    keys[i] = morton30(q[3 * i], q[3 * i + 1], q[3 * i + 2], boxes + 6 * (i / S));
+    vals[i] = (uint32_t)i;
+}
+
+int mesh_keys(const uint32_t* vals, size_t n, size_t per, uint32_t* keys, hipStream_t s) {
+    k_mesh_key<<<nblocks(n), kBlock, 0, s>>>(vals, n, per, keys);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+int query_morton_batch(const msh_tree* tree, const double* d_q, size_t n, size_t S, uint32_t* keys, uint32_t* vals,
+                       hipStream_t s) {
+    k_query_morton_batch<<<nblocks(n), kBlock, 0, s>>>(d_q, n, S, tree->d_boxes, keys, vals);
+    MSH_HIP(hipGetLastError());
     return MSH_OK;
 }
 

@@ -56,6 +56,7 @@ struct msh_tree {
     size_t P = 0;        // main-mesh vertices
     size_t T = 0;        // leaf primitives
     size_t T_main = 0;   // main-mesh faces (visibility: extra faces follow)
+    size_t B = 1;        // meshes in a batched tree (msh_batch_build; P, T are per mesh); 1 otherwise
     double* d_v = nullptr;         // (P,3) main vertices (visibility sources)
     msh::BNode* d_nodes = nullptr; // T-1 internal nodes (nullptr when T == 1)
     msh::BNode* d_nodes4 = nullptr; // n4 4-wide nodes (2 BNode halves each) for nearest queries
@@ -63,6 +64,8 @@ struct msh_tree {
     void* d_leaves = nullptr;      // T TriRec or PtRec in Morton order
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};  // bbox of all primitives
     double origin[3] = {0, 0, 0};  // fp64 scene-box centre: all fp32 node bounds are relative to it
+    double* d_orgs = nullptr;      // (B,3) per-mesh origins on the device (B = 1: a copy of origin)
+    double* d_boxes = nullptr;     // (B,6) per-mesh boxes (batched trees: query Morton codes)
     hipStream_t stream = nullptr;
     double build_ms = 0.0;
     int max_depth = 0;             // deepest leaf (root children = 1)
@@ -82,6 +85,21 @@ int exclusive_scan_u32(uint32_t* data, size_t n, Workspace& ws, hipStream_t s);
 // prim_lo/prim_hi: (T,3) fp64 bounds per primitive on device.  Builds nodes and the Morton order
 // `order` (sorted position -> primitive id).  scene box written to tree.
 int build_lbvh(msh_tree* tree, const double* d_prim_lo, const double* d_prim_hi, size_t T, uint32_t* d_order);
+// Batched LBVH over tree->B meshes of T primitives each (bounds (B*T,3), mesh b's primitives at
+// [bT, (b+1)T)): per-mesh boxes/origins, Morton codes, two-phase stable radix sort (Morton, then mesh),
+// per-mesh Karras emission with global child references, refit.
+int build_lbvh_batch(msh_tree* tree, const double* d_prim_lo, const double* d_prim_hi, size_t T, uint32_t* d_order);
+int tri_bounds_batch(const double* d_v, size_t P, const uint32_t* d_f, size_t B, size_t T, double* d_lo, double* d_hi,
+                     hipStream_t s);
+int pack_tri_leaves_batch(const double* d_v, size_t P, const uint32_t* d_f, const uint32_t* d_order, size_t B, size_t T,
+                          TriRec* d_out, hipStream_t s);
+// Morton codes of (B*S,3) queries in their mesh's box (query i belongs to mesh i / S) + iota values.
+int query_morton_batch(const msh_tree* tree, const double* d_q, size_t n, size_t S, uint32_t* keys, uint32_t* vals,
+                       hipStream_t s);
+// keys[j] = vals[j] / per (the mesh of element vals[j]), for the second, per-mesh sort phase
+int mesh_keys(const uint32_t* vals, size_t n, size_t per, uint32_t* keys, hipStream_t s);
+// device copy of tree->origin (single-mesh trees; blob unpack)
+int upload_origin(msh_tree* tree, hipStream_t s);
 // Oriented-box pass over the packed leaves (needs the node ranges recorded by build_lbvh).
 int build_obb(msh_tree* tree, bool triangles);
 // 4-wide node array from the finished binary tree (needs max_depth).  Uses ws.keys/vals/keys_alt.
@@ -97,6 +115,9 @@ int point_bounds(const double* d_v, size_t P, double* d_lo, double* d_hi, hipStr
 int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* keys, uint32_t* vals, hipStream_t s);
 int launch_nearest(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S, uint32_t* d_face,
                    uint32_t* d_part, double* d_pt, hipStream_t s);
+// batched trees: n = B*S queries, query i answered on mesh i / S
+int launch_nearest_batch(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t n, size_t S,
+                         uint32_t* d_face, uint32_t* d_part, double* d_pt, hipStream_t s);
 int launch_nearest_stats(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S,
                          unsigned long long* d_counts, hipStream_t s);
 int launch_nnearest(const msh_tree* tree, const double* d_q, const double* d_n, const uint32_t* d_perm, size_t S,

@@ -64,6 +64,11 @@ struct KnnArgs {
     double* out_dist;
     double eps;
     double org[3];  // tree origin: fp32 node bounds are relative to it
+    // batched trees (msh_batch_build): query i belongs to mesh i / qper, whose root is node mesh * npm
+    // and whose origin is orgs[3 * mesh]; orgs == nullptr for a single tree (root 0, origin org)
+    const double* orgs;
+    size_t qper;
+    size_t npm;
     unsigned* counters;
     unsigned ntiles;
     uint2* spill;
@@ -74,6 +79,19 @@ struct KnnArgs {
     unsigned* n_deferred;
     unsigned max_deferred;
 };
+
+// root node and fp32 query of query qi (batched trees: its mesh's root and origin)
+__device__ inline int query_root(const KnnArgs& a, size_t qi, const D3& q, QF& qf) {
+    if (a.orgs) {
+        const size_t mb = qi / a.qper;
+        const double o[3] = {a.orgs[3 * mb], a.orgs[3 * mb + 1], a.orgs[3 * mb + 2]};
+        qf = make_qf(q, o);
+        return (int)(mb * a.npm);
+    }
+    const double o[3] = {a.org[0], a.org[1], a.org[2]};
+    qf = make_qf(q, o);
+    return 0;
+}
 
 __device__ inline unsigned dequeue_tile(unsigned* counters, unsigned ntiles, unsigned group) {
     for (unsigned k = 0; k < 8; ++k) {
@@ -529,8 +547,9 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             pol.test(0);
             if (STATS) ++n_leaves;
         } else {
-            const QF qf = make_qf(q, a.org);
-            Walker w{0, 0};
+            QF qf;
+            const int root = query_root(a, qi, q, qf);
+            Walker w{root, 0};
             bool active = true, deferred = false;
             int p0 = -1, p1 = -1, p2 = -1, p3 = -1;  // leaf children waiting for a wave-wide leaf phase
             const bool wide = a.nodes4 != nullptr;
@@ -642,7 +661,8 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         const DeferRec r = a.deferred[item];
         const size_t qi = r.qi;
         const D3 q = D3{a.q[3 * qi], a.q[3 * qi + 1], a.q[3 * qi + 2]};
-        const QF qf = make_qf(q, a.org);
+        QF qf;
+        const int root = query_root(a, qi, q, qf);
         auto pol = make_pol<MODE>(a, qi, q);
         pol.shared = r.best;  // pass-1 best: an upper bound of the final best
         if (lane == 0) {
@@ -652,7 +672,7 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         }
         // breadth-first expansion of the top of the tree into <= kFront subtrees
         int cur = 0, n = 1;
-        if (lane == 0) front[wv][0][0] = make_uint2(0u, 0u);
+        if (lane == 0) front[wv][0][0] = make_uint2((unsigned)root, 0u);
         __builtin_amdgcn_wave_barrier();
         while (n > 0 && n <= kFront / 2) {
             int m = 0;
@@ -826,6 +846,16 @@ int launch_nearest(const msh_tree* tree, const double* d_q, const uint32_t* d_pe
     a.q = d_q; a.perm = d_perm; a.S = S;
     a.out_face = d_face; a.out_part = d_part; a.out_pt = d_pt;
     return launch_knn<0, false>(const_cast<msh_tree*>(tree), a, s, "nearest");
+}
+
+int launch_nearest_batch(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t n, size_t S,
+                         uint32_t* d_face, uint32_t* d_part, double* d_pt, hipStream_t s) {
+    KnnArgs a{};
+    a.nodes = tree->d_nodes; a.leaves = tree->d_leaves; a.T = tree->T;
+    a.q = d_q; a.perm = d_perm; a.S = n;
+    a.out_face = d_face; a.out_part = d_part; a.out_pt = d_pt;
+    a.orgs = tree->d_orgs; a.qper = S; a.npm = tree->T - 1;
+    return launch_knn<0, false>(const_cast<msh_tree*>(tree), a, s, "nearest_batch");
 }
 
 int launch_nearest_stats(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S,

@@ -8,7 +8,7 @@ import numpy as np
 
 from . import _native as N
 
-__all__ = ['AabbTree', 'AabbNormalsTree', 'ClosestPointTree', 'CGALClosestPointTree']
+__all__ = ['AabbTree', 'AabbNormalsTree', 'ClosestPointTree', 'CGALClosestPointTree', 'AabbTreeBatch']
 
 
 class AabbTree(object):
@@ -113,3 +113,35 @@ class AabbNormalsTree(object):
         from . import aabb_normals
         closest_tri, closest_p = aabb_normals.aabbtree_n_nearest(self.tree_handle, v_samples, n_samples)
         return (closest_tri, closest_p)
+
+
+class AabbTreeBatch(object):
+    """Many meshes sharing one topology, searched together (scan-to-mesh registration, BASELINE C4).
+
+    The reference answers this with one ``AabbTree`` per mesh (search.py:21-30); ``AabbTreeBatch(v, f)``
+    builds all B trees in one batched GPU build and ``nearest(q)`` answers every mesh's queries in one
+    launch.  ``nearest(q)[..., b]`` equals ``AabbTree(mesh_b).nearest(q[b])`` with mesh-local face
+    indices; shapes gain a leading mesh axis: face (B,S) uint32, part (B,S) uint32, point (B,S,3).
+    """
+
+    def __init__(self, v, f):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        f = np.ascontiguousarray(f, dtype=np.uint32)
+        if v.ndim != 3 or v.shape[2] != 3:
+            raise ValueError("Vertices must be BxPx3")
+        if f.ndim != 2 or f.shape[1] != 3:
+            raise ValueError("Faces must be Tx3")
+        self.n_meshes = v.shape[0]
+        self.cpp_handle = N.build_batch(v, f)
+
+    def nearest(self, v_samples, nearest_part=False):
+        q = np.ascontiguousarray(v_samples, dtype=np.float64)
+        if q.ndim != 3 or q.shape[0] != self.n_meshes or q.shape[2] != 3:
+            raise ValueError("Queries must be BxSx3 with B = %d" % self.n_meshes)
+        B, S = q.shape[0], q.shape[1]
+        face = np.empty((B, S), dtype=np.uint32)
+        part = np.empty((B, S), dtype=np.uint32)
+        pt = np.empty((B, S, 3), dtype=np.float64)
+        N.check(N.lib().msh_batch_nearest(self.cpp_handle.ptr, N.dptr(q), S, N.uptr(face), N.uptr(part),
+                                          N.dptr(pt)))
+        return (face, part, pt) if nearest_part else (face, pt)

@@ -124,3 +124,18 @@ def test_fp32_cull_bounds_are_conservative(tmp_path):
     out = subprocess.run([exe, "1000000"], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr
     assert "violations=0" in out.stdout
+
+
+def test_batch_build_validation():
+    # argument checks run on the host, before any device work
+    from mesh_amd import _native
+    L = _native.lib()
+    v = np.zeros((2, 3, 3))
+    f1 = np.array([[0, 1, 2]], np.uint32)
+    out = ctypes.c_void_p()
+    assert L.msh_batch_build(_native.dptr(v), 2, 3, _native.uptr(f1), 1, ctypes.byref(out)) == _native.MSH_EINVAL
+    assert b"T >= 2" in L.msh_last_error()
+    f2 = np.array([[0, 1, 2], [0, 2, 9]], np.uint32)
+    assert L.msh_batch_build(_native.dptr(v), 2, 3, _native.uptr(f2), 2, ctypes.byref(out)) == _native.MSH_EINVAL
+    assert b"references vertex 9" in L.msh_last_error()
+    assert L.msh_batch_nearest(None, None, 0, None, None, None) == _native.MSH_EINVAL

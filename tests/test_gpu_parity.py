@@ -402,3 +402,89 @@ def test_tree_bounds_contain_primitives(name):
     assert r["aabb_containment_violations"] == 0 and r["obb_containment_violations"] == 0, r
     assert r["reached_nodes"] == f.shape[0] - 1
     assert r["worst_relative_aabb_looseness_first2000"] < 1e-3, r
+
+
+def test_many_tied_candidates(oracle):
+    # Queries radially above / below icosphere vertices: the closest point is the vertex, shared by 5-6
+    # faces at exactly equal distance, so more tied candidates than the pass-1 candidate list holds
+    # (overflow -> exact on the spot) — the lexmin (d2, face) must still be bit-exact.
+    v, f = W.geodesic_icosphere(40)
+    q = np.vstack([v * 1.05, v * 0.95, v * 1.5])
+    face, _, _ = _assert_bit_exact_vs_brute(oracle, v, f, q)
+    assert face.shape[0] == q.shape[0]
+
+
+def test_wide_traversal_bit_exact(tmp_path):
+    # MESH_AMD_TRAVERSAL=wide (4-wide nodes) is read once per process: run it in one child process
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "wide.py"
+    script.write_text(
+        "import sys, numpy as np\n"
+        "sys.path.insert(0, %r)\n"
+        "import workloads as W\n"
+        "from mesh_amd import spatialsearch, _native\n"
+        "from oracle import oracle\n"
+        "_native.set_device(0)\n"
+        "v, f = W.c2_mesh()\n"
+        "q = W.uniform_in_box(v.min(0) - 0.1, v.max(0) + 0.1, 50000, seed=31)\n"
+        "t = spatialsearch.aabbtree_compute(v, f)\n"
+        "face, part, pt = spatialsearch.aabbtree_nearest(t, q)\n"
+        "bf, bp, bpt, _ = oracle.brute_nearest(v, f, q)\n"
+        "assert np.array_equal(face[0], bf) and np.array_equal(part[0], bp) and np.array_equal(pt, bpt)\n"
+        "print('wide ok')\n" % root)
+    env = dict(os.environ, MESH_AMD_TRAVERSAL="wide")
+    r = subprocess.run([sys.executable, str(script)], env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "wide ok" in r.stdout, r.stderr[-2000:]
+
+
+def test_batch_bit_exact_per_mesh(oracle):
+    # C4 shape at small B: the batched build + query must equal, mesh by mesh, the exhaustive answer
+    from mesh_amd.search import AabbTreeBatch
+    B = 6
+    f = W.c4_mesh(0)[1]
+    v = np.stack([W.c4_mesh(i)[0] for i in range(B)])
+    rng = np.random.default_rng(41)
+    q = np.empty((B, 3000, 3))
+    for b in range(B):
+        s, _ = W.surface_samples(v[b], f, 2000, seed=100 + b, sigma=0.003)
+        lo, hi = v[b].min(0), v[b].max(0)
+        q[b] = np.vstack([s, rng.uniform(lo - 0.05, hi + 0.05, (1000, 3))])
+    face, part, pt = AabbTreeBatch(v, f).nearest(q, nearest_part=True)
+    assert face.shape == (B, 3000) and part.shape == (B, 3000) and pt.shape == (B, 3000, 3)
+    for b in range(B):
+        bf, bp, bpt, _ = oracle.brute_nearest(v[b], f, q[b])
+        assert np.array_equal(face[b], bf), b
+        assert np.array_equal(part[b], bp), b
+        assert np.array_equal(pt[b], bpt), b
+
+
+def test_batch_matches_single_trees():
+    from mesh_amd import spatialsearch
+    from mesh_amd.search import AabbTreeBatch
+    B = 3
+    f = W.c4_mesh(0)[1]
+    v = np.stack([W.c4_mesh(i)[0] + i for i in range(B)])  # different boxes / origins per mesh
+    q = np.stack([W.uniform_in_box(v[b].min(0), v[b].max(0), 20000, seed=50 + b) for b in range(B)])
+    face, part, pt = AabbTreeBatch(v, f).nearest(q, nearest_part=True)
+    for b in range(B):
+        t = spatialsearch.aabbtree_compute(np.ascontiguousarray(v[b]), f)
+        sf, sp, spt = spatialsearch.aabbtree_nearest(t, q[b])
+        assert np.array_equal(face[b], sf[0]) and np.array_equal(part[b], sp[0]) and np.array_equal(pt[b], spt)
+
+
+def test_c4_full_size(oracle):
+    # BASELINE configs[3]: 4096 meshes x 10k scan points; exact vs brute force on 6 meshes, properties on all
+    from mesh_amd.search import AabbTreeBatch
+    v, f, q = W.c4_batch()
+    face, part, pt = AabbTreeBatch(v, f).nearest(q, nearest_part=True)
+    assert face.max() < f.shape[0] and part.max() <= 6 and np.isfinite(pt).all()
+    for b in np.random.default_rng(7).choice(v.shape[0], 6, replace=False):
+        bf, bp, bpt, _ = oracle.brute_nearest(v[b], f, q[b])
+        assert np.array_equal(face[b], bf) and np.array_equal(part[b], bp) and np.array_equal(pt[b], bpt), b
+    # every point is on its face's triangle (barycentric check, all 41M rows)
+    tri = v[np.arange(v.shape[0])[:, None], f[face.astype(np.int64)]]
+    n = np.cross(tri[..., 1, :] - tri[..., 0, :], tri[..., 2, :] - tri[..., 0, :])
+    off = np.abs(np.einsum("bsk,bsk->bs", pt - tri[..., 0, :], n)) / np.linalg.norm(n, axis=-1)
+    assert off.max() < 1e-9

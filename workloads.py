@@ -157,3 +157,16 @@ def c4_mesh(i):
     rng = np.random.default_rng(4 + i)
     radii = rng.uniform(0.07, 0.12, size=3)
     return _radial_noise(v, rng) * radii, f
+
+
+def c4_batch(B=4096, S=10_000, seed=4):
+    """C4 (BASELINE configs[3]): B meshes of the 72x70+2 UV topology (5,042 v / 10,080 f), per-mesh
+    shape c4_mesh(i), and S scan points per mesh = surface samples + N(0, 0.005 diag) noise.
+    Returns v (B,P,3), f (T,3), q (B,S,3)."""
+    f = c4_mesh(0)[1]
+    v = np.stack([c4_mesh(i)[0] for i in range(B)])
+    q = np.empty((B, S, 3))
+    for i in range(B):
+        diag = float(np.linalg.norm(v[i].max(0) - v[i].min(0)))
+        q[i] = surface_samples(v[i], f, S, seed=seed * 100003 + i, sigma=0.005 * diag)[0]
+    return v, f, q
