@@ -144,7 +144,6 @@ static void free_tree(msh_tree* t) {
     t->ws.release();
     if (t->d_v) (void)hipFree(t->d_v);
     if (t->d_nodes) (void)hipFree(t->d_nodes);
-    if (t->d_nodes4) (void)hipFree(t->d_nodes4);
     if (t->d_orgs) (void)hipFree(t->d_orgs);
     if (t->d_boxes) (void)hipFree(t->d_boxes);
     if (t->d_leaves) (void)hipFree(t->d_leaves);
@@ -197,7 +196,6 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
                                   static_cast<TriRec*>(t->d_leaves), s)) != MSH_OK)
             break;
         if ((st = build_obb(t, true)) != MSH_OK) break;
-        if ((st = build_bvh4(t)) != MSH_OK) break;
         (void)hipEventRecord(e1, s);
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) { set_error("LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
@@ -370,7 +368,6 @@ int msh_points_build(const double* v, size_t P, msh_tree** out) {
         if ((st = pack_point_leaves(t->d_v, dOrder.as<uint32_t>(), P, static_cast<PtRec*>(t->d_leaves), s)) != MSH_OK)
             break;
         if ((st = build_obb(t, false)) != MSH_OK) break;
-        if ((st = build_bvh4(t)) != MSH_OK) break;
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) { set_error("point LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
     } while (0);
@@ -757,9 +754,8 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
             break;
         }
         if ((st = upload_origin(t, t->stream)) != MSH_OK) break;
-        st = build_bvh4(t);  // the 4-wide nearest-query nodes are derived, not shipped
-        if (st == MSH_OK && hipStreamSynchronize(t->stream) != hipSuccess) {
-            set_error("blob unpack: 4-wide node build failed");
+        if (hipStreamSynchronize(t->stream) != hipSuccess) {
+            set_error("blob unpack: origin upload failed");
             st = MSH_EDEVICE;
         }
         t->ws.release();

@@ -438,112 +438,6 @@ int build_obb(msh_tree* tree, bool triangles) {
     return MSH_OK;
 }
 
-// ---- 4-wide tree for nearest queries ----
-// The binary tree is collapsed two levels at a time: every internal binary node at even depth becomes a
-// 4-wide node made of two BNode-shaped halves, one per binary child A of it.  An internal A contributes
-// itself verbatim (its frame, its two children and their boxes); a leaf A contributes a one-child half
-// holding A's boxes and frame from the parent, with the second slot empty (kEmpty4).  Nothing is
-// recomputed, so every bound is bit-identical to the binary tree's; internal child indices are
-// remapped to 4-wide node indices.
-__global__ __launch_bounds__(kBlock) void k_parents(const BNode* __restrict__ nodes, int nn, uint32_t* __restrict__ parent) {
-    const int x = blockIdx.x * kBlock + threadIdx.x;
-    if (x >= nn) return;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        const int c = __float_as_int(nodes[x].f[6 + s]);
-        if (c >= 0 && c < nn) parent[c] = (uint32_t)x;
-    }
-    if (x == 0) parent[0] = 0xFFFFFFFFu;
-}
-
-// flag[x] = 1 for internal nodes at even depth (the 4-wide node roots)
-__global__ __launch_bounds__(kBlock) void k_even_depth(const uint32_t* __restrict__ parent, int nn, int max_depth,
-                                                       uint32_t* __restrict__ flag) {
-    const int x = blockIdx.x * kBlock + threadIdx.x;
-    if (x >= nn) return;
-    int d = 0;
-    uint32_t p = (uint32_t)x;
-    while (p != 0u && d <= max_depth) {
-        p = parent[p];
-        ++d;
-    }
-    flag[x] = (d & 1) == 0 ? 1u : 0u;
-}
-
-__global__ __launch_bounds__(kBlock) void k_emit4(const BNode* __restrict__ nodes, int nn, const uint32_t* __restrict__ flag,
-                                                  const uint32_t* __restrict__ idx, BNode* __restrict__ out) {
-    const int x = blockIdx.x * kBlock + threadIdx.x;
-    if (x >= nn || !flag[x]) return;
-    const BNode& nx = nodes[x];
-    BNode* o = out + 2 * (size_t)idx[x];
-#pragma unroll
-    for (int side = 0; side < 2; ++side) {
-        const int a = __float_as_int(nx.f[6 + side]);
-        BNode h;
-        if (a >= 0) {
-            h = nodes[a];
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const int c = __float_as_int(h.f[6 + s]);
-                if (c >= 0) h.f[6 + s] = __int_as_float((int)idx[c]);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 32; ++k) h.f[k] = 0.f;
-#pragma unroll
-            for (int k = 0; k < 6; ++k) h.f[k] = nx.f[k];
-            h.f[6] = __int_as_float(a);
-            h.f[7] = __int_as_float(kEmpty4);
-#pragma unroll
-            for (int k = 0; k < 6; ++k) {
-                h.f[kAabb[0] + k] = nx.f[kAabb[side] + k];
-                h.f[kObb[0] + k] = nx.f[kObb[side] + k];
-            }
-        }
-        o[side] = h;
-    }
-}
-
-int build_bvh4(msh_tree* tree) {
-    if (tree->d_nodes4) {
-        (void)hipFree(tree->d_nodes4);
-        tree->d_nodes4 = nullptr;
-        tree->n4 = 0;
-    }
-    if (tree->T < 2) return MSH_OK;
-    hipStream_t s = tree->stream;
-    Workspace& ws = tree->ws;
-    const int nn = (int)(tree->T - 1);
-    MSH_TRY(ws.keys.reserve((size_t)nn * sizeof(uint32_t)));
-    MSH_TRY(ws.vals.reserve((size_t)nn * sizeof(uint32_t) + 64));
-    uint32_t* parent = ws.keys.as<uint32_t>();
-    uint32_t* idx = ws.vals.as<uint32_t>();
-    k_parents<<<nblocks(nn), kBlock, 0, s>>>(tree->d_nodes, nn, parent);
-    MSH_HIP(hipGetLastError());
-    k_even_depth<<<nblocks(nn), kBlock, 0, s>>>(parent, nn, tree->max_depth + 1, idx);
-    MSH_HIP(hipGetLastError());
-    // flags -> exclusive prefix (4-wide index); the flag of x is recovered as idx[x+1] - idx[x]
-    MSH_TRY(ws.keys_alt.reserve((size_t)nn * sizeof(uint32_t)));
-    uint32_t* flag = ws.keys_alt.as<uint32_t>();
-    MSH_HIP(hipMemcpyAsync(flag, idx, (size_t)nn * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-    MSH_TRY(exclusive_scan_u32(idx, (size_t)nn, ws, s));
-    uint32_t last_idx = 0, last_flag = 0;
-    MSH_HIP(hipMemcpyAsync(&last_idx, idx + nn - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    MSH_HIP(hipMemcpyAsync(&last_flag, flag + nn - 1, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    MSH_HIP(hipStreamSynchronize(s));
-    const size_t n4 = (size_t)last_idx + last_flag;
-    hipError_t e = hipMalloc(&tree->d_nodes4, n4 * 2 * sizeof(BNode));
-    if (e != hipSuccess) {
-        tree->d_nodes4 = nullptr;
-        set_error("hipMalloc 4-wide nodes: %s", hipGetErrorString(e));
-        return MSH_ENOMEM;
-    }
-    tree->n4 = n4;
-    k_emit4<<<nblocks(nn), kBlock, 0, s>>>(tree->d_nodes, nn, flag, idx, tree->d_nodes4);
-    MSH_HIP(hipGetLastError());
-    return MSH_OK;
-}
-
 // device copy of the single-mesh origin (kernels read per-mesh origins from tree->d_orgs)
 int upload_origin(msh_tree* tree, hipStream_t s) {
     if (!tree->d_orgs) MSH_HIP(hipMalloc(&tree->d_orgs, 3 * sizeof(double)));

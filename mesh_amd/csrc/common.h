@@ -35,7 +35,6 @@ struct alignas(16) BNode {
     float f[32];
 };
 static_assert(sizeof(BNode) == 128, "BNode must be 128 B");
-constexpr int kEmpty4 = 0x7FFFFFFF;  // empty slot of a 4-wide node half
 constexpr int kAabb[2] = {8, 20};
 constexpr int kObb[2] = {14, 26};
 
@@ -327,7 +326,10 @@ __host__ __device__ inline void tri_d2_bounds(float ax, float ay, float az, floa
     // conditioning 1/sin^2 <= 100 (sliver guard above), i.e. ~2^-17.4 M; 2^-15 M leaves a 5x cushion.
     // Measured: over 10^7 random/adversarial cases (tests/csrc/pretest_check.cpp) violations first
     // appear with a 2^-21 M margin, 64x below the one used.
-    const float dist = sqrtf(px * px + py * py + pz * pz), mg = M * 3.0517578125e-5f;  // 2^-15
+#ifndef MSH_PRETEST_MARGIN
+#define MSH_PRETEST_MARGIN 3.0517578125e-5f  // 2^-15
+#endif
+    const float dist = sqrtf(px * px + py * py + pz * pz), mg = M * MSH_PRETEST_MARGIN;
     const float dl = dist - mg, dh = dist + mg;
     lo = dl > 0.f ? dl * dl * 0.999999523162841796875f : (dl <= 0.f ? 0.f : dl);  // 1 - 2^-21; NaN propagates
     hi = dh * dh * 1.00000095367431640625f;  // 1 + 2^-20 (NaN propagates: never prunes)

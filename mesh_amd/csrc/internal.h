@@ -59,8 +59,6 @@ struct msh_tree {
     size_t B = 1;        // meshes in a batched tree (msh_batch_build; P, T are per mesh); 1 otherwise
     double* d_v = nullptr;         // (P,3) main vertices (visibility sources)
     msh::BNode* d_nodes = nullptr; // T-1 internal nodes (nullptr when T == 1)
-    msh::BNode* d_nodes4 = nullptr; // n4 4-wide nodes (2 BNode halves each) for nearest queries
-    size_t n4 = 0;
     void* d_leaves = nullptr;      // T TriRec or PtRec in Morton order
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};  // bbox of all primitives
     double origin[3] = {0, 0, 0};  // fp64 scene-box centre: all fp32 node bounds are relative to it
@@ -102,8 +100,6 @@ int mesh_keys(const uint32_t* vals, size_t n, size_t per, uint32_t* keys, hipStr
 int upload_origin(msh_tree* tree, hipStream_t s);
 // Oriented-box pass over the packed leaves (needs the node ranges recorded by build_lbvh).
 int build_obb(msh_tree* tree, bool triangles);
-// 4-wide node array from the finished binary tree (needs max_depth).  Uses ws.keys/vals/keys_alt.
-int build_bvh4(msh_tree* tree);
 int tri_bounds(const double* d_v, const uint32_t* d_f, size_t T, double* d_lo, double* d_hi, hipStream_t s);
 int pack_tri_leaves(const double* d_v, const uint32_t* d_f, const uint32_t* d_order, size_t T, uint32_t face_base,
                     TriRec* d_out, hipStream_t s);

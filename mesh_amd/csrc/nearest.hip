@@ -51,7 +51,6 @@ static_assert(sizeof(DeferRec) == 32, "DeferRec must be 32 B");
 
 struct KnnArgs {
     const BNode* nodes;
-    const BNode* nodes4;  // 4-wide nodes (2 halves each) for pass 1; nullptr -> binary walk
     const void* leaves;
     size_t T;
     const double* q;
@@ -388,51 +387,6 @@ struct Walker {
     }
 };
 
-// One step on the 4-wide tree: both halves of node w.node give two child bounds each; leaf children
-// that survive are parked in p0..p3 (slot k -> pk, -1 = none), internal ones are
-// ordered nearest first: the nearest is entered, the others pushed farthest-first.
-template <class Pol, bool STATS>
-__device__ inline bool step4_collect(Walker& w, const BNode* __restrict__ nodes4, const QF& qf, const Pol& pol,
-                                     uint2* __restrict__ lds, uint2* __restrict__ spill, unsigned& n_nodes, int& p0,
-                                     int& p1, int& p2, int& p3) {
-    const NodeV ha = load_node(nodes4, 2 * w.node);
-    const NodeV hb = load_node(nodes4, 2 * w.node + 1);
-    if (STATS) ++n_nodes;
-    float d0, d1, d2, d3;
-    node_child_bounds(ha, qf, d0, d1);
-    node_child_bounds(hb, qf, d2, d3);
-    int c0 = ha.child(0), c1 = ha.child(1), c2 = hb.child(0), c3 = hb.child(1);
-    const float lim = __double2float_ru(pol.limit());
-    int nh = 0;
-    // classify one slot: a surviving leaf is parked in its own pending register, a surviving internal
-    // child gets its bound as sort key (bounds are >= 0, so uint order = float order; misses sort last)
-    auto slot = [&](int c, float d, int& pend) -> unsigned {
-        const bool hit = c != kEmpty4 && d <= lim;
-        pend = hit && c < 0 ? ~c : -1;
-        const bool inner = hit && c >= 0;
-        nh += inner ? 1 : 0;
-        return inner ? __float_as_uint(d) : 0xFFFFFFFFu;
-    };
-    unsigned k0 = slot(c0, d0, p0), k1 = slot(c1, d1, p1), k2 = slot(c2, d2, p2), k3 = slot(c3, d3, p3);
-    if (nh == 0) return w.pop(pol, lds, spill);
-    auto cswap = [](unsigned& ka, int& ca, unsigned& kb, int& cb) {
-        if (kb < ka) {
-            const unsigned tk = ka; ka = kb; kb = tk;
-            const int tc = ca; ca = cb; cb = tc;
-        }
-    };
-    cswap(k0, c0, k1, c1);
-    cswap(k2, c2, k3, c3);
-    cswap(k0, c0, k2, c2);
-    cswap(k1, c1, k3, c3);
-    cswap(k1, c1, k2, c2);
-    if (nh > 3) w.push(make_uint2((unsigned)c3, k3), lds, spill);
-    if (nh > 2) w.push(make_uint2((unsigned)c2, k2), lds, spill);
-    if (nh > 1) w.push(make_uint2((unsigned)c1, k1), lds, spill);
-    w.node = c0;
-    return true;
-}
-
 // Outputs of one query from its policy (winner's leaf -> point / part recomputed exactly).
 template <int MODE, class Pol>
 __device__ inline void write_result(const KnnArgs& a, size_t qi, const D3& q, const Pol& pol) {
@@ -488,24 +442,21 @@ __device__ inline typename PolOf<MODE>::T make_pol(const KnnArgs& a, size_t qi, 
     return pol;
 }
 
-// Test the parked leaves p0..p3 (-1 = empty) through ONE call site: the registers rotate, so the
-// (large, fp64) leaf test is instantiated once instead of once per slot.
+// Test the parked leaves p0, p1 (-1 = empty).
 template <class Pol>
-__device__ inline void test_pending(Pol& pol, int& p0, int& p1, int& p2, int& p3) {
-#pragma unroll 1
-    while (max(max(p0, p1), max(p2, p3)) >= 0) {
-        if (p0 >= 0) pol.test(p0);
-        p0 = p1;
-        p1 = p2;
-        p2 = p3;
-        p3 = -1;
-    }
+__device__ inline void test_pending(Pol& pol, int& p0, int& p1) {
+    if (p0 >= 0) pol.test(p0);
+    if (p1 >= 0) pol.test(p1);
+    p0 = p1 = -1;
 }
 
 // pass-1 policy: candidate-deferring triangles for plain closest point, the exact policies otherwise
+#ifndef MSH_CAND
+#define MSH_CAND 1
+#endif
 template <int MODE>
 __device__ inline auto make_pol1(const KnnArgs& a, size_t qi, const D3& q) {
-    if constexpr (MODE == 0) {
+    if constexpr (MODE == 0 && MSH_CAND) {
         TriCandPol pol;
         pol.tris = static_cast<const TriRec*>(a.leaves);
         pol.q = q;
@@ -551,15 +502,14 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             const int root = query_root(a, qi, q, qf);
             Walker w{root, 0};
             bool active = true, deferred = false;
-            int p0 = -1, p1 = -1, p2 = -1, p3 = -1;  // leaf children waiting for a wave-wide leaf phase
-            const bool wide = a.nodes4 != nullptr;
+            int p0 = -1, p1 = -1;  // leaf children waiting for a wave-wide leaf phase
             size_t steps = 0;
             // Wave-synchronous loop.  Lanes that reach leaves park them; leaf tests run when the
             // parked lanes are at least a third of the busy ones (or nobody can traverse), so the
             // expensive fp64 leaf path executes for many lanes at once instead of stalling the wave
             // on one lane every iteration (Aila & Laine 2009, "postponed leaf" while-while).
             for (;;) {
-                const bool parked = max(max(p0, p1), max(p2, p3)) >= 0;
+                const bool parked = p0 >= 0;
                 const unsigned long long bp = __ballot(parked);
                 const unsigned long long bt = __ballot(active && !parked);
                 if ((bp | bt) == 0ull) break;
@@ -570,8 +520,8 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         u_leaf_lanes += np;
                     }
                     if (parked) {
-                        if (STATS) n_leaves += (p0 >= 0) + (p1 >= 0) + (p2 >= 0) + (p3 >= 0);
-                        test_pending(pol, p0, p1, p2, p3);
+                        if (STATS) n_leaves += 1 + (p1 >= 0);
+                        test_pending(pol, p0, p1);
                     }
                     continue;
                 }
@@ -580,15 +530,13 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     u_trav_lanes += nt;
                 }
                 if (active && !parked) {
-                    active = wide ? step4_collect<decltype(pol), STATS>(w, a.nodes4, qf, pol, lds, spill, n_nodes, p0,
-                                                                        p1, p2, p3)
-                                  : w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, p0, p1);
+                    active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, p0, p1);
                     ++steps;
                     if (active && steps >= a.T) active = false;  // each node is entered once: corrupt tree
                     if (active && steps == a.budget) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
                         if (slot < a.max_deferred) {
-                            test_pending(pol, p0, p1, p2, p3);
+                            test_pending(pol, p0, p1);
                             pol.flush();
                             DeferRec r;
                             r.qi = (uint32_t)qi;
@@ -785,16 +733,6 @@ static int device_cus(int dev) {
 constexpr unsigned kBudget = 2048;  // pass-1 node steps per lane before a query is deferred
 
 // Common launch: grid, counters, spill area, deferred list; pass 1 then pass 2.
-// Pass 1 walks the binary tree; MESH_AMD_TRAVERSAL=wide selects the 4-wide tree (measured slower on
-// C3: half the steps at twice the cost each, plus 28% more leaf tests).
-static bool wide_traversal() {
-    static const bool w = [] {
-        const char* e = getenv("MESH_AMD_TRAVERSAL");
-        return e && strcmp(e, "wide") == 0;
-    }();
-    return w;
-}
-
 template <int MODE, bool STATS>
 static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* timer) {
     if (a.S == 0) return MSH_OK;
@@ -812,9 +750,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     MSH_HIP(hipMemsetAsync(a.counters, 0, 9 * 32 * sizeof(unsigned), s));
     // pass 2 lanes carry up to kFront/64 dealt subtrees on top of a depth-first path
     const unsigned nblk2 = ncu * 2u;
-    a.nodes4 = wide_traversal() ? tree->d_nodes4 : nullptr;
-    // binary walk: one push per level; 4-wide: up to 3 pushes per 4-wide level (= 2 binary levels)
-    const int need = std::max(tree->max_depth + 1 + kFront / 64 + 1, 3 * (tree->max_depth / 2 + 1) + 2);
+    const int need = tree->max_depth + 1 + kFront / 64 + 1;
     a.spill = nullptr;
     a.spill_depth = 0;
     if (need > kStack) {

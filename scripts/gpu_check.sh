@@ -23,6 +23,7 @@ for s in $STAGES; do
         MESH_AMD_LIB=$PWD/$so timeout -k 10 300 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/var_$n.log 2>&1; ok var_$n $?
       done ;;
     bench_wide) MESH_AMD_TRAVERSAL=wide timeout -k 10 600 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_wide.log 2>&1; ok bench_wide $? ;;
+    configs) timeout -k 10 900 python scripts/bench_configs.py > gpurun_out/bench_configs.log 2>&1; ok configs $? ;;
     bench)  timeout -k 10 900 python bench.py > gpurun_out/bench.log 2>&1; ok bench $? ;;
     prof_small) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof_small" -o run -- python3 "$OLDPWD/bench.py" --queries 10000000 --steps 2 --warmup 1 --no-cpu > "$OLDPWD/gpurun_out/prof_small.log" 2>&1); ok prof_small $? ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 3 --warmup 1 --no-cpu > "$OLDPWD/gpurun_out/prof.log" 2>&1); ok prof $? ;;
