@@ -123,7 +123,6 @@ struct TriPol {
     double best, shared;
     uint32_t best_face;
     int best_leaf;
-    unsigned n_exact;  // exact constructions run (statistics only)
     __device__ double limit() const { return fmin(best, shared) * kSlack; }
     __device__ void flush() {}
     __device__ void test(int leaf) {
@@ -136,7 +135,6 @@ struct TriPol {
         rel_f32(c, q, cx, cy, cz);
         const float lo = tri_d2_lo(ax, ay, az, bx, by, bz, cx, cy, cz);
         if (lo > __double2float_ru(limit())) return;  // NaN never rejects
-        ++n_exact;
 #ifdef MSH_DIAG_SKIP_EXACT  // timing diagnostic only: wrong results
         if ((double)lo < best) { best = lo; best_face = face; best_leaf = leaf; }
         return;
@@ -434,7 +432,6 @@ __device__ inline typename PolOf<MODE>::T make_pol(const KnnArgs& a, size_t qi, 
         pol.eps = a.eps;
         pol.pmin = fmin(a.eps * (1 - nq), a.eps * (1 + nq));
     }
-    if constexpr (MODE == 0) pol.n_exact = 0;
     pol.best = INFINITY;
     pol.shared = INFINITY;
     pol.best_face = 0xFFFFFFFFu;
@@ -451,8 +448,11 @@ __device__ inline void test_pending(Pol& pol, int& p0, int& p1) {
 }
 
 // pass-1 policy: candidate-deferring triangles for plain closest point, the exact policies otherwise
+// MSH_CAND=1 selects TriCandPol for pass 1.  Off by default: on C3 it cut exact constructions from 10
+// to 5.4 per query but cost 18 VGPRs (3 instead of 4 waves/SIMD) and 2% more node visits: 293M vs
+// 332M queries/s (10M queries, one MI355X).
 #ifndef MSH_CAND
-#define MSH_CAND 1
+#define MSH_CAND 0
 #endif
 template <int MODE>
 __device__ inline auto make_pol1(const KnnArgs& a, size_t qi, const D3& q) {
@@ -557,7 +557,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         }
         pol.flush();
         if (!STATS) write_result<MODE>(a, qi, q, pol);
-        if constexpr (STATS && MODE == 0) n_exact += pol.n_exact;
+        if constexpr (STATS && MODE == 0 && MSH_CAND) n_exact += pol.n_exact;
     }
     if (STATS) {
         atomicAdd(&a.stats[6], (unsigned long long)n_exact);

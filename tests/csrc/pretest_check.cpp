@@ -1,5 +1,5 @@
 // Host-side property check of the conservative fp32 culling bounds in mesh_amd/csrc/common.h
-// (tri_d2_bounds, box_d2_lo): on random and adversarial triangles the fp32 lower bound must never
+// (tri_d2_lo, tri_d2_bounds): on random and adversarial triangles the fp32 lower bound must never
 // exceed, and the upper bound never undercut, the exact squared distance (closest_on_triangle in
 // common.h is device-only, so the exact value here is re-derived in long double).  Built with hipcc
 // as host code; prints "violations=<n> checked=<m> rejected=<r> upper=<u>".
@@ -81,6 +81,7 @@ int main(int argc, char** argv) {
             for (int k = 0; k < 3; ++k) f[3 * c + k] = (float)(t[3 * c + k] - q[k]);
         float lo, hi;
         msh::tri_d2_bounds(f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7], f[8], lo, hi);
+        const float lo1 = msh::tri_d2_lo(f[0], f[1], f[2], f[3], f[4], f[5], f[6], f[7], f[8]);
         long double P[3] = {q[0], q[1], q[2]}, A[3] = {t[0], t[1], t[2]}, B[3] = {t[3], t[4], t[5]}, C[3] = {t[6], t[7], t[8]};
         const long double ex = tri_d2(P, A, B, C);
         if (lo > 0) ++rej;
@@ -93,6 +94,10 @@ int main(int argc, char** argv) {
             ++viol;
         }
         if (hi < INFINITY) ++pruned;
+        if ((long double)lo1 > ex * (1 + 1e-12L) + 1e-300L) {  // the exact policies' pretest
+            if (viol < 5) fprintf(stderr, "violation kind=%d tri_d2_lo=%.9g exact=%.17Lg\n", kind, lo1, ex);
+            ++viol;
+        }
     }
     printf("violations=%ld checked=%ld rejected=%ld upper=%ld\n", viol, n, rej, pruned);
     return viol != 0;
