@@ -139,3 +139,13 @@ def test_batch_build_validation():
     assert L.msh_batch_build(_native.dptr(v), 2, 3, _native.uptr(f2), 2, ctypes.byref(out)) == _native.MSH_EINVAL
     assert b"references vertex 9" in L.msh_last_error()
     assert L.msh_batch_nearest(None, None, 0, None, None, None) == _native.MSH_EINVAL
+
+
+def test_batch_python_validation():
+    # shape checks of search.AabbTreeBatch happen before any device work
+    from mesh_amd.search import AabbTreeBatch
+    f = np.array([[0, 1, 2], [0, 2, 3]], np.uint32)
+    with pytest.raises(ValueError, match="BxPx3"):
+        AabbTreeBatch(np.zeros((4, 3)), f)
+    with pytest.raises(ValueError, match="Tx3"):
+        AabbTreeBatch(np.zeros((2, 4, 3)), np.zeros((2, 4), np.uint32))
