@@ -39,41 +39,74 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--queries", type=int, default=100_000_000, help="queries per GPU per step")
     ap.add_argument("--freq", type=int, default=224, help="icosphere frequency (224 -> 1,003,520 faces)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline time budget")
+    ap.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU baseline time budget (both modes)")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
 
+def host_threads():
+    """Host threads this process may use (the GPU box exports OMP_NUM_THREADS = its CPU share)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
 def cpu_baseline(v, f, budget_s):
-    """Oracle CGAL-tree restatement, 1 thread, on the first queries of the rank-0 stream."""
+    """Oracle CGAL-tree restatement on the C3 query stream (seed 3, rank 0), timed as BASELINE.md §2
+    prescribes: 3 warm-up chunks, then the median rate of 10 timed chunks, in two modes:
+      * 1 thread (the reference's aabbtree_nearest loop is serial: its omp pragma is compiled out,
+        spatialsearchmodule.cpp:212-214) -> the reported `cpu_baseline`;
+      * all host threads this process may use (OpenMP over queries) -> `cpu_baseline_allcores`.
+    The chunk size is chosen so the 13 chunks of a mode take about budget_s / 2 seconds."""
     from oracle import oracle as O
     t0 = time.perf_counter()
     tree = O.CgalTree(v, f, hint=True)
     build_s = time.perf_counter() - t0
     rng = np.random.default_rng(3)
-    done, spent, chunk = 0, 0.0, 2000
-    while spent < budget_s and done < 2_000_000:
-        q = rng.uniform(-1.1, 1.1, (chunk, 3))
+    pool = rng.uniform(-1.1, 1.1, (4_000_000, 3))
+    out = {}
+    for mode, threads in (("1", 1), ("all", host_threads())):
+        # calibrate: how many queries per second at this thread count
+        n = 2000 * threads
         t0 = time.perf_counter()
-        tree.nearest(q, threads=1)
-        spent += time.perf_counter() - t0
-        done += chunk
-        chunk = min(chunk * 2, 50000)
-    return {"value": done / spent, "unit": "queries/s", "cores": 1, "kind": "port",
-            "sample": "%d uniform queries of the C3 stream (seed 3) on the 1,003,520-face icosphere; CGAL-faithful "
-                      "restatement (median-split AABB tree + KD hint, fp64, g++ -O3 -ffp-contract=off), 1 thread "
-                      "(the reference's aabbtree_nearest loop is serial, spatialsearchmodule.cpp:212-217); "
-                      "tree build %.2f s excluded" % (done, build_s)}
+        tree.nearest(pool[:n], threads=threads)
+        rate0 = n / max(time.perf_counter() - t0, 1e-6)
+        chunk = int(min(max(rate0 * budget_s / 2 / 13, 500), pool.shape[0] // 13))
+        rates, off = [], 0
+        for k in range(13):
+            q = pool[off:off + chunk]
+            off += chunk
+            t0 = time.perf_counter()
+            tree.nearest(q, threads=threads)
+            dt = time.perf_counter() - t0
+            if k >= 3:
+                rates.append(chunk / dt)
+        out[mode] = (float(np.median(rates)), chunk, threads)
+    def obj(mode, label):
+        rate, chunk, threads = out[mode]
+        return {"value": rate, "unit": "queries/s", "cores": threads, "kind": "port",
+                "sample": "median of 10 timed chunks of %d uniform C3 queries (seed 3; 3 warm-up chunks) on the "
+                          "1,003,520-face icosphere; CGAL-faithful restatement (median-split AABB tree + KD hint, "
+                          "fp64, g++ -O3 -ffp-contract=off), %s; tree build %.2f s excluded"
+                          % (chunk, label, build_s)}
+    return (obj("1", "1 thread (the reference's aabbtree_nearest loop is serial, spatialsearchmodule.cpp:212-217)"),
+            obj("all", "OpenMP over queries on %d host threads" % out["all"][2]))
 
 
 def load_traffic(workload, S):
+    """profiles/pmc_traffic.json (scripts/pmc_summary.py): PMC HBM bytes per launch of the traversal
+    kernels for this workload, or None when no profile of this workload exists."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as fh:
             d = json.load(fh)
         if d.get("workload") == workload and int(d.get("queries")) == S:
-            return d.get("bytes_per_launch")
-    except Exception:
+            return d
+    except (OSError, ValueError, TypeError):
         pass
     return None
 
@@ -86,15 +119,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, world), file=sys.stderr)
+    if world != args.gpus:
+        sys.exit("bench.py: --gpus %d but WORLD_SIZE %d (launch N>1 with torch.distributed.run --nproc-per-node N)"
+                 % (args.gpus, world))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
     from mesh_amd import _native, spatialsearch
-    from mesh_amd.distributed import nearest_device, replicate_tree
+    from mesh_amd.distributed import gather_results, nearest_device, replicate_tree
     import workloads as W
 
     _native.set_device(local)
@@ -148,12 +182,33 @@ def main():
     elapsed = time.perf_counter() - t0
     _native.timing_enable(False)
     k_ms, k_n = _native.timing_get("nearest")
+    p1_ms, p1_n = _native.timing_get("knn_pass1")
+    p2_ms, p2_n = _native.timing_get("knn_pass2")
     s_ms, s_n = _native.timing_get("sort")
     m_ms, m_n = _native.timing_get("morton")
+    g_ms, g_n = _native.timing_get("gather")
+    u_ms, u_n = _native.timing_get("unpermute")
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    # ---- N > 1: the same steps followed by the result all-gather of SURVEY §8(d)'s primary metric ----
+    elapsed_ag = None
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+            gather_results(face, S * world)
+            gather_results(part, S * world)
+            gather_results(pt, S * world)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed_ag = float(t.item())
 
     # ---- instrumented traversal (untimed): algorithmic bytes ----
     nodes, leaves = _native.ctypes.c_uint64(0), _native.ctypes.c_uint64(0)
@@ -161,7 +216,12 @@ def main():
                                                         _native.ctypes.byref(leaves)))
     n_node = nodes.value / S
     n_leaf = leaves.value / S
-    bytes_per_query = 56 + 64 * n_node + 80 * n_leaf
+    info = tree.info()
+    node_b, leaf_b = int(info.node_bytes), int(info.leaf_bytes)
+    # bytes the traversal requests per query with this layout (node_b-B nodes, leaf_b-B leaves), and the
+    # same counts priced with SURVEY §8(d)'s 64-B node model
+    bytes_per_query = 56 + node_b * n_node + leaf_b * n_leaf
+    bytes_per_query_s8d = 56 + 64 * n_node + 80 * n_leaf
 
     if rank != 0:
         if world > 1:
@@ -170,7 +230,9 @@ def main():
         return
     avg_kernel_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = S * bytes_per_query / avg_kernel_s / 1e9
-    traffic = load_traffic(workload, S)
+    achieved_s8d = S * bytes_per_query_s8d / avg_kernel_s / 1e9
+    tr = load_traffic(workload, S)
+    traffic = tr.get("bytes_per_launch") if tr else None
     total_q = S * world * args.steps
     out = {
         "metric": METRIC,
@@ -189,15 +251,26 @@ def main():
                    "parallelism": "dp%d (queries sharded per GPU, BVH replicated by RCCL broadcast)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_knn<0,false> (traversal + fp64 refinement)", "kernel_ms": avg_kernel_s * 1e3,
-                     "bytes_per_query": bytes_per_query, "nodes_per_query": n_node, "leaves_per_query": n_leaf},
-        "breakdown_ms_per_step": {"traversal": k_ms / max(k_n, 1), "sort": s_ms / max(s_n, 1),
-                                  "morton": m_ms / max(m_n, 1)},
+                     "kernel": "k_knn<0,false> + k_knn_coop<0,false> (pass 1 + pass 2: traversal + fp64 refinement)",
+                     "kernel_ms": avg_kernel_s * 1e3, "bytes_per_query": bytes_per_query,
+                     "node_bytes": node_b, "leaf_bytes": leaf_b,
+                     "nodes_per_query": n_node, "leaves_per_query": n_leaf,
+                     "s8d_64B_nodes": {"bytes_per_query": bytes_per_query_s8d, "achieved": achieved_s8d,
+                                       "frac": achieved_s8d / HBM_PEAK_GBS},
+                     "measured": ({"hbm_GBps": tr["bytes_per_launch"] / avg_kernel_s / 1e9,
+                                   "l2_hit_rate": tr.get("l2_hit_rate"), "code": tr.get("code")} if tr else None)},
+        "breakdown_ms_per_step": {"traversal": k_ms / max(k_n, 1), "pass1": p1_ms / max(p1_n, 1),
+                                  "pass2": p2_ms / max(p2_n, 1), "sort": s_ms / max(s_n, 1),
+                                  "morton": m_ms / max(m_n, 1), "gather": g_ms / max(g_n, 1),
+                                  "unpermute": u_ms / max(u_n, 1)},
         "build_ms": build_ms,
         "bvh_broadcast_ms": bcast_ms,
     }
+    if elapsed_ag is not None:
+        out["value_with_allgather"] = total_q / elapsed_ag
+        out["ms_per_step_with_allgather"] = elapsed_ag / args.steps * 1e3
     if world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_baseline(v, f, args.cpu_seconds)
+        out["cpu_baseline"], out["cpu_baseline_allcores"] = cpu_baseline(v, f, args.cpu_seconds)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -19,7 +19,10 @@
  *    (passed as void*, NULL = the handle's own stream) and are asynchronous on that stream.
  *  - A handle owns device copies of the mesh and its BVH (the reference's TreeAndTri owns host
  *    copies, nearest_triangle.hpp:28-32); input arrays are not retained.  Calls on one handle must be
- *    serialised by the caller; different handles are independent.
+ *    serialised by the caller (host threads); on the device, launches that share a handle's scratch
+ *    are ordered with an event, whatever streams they are issued on.  Different handles are
+ *    independent.
+ *  - Query counts per call are limited to 2^32 - 1 (device slot indices are 32-bit).
  *  - There is no CPU fallback: without a usable gfx950 device every compute entry point fails with
  *    MSH_EDEVICE.
  */
@@ -54,7 +57,19 @@ typedef struct msh_tree_info {
     float scene_lo[3], scene_hi[3];
     double build_ms;     /* GPU time of the LBVH build (Morton + radix sort + emission + refit) */
     uint64_t n_meshes;   /* meshes in a batched tree (msh_batch_build), 1 otherwise */
+    uint32_t node_bytes; /* bytes of one internal node as stored in HBM (one traversal step reads it) */
+    uint32_t leaf_bytes; /* bytes of one leaf record (triangle: 9 x f64 + face id; point: 3 x f64 + id) */
+    int32_t max_depth;   /* deepest leaf below the root */
 } msh_tree_info;
+
+/* Layout of a packed tree blob (msh_tree_blob_*), readable on the host without a device. */
+typedef struct msh_blob_info {
+    int32_t kind, max_depth;
+    uint64_t n_points, n_faces, n_main_faces;
+    uint64_t off_vertices, off_nodes, off_leaves, total;
+    uint32_t node_bytes, leaf_bytes;
+    double origin[3];
+} msh_blob_info;
 
 /* ---- library / device ---- */
 const char* msh_last_error(void);
@@ -82,15 +97,25 @@ int msh_tree_get_info(const msh_tree* tree, msh_tree_info* info);
 int msh_tree_nearest(msh_tree* tree, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt);
 int msh_tree_nearest_device(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part,
                             double* d_pt, void* stream);
-/* Instrumented traversal (not timed): total internal nodes popped and leaf triangles tested over the
- * S queries, for the algorithmic-bytes figure of the roofline. */
+/* Instrumented traversal (not timed, same two-pass traversal as msh_tree_nearest_device): total internal
+ * nodes popped and leaf triangles tested over the S queries, for the algorithmic-bytes figure of the
+ * roofline. */
 int msh_tree_nearest_stats(msh_tree* tree, const double* d_q, size_t S, uint64_t* nodes, uint64_t* leaves);
+/* nearest + barycentric weights of the closest point in its face (Heidrich's projection, the reference's
+ * Mesh.barycentric_coordinates_for_points, mesh.py:218-222 / barycentric_coordinates_of_projection.py:9-49,
+ * as called by landmarks.py:61-62): face (S,) u32, point (S,3) f64, w (S,3) f64 for vertices f[face]. */
+int msh_tree_nearest_bary(msh_tree* tree, const double* q, size_t S, uint32_t* face, double* pt, double* w);
+int msh_tree_nearest_bary_device(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_face, double* d_pt,
+                                 double* d_w, void* stream);
 
 /* aabbtree_nearest_alongnormal(tree, p, n) -> (dist (S,) f64, face (S,) u32, point (S,3) f64):
- * spatialsearchmodule.cpp:222-323.  Nearest hit of the rays (p, n) and (p, -n).  No hit:
- * dist = 1e100 (as the reference), face = MSH_NO_FACE, point = NaN (reference: uninitialised). */
+ * spatialsearchmodule.cpp:222-323.  Nearest hit of the rays (p, n) and (p, -n); hit point = CGAL's
+ * Plane_3 / Line_3 construction.  No hit: dist = 1e100 (as the reference), face = MSH_NO_FACE,
+ * point = NaN (reference: uninitialised). */
 int msh_tree_nearest_alongnormal(msh_tree* tree, const double* p, const double* n, size_t S, double* dist,
                                  uint32_t* face, double* pt);
+int msh_tree_nearest_alongnormal_device(msh_tree* tree, const double* d_p, const double* d_n, size_t S,
+                                        double* d_dist, uint32_t* d_face, double* d_pt, void* stream);
 
 /* aabbtree_intersections_indices(tree, qv, qf) -> ascending query-face indices (K,) u32 whose
  * triangle intersects any mesh triangle: spatialsearchmodule.cpp:326-417 (unregistered there,
@@ -116,6 +141,19 @@ int msh_ntree_selfintersects(msh_tree* tree, int64_t* count);
  * freed (fixes the double free at py_visibility.cpp:212). */
 int msh_visibility(msh_tree* tree, const double* cams, size_t C, const double* normals, const double* sensors,
                    double min_dist, uint32_t* vis, double* ndc);
+/* Device-resident shard of visibility_compute: vertices [v_begin, v_begin + v_count) of the main mesh
+ * (the multi-GPU split of the (C x P) ray grid by vertex range, visibility.cpp:136-173).  d_normals is
+ * indexed by global vertex (P,3); d_vis / d_ndc are (C, v_count). */
+int msh_visibility_device(msh_tree* tree, const double* d_cams, size_t C, const double* d_normals,
+                          const double* d_sensors, double min_dist, size_t v_begin, size_t v_count, uint32_t* d_vis,
+                          double* d_ndc, void* stream);
+
+/* ---- mesh geometry feeding the path ---- */
+/* Mesh.estimate_vertex_normals (mesh.py:208-216): per vertex, the sum in ascending face order of the
+ * faces' cross products (v1 - v0) x (v2 - v0) (tri_normals.py:23-24), divided by its norm (0 -> 1). */
+int msh_vertex_normals(const double* v, size_t P, const uint32_t* f, size_t T, double* vn);
+/* device pointers; returns when the result is in d_vn (stream may be NULL) */
+int msh_vertex_normals_device(const double* d_v, size_t P, const uint32_t* d_f, size_t T, double* d_vn, void* stream);
 
 /* ---- batched trees: scan-to-mesh registration over many meshes (BASELINE configs[3], C4) ----
  * The reference answers this with one AabbTree per mesh (search.py:21-30, one aabbtree_compute +
@@ -129,6 +167,11 @@ int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size
 int msh_batch_nearest(msh_tree* tree, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt);
 int msh_batch_nearest_device(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part,
                              double* d_pt, void* stream);
+/* registration-ready variant: face (B,S), point (B,S,3), barycentric weights (B,S,3) (see
+ * msh_tree_nearest_bary) */
+int msh_batch_nearest_bary(msh_tree* tree, const double* q, size_t S, uint32_t* face, double* pt, double* w);
+int msh_batch_nearest_bary_device(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_face, double* d_pt,
+                                  double* d_w, void* stream);
 
 /* ---- ClosestPointTree (search.py:52-65, scipy.spatial.KDTree) ---- */
 int msh_points_build(const double* v, size_t P, msh_tree** out);
@@ -143,6 +186,11 @@ int msh_tree_blob_pack(const msh_tree* tree, void* d_dst, void* stream);
 /* Create a handle on `device` from a packed blob already resident in that device's HBM
  * (e.g. after an RCCL broadcast).  The blob is copied; the caller keeps ownership of d_src. */
 int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stream, msh_tree** out);
+/* Host-side blob header (no device): write the header of a blob for the given sizes into dst (cap
+ * bytes), or parse + validate a header copied to host memory (magic, layout, version, length). */
+int msh_blob_header_write(int kind, uint64_t P, uint64_t T, uint64_t T_main, void* dst, size_t cap,
+                          msh_blob_info* info);
+int msh_blob_header_parse(const void* src, size_t bytes, msh_blob_info* info);
 
 /* ---- kernel timing (HIP events on the launch stream; used by bench.py's roofline) ---- */
 int msh_timing_enable(int on);

@@ -39,12 +39,18 @@ SIGNATURES = [
     ("msh_tree_nearest", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_u32_p, _c_double_p]),
     ("msh_tree_nearest_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     ("msh_tree_nearest_stats", _i, [_vp, _vp, _sz, _c_u64_p, _c_u64_p]),
+    ("msh_tree_nearest_bary", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_double_p, _c_double_p]),
+    ("msh_tree_nearest_bary_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     ("msh_tree_nearest_alongnormal", _i, [_vp, _c_double_p, _c_double_p, _sz, _c_double_p, _c_u32_p, _c_double_p]),
+    ("msh_tree_nearest_alongnormal_device", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     ("msh_tree_intersections", _i, [_vp, _c_double_p, _sz, _c_u32_p, _sz, _c_u32_p, ctypes.POINTER(_sz)]),
     ("msh_ntree_build", _i, [_c_double_p, _sz, _c_u32_p, _sz, ctypes.c_double, ctypes.POINTER(_vp)]),
     ("msh_ntree_nearest", _i, [_vp, _c_double_p, _c_double_p, _sz, _c_u32_p, _c_double_p]),
     ("msh_ntree_selfintersects", _i, [_vp, _c_i64_p]),
     ("msh_visibility", _i, [_vp, _c_double_p, _sz, _c_double_p, _c_double_p, ctypes.c_double, _c_u32_p, _c_double_p]),
+    ("msh_visibility_device", _i, [_vp, _vp, _sz, _vp, _vp, ctypes.c_double, _sz, _sz, _vp, _vp, _vp]),
+    ("msh_vertex_normals", _i, [_c_double_p, _sz, _c_u32_p, _sz, _c_double_p]),
+    ("msh_vertex_normals_device", _i, [_vp, _sz, _vp, _sz, _vp, _vp]),
     ("msh_points_build", _i, [_c_double_p, _sz, ctypes.POINTER(_vp)]),
     ("msh_points_nearest", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_double_p]),
     ("msh_tree_blob_size", _i, [_vp, ctypes.POINTER(_sz)]),
@@ -53,6 +59,10 @@ SIGNATURES = [
     ("msh_batch_build", _i, [_c_double_p, _sz, _sz, _c_u32_p, _sz, ctypes.POINTER(_vp)]),
     ("msh_batch_nearest", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_u32_p, _c_double_p]),
     ("msh_batch_nearest_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    ("msh_batch_nearest_bary", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_double_p, _c_double_p]),
+    ("msh_batch_nearest_bary_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    ("msh_blob_header_write", _i, [_i, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp, _sz, _vp]),
+    ("msh_blob_header_parse", _i, [_vp, _sz, _vp]),
     ("msh_timing_enable", _i, [_i]),
     ("msh_timing_get", _i, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _c_i64_p]),
     ("msh_timing_reset", _i, []),
@@ -63,7 +73,16 @@ class TreeInfo(ctypes.Structure):
     _fields_ = [("device", _i), ("kind", _i), ("n_points", ctypes.c_uint64), ("n_faces", ctypes.c_uint64),
                 ("n_main_faces", ctypes.c_uint64), ("n_nodes", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
                 ("eps", ctypes.c_double), ("scene_lo", ctypes.c_float * 3), ("scene_hi", ctypes.c_float * 3),
-                ("build_ms", ctypes.c_double), ("n_meshes", ctypes.c_uint64)]
+                ("build_ms", ctypes.c_double), ("n_meshes", ctypes.c_uint64), ("node_bytes", ctypes.c_uint32),
+                ("leaf_bytes", ctypes.c_uint32), ("max_depth", ctypes.c_int32)]
+
+
+class BlobInfo(ctypes.Structure):
+    """msh_blob_info (include/meshsearch.h): layout of a packed tree blob."""
+    _fields_ = [("kind", ctypes.c_int32), ("max_depth", ctypes.c_int32), ("n_points", ctypes.c_uint64),
+                ("n_faces", ctypes.c_uint64), ("n_main_faces", ctypes.c_uint64), ("off_vertices", ctypes.c_uint64),
+                ("off_nodes", ctypes.c_uint64), ("off_leaves", ctypes.c_uint64), ("total", ctypes.c_uint64),
+                ("node_bytes", ctypes.c_uint32), ("leaf_bytes", ctypes.c_uint32), ("origin", ctypes.c_double * 3)]
 
 
 def _preload_single_hip_runtime():

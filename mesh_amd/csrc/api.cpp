@@ -10,10 +10,12 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "internal.h"
@@ -53,8 +55,8 @@ void DevBuf::release() {
 }
 
 void Workspace::release() {
-    DevBuf* all[] = {&keys, &vals, &keys_alt, &vals_alt, &hist, &scan, &q, &out_a, &out_b, &out_c,
-                     &flags, &counters, &spill, &stats, &ranges};
+    DevBuf* all[] = {&keys, &vals, &keys_alt, &vals_alt, &hist, &scan, &q, &n, &out_a, &out_b, &out_c, &out_d,
+                     &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w};
     for (DevBuf* b : all) b->release();
 }
 
@@ -130,6 +132,15 @@ static int check_faces(const uint32_t* f, size_t T, size_t P, const char* what) 
     return MSH_OK;
 }
 
+// queries, rays and permutation slots are 32-bit indices on the device
+static int check_count(size_t S, const char* fn) {
+    if (S > (size_t)0xFFFFFFFFull) {
+        set_error("%s: %zu queries exceed the 32-bit index range of one call (split the batch)", fn, S);
+        return MSH_EINVAL;
+    }
+    return MSH_OK;
+}
+
 template <class T>
 static int upload(DevBuf& buf, const T* host, size_t n, hipStream_t s) {
     MSH_TRY(buf.reserve(n * sizeof(T)));
@@ -141,12 +152,24 @@ static void free_tree(msh_tree* t) {
     if (!t) return;
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);
+    if (t->ws_done) (void)hipEventSynchronize(t->ws_done);
     t->ws.release();
     if (t->d_v) (void)hipFree(t->d_v);
     if (t->d_nodes) (void)hipFree(t->d_nodes);
     if (t->d_orgs) (void)hipFree(t->d_orgs);
     if (t->d_boxes) (void)hipFree(t->d_boxes);
     if (t->d_leaves) (void)hipFree(t->d_leaves);
+    if (t->d_vorder) (void)hipFree(t->d_vorder);
+    for (int b = 0; b < 2; ++b) {
+        if (t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
+        if (t->d_stage[b]) (void)hipFree(t->d_stage[b]);
+        if (t->e_up[b]) (void)hipEventDestroy(t->e_up[b]);
+        if (t->e_run[b]) (void)hipEventDestroy(t->e_run[b]);
+        if (t->e_down[b]) (void)hipEventDestroy(t->e_down[b]);
+    }
+    if (t->s_up) (void)hipStreamDestroy(t->s_up);
+    if (t->s_down) (void)hipStreamDestroy(t->s_down);
+    if (t->ws_done) (void)hipEventDestroy(t->ws_done);
     if (t->stream) (void)hipStreamDestroy(t->stream);
     delete t;
 }
@@ -159,14 +182,29 @@ static int new_tree(int kind, msh_tree** out) {
     t->device = dev;
     t->kind = kind;
     hipError_t e = hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ws_done, hipEventDisableTiming);
     if (e != hipSuccess) {
-        set_error("hipStreamCreate failed on device %d: %s", dev, hipGetErrorString(e));
-        delete t;
+        set_error("hipStreamCreate / hipEventCreate failed on device %d: %s", dev, hipGetErrorString(e));
+        free_tree(t);
         return MSH_EDEVICE;
     }
     *out = t;
     return MSH_OK;
 }
+
+// Stream ordering of the handle's workspace: every launch sequence that uses `ws` first waits for the
+// previous one (whatever stream it ran on) and then marks its own end, so a *_device call on a
+// caller's stream followed by any other call on the same handle cannot overwrite scratch still in use.
+struct WsOrder {
+    msh_tree* t;
+    hipStream_t s;
+    WsOrder(msh_tree* tree, hipStream_t st) : t(tree), s(st) {
+        if (t->ws_done) (void)hipStreamWaitEvent(s, t->ws_done, 0);
+    }
+    ~WsOrder() {
+        if (t->ws_done) (void)hipEventRecord(t->ws_done, s);
+    }
+};
 
 // Triangle tree over v (P rows) and f (T rows, indices into v).
 static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint32_t* f, size_t T) {
@@ -213,19 +251,54 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
 
 static const size_t kSortMin = 4096;  // below this the query Morton sort costs more than it saves
 
-// Morton-sort S points (device) into ws.vals; returns the permutation (or nullptr for small S).
-static int sort_queries(msh_tree* t, const double* d_q, size_t S, hipStream_t s, const uint32_t** perm) {
-    *perm = nullptr;
+// Query order for S point rows (device): below kSortMin the caller's arrays are used as they are;
+// otherwise Morton codes + radix sort give the permutation (ws.vals), and the rows (and normals, when
+// given) are gathered once into slot order (ws.qs / ws.ns) with the inverse permutation (ws.inv).
+static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_t S, hipStream_t s,
+                        QueryOrder* ord) {
+    *ord = QueryOrder{d_q, d_n, nullptr, nullptr};
     if (S < kSortMin) return MSH_OK;
     Workspace& ws = t->ws;
     MSH_TRY(ws.keys.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.vals.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.keys_alt.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.vals_alt.reserve(S * sizeof(uint32_t)));
+    MSH_TRY(ws.qs.reserve(3 * S * sizeof(double)));
+    MSH_TRY(ws.inv.reserve(S * sizeof(uint32_t)));
+    if (d_n) MSH_TRY(ws.ns.reserve(3 * S * sizeof(double)));
     MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
     MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
                              ws.vals_alt.as<uint32_t>(), S, 30, ws, s));
-    *perm = ws.vals.as<uint32_t>();
+    MSH_TRY(gather_rows(d_q, d_n, ws.vals.as<uint32_t>(), S, ws.qs.as<double>(), d_n ? ws.ns.as<double>() : nullptr,
+                        ws.inv.as<uint32_t>(), s));
+    *ord = QueryOrder{ws.qs.as<double>(), d_n ? ws.ns.as<double>() : nullptr, ws.vals.as<uint32_t>(),
+                      ws.inv.as<uint32_t>()};
+    return MSH_OK;
+}
+
+// Batched trees: Morton order inside each mesh, meshes in order (two stable passes), then the gather.
+static int sort_batch_queries(msh_tree* t, const double* d_q, size_t n, size_t S, hipStream_t s, QueryOrder* ord) {
+    *ord = QueryOrder{d_q, nullptr, nullptr, nullptr};
+    if (n < kSortMin) return MSH_OK;
+    Workspace& ws = t->ws;
+    MSH_TRY(ws.keys.reserve(n * sizeof(uint32_t)));
+    MSH_TRY(ws.vals.reserve(n * sizeof(uint32_t)));
+    MSH_TRY(ws.keys_alt.reserve(n * sizeof(uint32_t)));
+    MSH_TRY(ws.vals_alt.reserve(n * sizeof(uint32_t)));
+    MSH_TRY(ws.qs.reserve(3 * n * sizeof(double)));
+    MSH_TRY(ws.inv.reserve(n * sizeof(uint32_t)));
+    uint32_t* keys = ws.keys.as<uint32_t>();
+    uint32_t* vals = ws.vals.as<uint32_t>();
+    MSH_TRY(query_morton_batch(t, d_q, n, S, keys, vals, s));
+    MSH_TRY(radix_sort_pairs(keys, vals, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n, 30, ws, s));
+    if (t->B > 1) {
+        MSH_TRY(mesh_keys(vals, n, S, keys, s));
+        int bits = 0;
+        while (bits < 32 && ((size_t)1 << bits) < t->B) ++bits;
+        MSH_TRY(radix_sort_pairs(keys, vals, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n, bits, ws, s));
+    }
+    MSH_TRY(gather_rows(d_q, nullptr, vals, n, ws.qs.as<double>(), nullptr, ws.inv.as<uint32_t>(), s));
+    *ord = QueryOrder{ws.qs.as<double>(), nullptr, vals, ws.inv.as<uint32_t>()};
     return MSH_OK;
 }
 
@@ -238,7 +311,8 @@ static int check_tree(const msh_tree* t, int want_kind, const char* fn) {
         set_error("%s: wrong handle kind %d", fn, t->kind);
         return MSH_EINVAL;
     }
-    if (t->B != 1) {
+    // any batched handle (also B == 1: its bounds are relative to the per-mesh origins)
+    if (t->B != 1 || t->d_boxes) {
         set_error("%s: batched tree handle (use the msh_batch_* entry points)", fn);
         return MSH_EINVAL;
     }
@@ -257,6 +331,194 @@ static int check_batch(const msh_tree* t, const char* fn) {
     return use_device(t->device);
 }
 
+static hipStream_t pick(msh_tree* t, void* stream) { return stream ? static_cast<hipStream_t>(stream) : t->stream; }
+
+// ---- host staging: pinned double-buffered chunks, copies overlapped with the kernels ----
+static int host_threads() {
+    const char* e = getenv("MESH_AMD_COPY_THREADS");
+    int n = e ? atoi(e) : 0;
+    if (n <= 0) {
+        const char* o = getenv("OMP_NUM_THREADS");
+        n = o ? atoi(o) : 8;
+    }
+    return std::max(1, std::min(n, 32));
+}
+
+static void par_copy(void* dst, const void* src, size_t bytes) {
+    const int nt = bytes < ((size_t)8 << 20) ? 1 : host_threads();
+    if (nt <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (bytes + nt - 1) / nt;
+    for (int k = 0; k < nt; ++k) {
+        const size_t o = (size_t)k * per;
+        if (o >= bytes) break;
+        const size_t n = std::min(per, bytes - o);
+        th.emplace_back([=] { std::memcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o, n); });
+    }
+    for (auto& x : th) x.join();
+}
+
+// One pipelined host call: rows [0, S) in chunks; inputs (ni arrays of in_w doubles per row) are staged
+// through pinned buffers and uploaded on a copy stream, `run(chunk, n, dev_in, dev_out)` enqueues the
+// kernels on the handle's stream, and outputs (no arrays of out_b bytes per row) come back on a second
+// copy stream while the next chunk computes.
+struct HostArr {
+    const void* in;   // input (caller memory) or nullptr
+    void* out;        // output (caller memory) or nullptr
+    size_t row_bytes;
+};
+
+static void release_stage(msh_tree* t) {
+    for (int b = 0; b < 2; ++b) {
+        if (t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
+        if (t->d_stage[b]) (void)hipFree(t->d_stage[b]);
+        t->h_stage[b] = t->d_stage[b] = nullptr;
+    }
+    t->stage_bytes = 0;
+}
+
+static int stage_setup(msh_tree* t, size_t bytes) {
+    if (!t->s_up) MSH_HIP(hipStreamCreateWithFlags(&t->s_up, hipStreamNonBlocking));
+    if (!t->s_down) MSH_HIP(hipStreamCreateWithFlags(&t->s_down, hipStreamNonBlocking));
+    for (int b = 0; b < 2; ++b) {
+        if (!t->e_up[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_up[b], hipEventDisableTiming));
+        if (!t->e_run[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_run[b], hipEventDisableTiming));
+        if (!t->e_down[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_down[b], hipEventDisableTiming));
+    }
+    if (t->stage_bytes >= bytes) return MSH_OK;
+    release_stage(t);
+    for (int b = 0; b < 2; ++b) {
+        MSH_HIP(hipHostMalloc(&t->h_stage[b], bytes, hipHostMallocDefault));
+        MSH_HIP(hipMalloc(&t->d_stage[b], bytes));
+    }
+    t->stage_bytes = bytes;
+    return MSH_OK;
+}
+
+template <class Run>
+static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, size_t chunk, Run run) {
+    size_t row = 0;
+    for (const HostArr& a : arrs) row += a.row_bytes;
+    hipStream_t sc = t->stream;
+    int st = MSH_OK;
+    if (S * row <= ((size_t)16 << 20)) {  // small call: one pageable round trip through device scratch
+        DevBuf tmp;
+        MSH_TRY(tmp.reserve(S * row));
+        std::vector<char*> slabs;
+        size_t off = 0;
+        hipError_t e = hipSuccess;
+        for (const HostArr& a : arrs) {
+            char* d = static_cast<char*>(tmp.ptr) + off * S;
+            slabs.push_back(d);
+            if (a.in && e == hipSuccess) e = hipMemcpyAsync(d, a.in, S * a.row_bytes, hipMemcpyHostToDevice, sc);
+            off += a.row_bytes;
+        }
+        if (e == hipSuccess) st = run(0, S, slabs);
+        off = 0;
+        for (const HostArr& a : arrs) {
+            if (a.out && e == hipSuccess && st == MSH_OK)
+                e = hipMemcpyAsync(a.out, static_cast<char*>(tmp.ptr) + off * S, S * a.row_bytes, hipMemcpyDeviceToHost, sc);
+            off += a.row_bytes;
+        }
+        const hipError_t e2 = hipStreamSynchronize(sc);
+        if (e == hipSuccess) e = e2;
+        tmp.release();
+        if (st == MSH_OK && e != hipSuccess) {
+            set_error("host call: %s", hipGetErrorString(e));
+            st = MSH_EDEVICE;
+        }
+        return st;
+    }
+    const size_t nch = (S + chunk - 1) / chunk;
+    MSH_TRY(stage_setup(t, chunk * row));
+    hipStream_t up = t->s_up, down = t->s_down;
+    hipEvent_t* e_up = t->e_up;
+    hipEvent_t* e_run = t->e_run;
+    hipEvent_t* e_down = t->e_down;
+    void* const* host = t->h_stage;
+    void* const* dev = t->d_stage;
+    auto fail = [&](hipError_t e, const char* what) {
+        set_error("%s: %s", what, hipGetErrorString(e));
+        st = e == hipErrorOutOfMemory ? MSH_ENOMEM : MSH_EDEVICE;
+    };
+    do {
+        hipError_t e = hipSuccess;
+        for (size_t k = 0; k <= nch && st == MSH_OK; ++k) {
+            if (k < nch) {
+                const int b = (int)(k & 1);
+                const size_t r0 = k * chunk, n = std::min(chunk, S - r0);
+                if (k >= 2 && (e = hipEventSynchronize(e_up[b])) != hipSuccess) { fail(e, "staging"); break; }
+                // inputs: pinned slab of this buffer, array by array
+                size_t off = 0;
+                for (const HostArr& a : arrs) {
+                    if (a.in)
+                        par_copy(static_cast<char*>(host[b]) + off * chunk, static_cast<const char*>(a.in) + r0 * a.row_bytes,
+                                 n * a.row_bytes);
+                    off += a.row_bytes;
+                }
+                off = 0;
+                for (const HostArr& a : arrs) {
+                    if (a.in && (e = hipMemcpyAsync(static_cast<char*>(dev[b]) + off * chunk,
+                                                    static_cast<char*>(host[b]) + off * chunk, n * a.row_bytes,
+                                                    hipMemcpyHostToDevice, up)) != hipSuccess)
+                        break;
+                    off += a.row_bytes;
+                }
+                if (e == hipSuccess) e = hipEventRecord(e_up[b], up);
+                if (e == hipSuccess) e = hipStreamWaitEvent(sc, e_up[b], 0);
+                if (e == hipSuccess && k >= 2) e = hipStreamWaitEvent(sc, e_down[b], 0);
+                if (e != hipSuccess) { fail(e, "upload"); break; }
+                std::vector<char*> slabs;
+                off = 0;
+                for (const HostArr& a : arrs) {
+                    slabs.push_back(static_cast<char*>(dev[b]) + off * chunk);
+                    off += a.row_bytes;
+                }
+                if ((st = run(r0, n, slabs)) != MSH_OK) break;
+                if ((e = hipEventRecord(e_run[b], sc)) != hipSuccess || (e = hipStreamWaitEvent(down, e_run[b], 0)) != hipSuccess) {
+                    fail(e, "launch");
+                    break;
+                }
+                off = 0;
+                for (const HostArr& a : arrs) {
+                    if (a.out && (e = hipMemcpyAsync(static_cast<char*>(host[b]) + off * chunk,
+                                                     static_cast<char*>(dev[b]) + off * chunk, n * a.row_bytes,
+                                                     hipMemcpyDeviceToHost, down)) != hipSuccess)
+                        break;
+                    off += a.row_bytes;
+                }
+                if (e == hipSuccess) e = hipEventRecord(e_down[b], down);
+                if (e != hipSuccess) { fail(e, "download"); break; }
+            }
+            if (k >= 1) {  // drain chunk k - 1
+                const int b = (int)((k - 1) & 1);
+                const size_t r0 = (k - 1) * chunk, n = std::min(chunk, S - r0);
+                if ((e = hipEventSynchronize(e_down[b])) != hipSuccess) { fail(e, "kernels / download"); break; }
+                size_t off = 0;
+                for (const HostArr& a : arrs) {
+                    if (a.out)
+                        par_copy(static_cast<char*>(a.out) + r0 * a.row_bytes, static_cast<char*>(host[b]) + off * chunk,
+                                 n * a.row_bytes);
+                    off += a.row_bytes;
+                }
+            }
+        }
+    } while (0);
+    (void)hipStreamSynchronize(up);
+    (void)hipStreamSynchronize(down);
+    (void)hipStreamSynchronize(sc);
+    return st;
+}
+
+static size_t host_chunk() {
+    const char* e = getenv("MESH_AMD_HOST_CHUNK");
+    const long long c = e ? atoll(e) : 0;
+    return c > 0 ? (size_t)c : ((size_t)4 << 20);  // 4M rows per chunk
+}
+
 }  // namespace msh
 
 using namespace msh;
@@ -265,7 +527,7 @@ extern "C" {
 
 const char* msh_last_error(void) { return g_err.c_str(); }
 
-int msh_version(void) { return 1; }
+int msh_version(void) { return 2; }
 
 int msh_device_count(int* n) {
     int c = 0;
@@ -396,8 +658,6 @@ int msh_tree_get_info(const msh_tree* t, msh_tree_info* info) {
     info->n_nodes = t->T > 0 ? t->B * (t->T - 1) : 0;
     info->n_meshes = t->B;
     const size_t leaf = t->kind == kPoints ? sizeof(PtRec) : sizeof(TriRec);
-    const size_t vrows = t->kind == kPoints ? t->P : t->P;  // main vertices (extra mesh rows follow)
-    (void)vrows;
     info->bytes = info->n_nodes * sizeof(BNode) + t->B * t->T * leaf;
     info->eps = t->eps;
     for (int k = 0; k < 3; ++k) {
@@ -405,6 +665,9 @@ int msh_tree_get_info(const msh_tree* t, msh_tree_info* info) {
         info->scene_hi[k] = t->scene_hi[k];
     }
     info->build_ms = t->build_ms;
+    info->node_bytes = (uint32_t)sizeof(BNode);
+    info->leaf_bytes = (uint32_t)leaf;
+    info->max_depth = t->max_depth;
     return MSH_OK;
 }
 
@@ -412,85 +675,106 @@ int msh_tree_get_info(const msh_tree* t, msh_tree_info* info) {
 int msh_tree_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part, double* d_pt,
                             void* stream) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_device"));
+    MSH_TRY(check_count(S, "msh_tree_nearest_device"));
     if (S == 0) return MSH_OK;
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : t->stream;
-    const uint32_t* perm = nullptr;
-    MSH_TRY(sort_queries(t, d_q, S, s, &perm));
-    return launch_nearest(t, d_q, perm, S, d_face, d_part, d_pt, s);
+    hipStream_t s = pick(t, stream);
+    WsOrder order(t, s);
+    QueryOrder ord;
+    MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord));
+    return launch_nearest(t, ord, S, SlotOut{d_face, d_part, d_pt, nullptr, nullptr}, s);
+}
+
+int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, double* d_pt, double* d_w,
+                                 void* stream) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_bary_device"));
+    MSH_TRY(check_count(S, "msh_tree_nearest_bary_device"));
+    if (S == 0) return MSH_OK;
+    if (!d_w) { set_error("msh_tree_nearest_bary_device: null weights"); return MSH_EINVAL; }
+    hipStream_t s = pick(t, stream);
+    WsOrder order(t, s);
+    QueryOrder ord;
+    MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord));
+    return launch_nearest(t, ord, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_w}, s);
 }
 
 int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest"));
+    MSH_TRY(check_count(S, "msh_tree_nearest"));
     if (S == 0) return MSH_OK;
-    hipStream_t s = t->stream;
-    Workspace& ws = t->ws;
-    MSH_TRY(upload(ws.q, q, 3 * S, s));
-    MSH_TRY(ws.out_a.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.out_b.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.out_c.reserve(3 * S * sizeof(double)));
-    MSH_TRY(msh_tree_nearest_device(t, ws.q.as<double>(), S, ws.out_a.as<uint32_t>(),
-                                    part ? ws.out_b.as<uint32_t>() : nullptr, ws.out_c.as<double>(), s));
-    MSH_HIP(hipMemcpyAsync(face, ws.out_a.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    if (part) MSH_HIP(hipMemcpyAsync(part, ws.out_b.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    MSH_HIP(hipMemcpyAsync(pt, ws.out_c.ptr, 3 * S * sizeof(double), hipMemcpyDeviceToHost, s));
-    MSH_HIP(hipStreamSynchronize(s));
-    return MSH_OK;
+    if (!q || !face || !pt) { set_error("msh_tree_nearest: null argument"); return MSH_EINVAL; }
+    // rows: q (24 B in) | face (4 B out) | part (4 B out) | point (24 B out)
+    const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, part, 4}, {nullptr, pt, 24}};
+    return pipelined(t, S, arrs, std::min(S, host_chunk()), [&](size_t, size_t n, const std::vector<char*>& d) {
+        return msh_tree_nearest_device(t, reinterpret_cast<const double*>(d[0]), n, reinterpret_cast<uint32_t*>(d[1]),
+                                       part ? reinterpret_cast<uint32_t*>(d[2]) : nullptr,
+                                       reinterpret_cast<double*>(d[3]), t->stream);
+    });
+}
+
+int msh_tree_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face, double* pt, double* w) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_bary"));
+    MSH_TRY(check_count(S, "msh_tree_nearest_bary"));
+    if (S == 0) return MSH_OK;
+    if (!q || !face || !pt || !w) { set_error("msh_tree_nearest_bary: null argument"); return MSH_EINVAL; }
+    const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, pt, 24}, {nullptr, w, 24}};
+    return pipelined(t, S, arrs, std::min(S, host_chunk()), [&](size_t, size_t n, const std::vector<char*>& d) {
+        return msh_tree_nearest_bary_device(t, reinterpret_cast<const double*>(d[0]), n, reinterpret_cast<uint32_t*>(d[1]),
+                                            reinterpret_cast<double*>(d[2]), reinterpret_cast<double*>(d[3]), t->stream);
+    });
 }
 
 int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* nodes, uint64_t* leaves) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_stats"));
+    MSH_TRY(check_count(S, "msh_tree_nearest_stats"));
     *nodes = 0;
     *leaves = 0;
     if (S == 0) return MSH_OK;
     hipStream_t s = t->stream;
-    const uint32_t* perm = nullptr;
-    MSH_TRY(sort_queries(t, d_q, S, s, &perm));
-    MSH_TRY(t->ws.stats.reserve(8 * sizeof(unsigned long long)));
-    MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, 8 * sizeof(unsigned long long), s));
-    MSH_TRY(launch_nearest_stats(t, d_q, perm, S, t->ws.stats.as<unsigned long long>(), s));
     unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    MSH_HIP(hipMemcpyAsync(h, t->ws.stats.ptr, sizeof(h), hipMemcpyDeviceToHost, s));
+    {
+        WsOrder order(t, s);
+        QueryOrder ord;
+        MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord));
+        MSH_TRY(t->ws.stats.reserve(8 * sizeof(unsigned long long)));
+        MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, 8 * sizeof(unsigned long long), s));
+        MSH_TRY(launch_nearest_stats(t, ord, S, t->ws.stats.as<unsigned long long>(), s));
+        MSH_HIP(hipMemcpyAsync(h, t->ws.stats.ptr, sizeof(h), hipMemcpyDeviceToHost, s));
+    }
     MSH_HIP(hipStreamSynchronize(s));
     *nodes = h[0];
     *leaves = h[1];
     if (getenv("MESH_AMD_STATS_DUMP"))  // development: wave-iteration utilisation of pass 1
         fprintf(stderr, "[msh stats] S=%zu nodes=%llu leaves=%llu trav_it=%llu trav_lanes=%llu leaf_it=%llu "
-                        "leaf_lanes=%llu exact=%llu\n", S, h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+                        "leaf_lanes=%llu pass2_items=%llu\n", S, h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
     return MSH_OK;
+}
+
+int msh_tree_nearest_alongnormal_device(msh_tree* t, const double* d_p, const double* d_n, size_t S, double* d_dist,
+                                        uint32_t* d_face, double* d_pt, void* stream) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_alongnormal_device"));
+    MSH_TRY(check_count(S, "msh_tree_nearest_alongnormal_device"));
+    if (S == 0) return MSH_OK;
+    hipStream_t s = pick(t, stream);
+    WsOrder order(t, s);
+    QueryOrder ord;
+    MSH_TRY(sort_queries(t, d_p, d_n, S, s, &ord));
+    return launch_alongnormal(t, ord, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_dist}, s);
 }
 
 int msh_tree_nearest_alongnormal(msh_tree* t, const double* p, const double* n, size_t S, double* dist, uint32_t* face,
                                  double* pt) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_alongnormal"));
+    MSH_TRY(check_count(S, "msh_tree_nearest_alongnormal"));
     if (S == 0) return MSH_OK;
-    hipStream_t s = t->stream;
-    Workspace& ws = t->ws;
-    DevBuf dn, dd;
-    int st = MSH_OK;
-    do {
-        if ((st = upload(ws.q, p, 3 * S, s)) != MSH_OK) break;
-        if ((st = upload(dn, n, 3 * S, s)) != MSH_OK) break;
-        if ((st = dd.reserve(S * sizeof(double))) != MSH_OK) break;
-        if ((st = ws.out_a.reserve(S * sizeof(uint32_t))) != MSH_OK) break;
-        if ((st = ws.out_c.reserve(3 * S * sizeof(double))) != MSH_OK) break;
-        const uint32_t* perm = nullptr;
-        if ((st = sort_queries(t, ws.q.as<double>(), S, s, &perm)) != MSH_OK) break;
-        if ((st = launch_alongnormal(t, ws.q.as<double>(), dn.as<double>(), perm, S, dd.as<double>(),
-                                     ws.out_a.as<uint32_t>(), ws.out_c.as<double>(), s)) != MSH_OK)
-            break;
-        hipError_t e;
-        if ((e = hipMemcpyAsync(dist, dd.ptr, S * sizeof(double), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipMemcpyAsync(face, ws.out_a.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipMemcpyAsync(pt, ws.out_c.ptr, 3 * S * sizeof(double), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipStreamSynchronize(s)) != hipSuccess) {
-            set_error("alongnormal: %s", hipGetErrorString(e));
-            st = MSH_EDEVICE;
-        }
-    } while (0);
-    (void)hipStreamSynchronize(s);
-    dn.release();
-    dd.release();
-    return st;
+    if (!p || !n || !dist || !face || !pt) { set_error("msh_tree_nearest_alongnormal: null argument"); return MSH_EINVAL; }
+    const std::vector<HostArr> arrs = {{p, nullptr, 24}, {n, nullptr, 24}, {nullptr, dist, 8}, {nullptr, face, 4},
+                                       {nullptr, pt, 24}};
+    return pipelined(t, S, arrs, std::min(S, host_chunk()), [&](size_t, size_t c, const std::vector<char*>& d) {
+        return msh_tree_nearest_alongnormal_device(t, reinterpret_cast<const double*>(d[0]),
+                                                   reinterpret_cast<const double*>(d[1]), c,
+                                                   reinterpret_cast<double*>(d[2]), reinterpret_cast<uint32_t*>(d[3]),
+                                                   reinterpret_cast<double*>(d[4]), t->stream);
+    });
 }
 
 static void host_tris(const double* v, const uint32_t* f, size_t T, std::vector<TriRec>& out) {
@@ -508,6 +792,7 @@ int msh_tree_intersections(msh_tree* t, const double* qv, size_t Pq, const uint3
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_intersections"));
     *K = 0;
     if (Tq == 0) return MSH_OK;
+    MSH_TRY(check_count(Tq, "msh_tree_intersections"));
     MSH_TRY(check_faces(qf, Tq, Pq, "query faces"));
     hipStream_t s = t->stream;
     std::vector<TriRec> ht;
@@ -516,6 +801,7 @@ int msh_tree_intersections(msh_tree* t, const double* qv, size_t Pq, const uint3
     int st = MSH_OK;
     std::vector<uint32_t> flags(Tq);
     do {
+        WsOrder order(t, s);
         if ((st = upload(dq, ht.data(), Tq, s)) != MSH_OK) break;
         if ((st = df.reserve(Tq * sizeof(uint32_t))) != MSH_OK) break;
         if ((st = launch_tri_intersect(t, dq.as<TriRec>(), Tq, 0, df.as<uint32_t>(), s)) != MSH_OK) break;
@@ -539,31 +825,35 @@ int msh_tree_intersections(msh_tree* t, const double* qv, size_t Pq, const uint3
 
 int msh_ntree_nearest(msh_tree* t, const double* q, const double* n, size_t S, uint32_t* face, double* pt) {
     MSH_TRY(check_tree(t, kNormals, "msh_ntree_nearest"));
+    MSH_TRY(check_count(S, "msh_ntree_nearest"));
     if (S == 0) return MSH_OK;
     hipStream_t s = t->stream;
     Workspace& ws = t->ws;
-    DevBuf dn;
     int st = MSH_OK;
-    do {
-        if ((st = upload(ws.q, q, 3 * S, s)) != MSH_OK) break;
-        if ((st = upload(dn, n, 3 * S, s)) != MSH_OK) break;
-        if ((st = ws.out_a.reserve(S * sizeof(uint32_t))) != MSH_OK) break;
-        if ((st = ws.out_c.reserve(3 * S * sizeof(double))) != MSH_OK) break;
-        const uint32_t* perm = nullptr;
-        if ((st = sort_queries(t, ws.q.as<double>(), S, s, &perm)) != MSH_OK) break;
-        if ((st = launch_nnearest(t, ws.q.as<double>(), dn.as<double>(), perm, S, ws.out_a.as<uint32_t>(),
-                                  ws.out_c.as<double>(), s)) != MSH_OK)
-            break;
-        hipError_t e;
-        if ((e = hipMemcpyAsync(face, ws.out_a.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipMemcpyAsync(pt, ws.out_c.ptr, 3 * S * sizeof(double), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipStreamSynchronize(s)) != hipSuccess) {
-            set_error("normals nearest: %s", hipGetErrorString(e));
-            st = MSH_EDEVICE;
-        }
-    } while (0);
-    (void)hipStreamSynchronize(s);
-    dn.release();
+    {
+        WsOrder order(t, s);
+        do {
+            if ((st = upload(ws.q, q, 3 * S, s)) != MSH_OK) break;
+            if ((st = upload(ws.n, n, 3 * S, s)) != MSH_OK) break;
+            if ((st = ws.out_a.reserve(S * sizeof(uint32_t))) != MSH_OK) break;
+            if ((st = ws.out_c.reserve(3 * S * sizeof(double))) != MSH_OK) break;
+            QueryOrder ord;
+            if ((st = sort_queries(t, ws.q.as<double>(), ws.n.as<double>(), S, s, &ord)) != MSH_OK) break;
+            if ((st = launch_nnearest(t, ord, S, SlotOut{ws.out_a.as<uint32_t>(), nullptr, ws.out_c.as<double>(), nullptr,
+                                                        nullptr}, s)) != MSH_OK)
+                break;
+            hipError_t e;
+            if ((e = hipMemcpyAsync(face, ws.out_a.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                (e = hipMemcpyAsync(pt, ws.out_c.ptr, 3 * S * sizeof(double), hipMemcpyDeviceToHost, s)) != hipSuccess) {
+                set_error("normals nearest: %s", hipGetErrorString(e));
+                st = MSH_EDEVICE;
+            }
+        } while (0);
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && st == MSH_OK) {
+        set_error("normals nearest: kernel failure");
+        st = MSH_EDEVICE;
+    }
     return st;
 }
 
@@ -575,6 +865,7 @@ int msh_ntree_selfintersects(msh_tree* t, int64_t* count) {
     std::vector<uint32_t> flags(t->T);
     int st = MSH_OK;
     do {
+        WsOrder order(t, s);
         if ((st = df.reserve(t->T * sizeof(uint32_t))) != MSH_OK) break;
         if ((st = launch_tri_intersect(t, static_cast<const TriRec*>(t->d_leaves), t->T, 1, df.as<uint32_t>(), s)) !=
             MSH_OK)
@@ -595,6 +886,20 @@ int msh_ntree_selfintersects(msh_tree* t, int64_t* count) {
     return MSH_OK;
 }
 
+int msh_visibility_device(msh_tree* t, const double* d_cams, size_t C, const double* d_normals, const double* d_sensors,
+                          double min_dist, size_t v_begin, size_t v_count, uint32_t* d_vis, double* d_ndc, void* stream) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_visibility_device"));
+    if (v_begin > t->P || v_count > t->P - v_begin) {
+        set_error("msh_visibility_device: vertex range [%zu, %zu) outside the %zu main-mesh vertices", v_begin,
+                  v_begin + v_count, t->P);
+        return MSH_EINVAL;
+    }
+    if (C * v_count == 0) return MSH_OK;
+    hipStream_t s = pick(t, stream);
+    WsOrder order(t, s);
+    return launch_visibility(t, d_cams, C, d_normals, d_sensors, min_dist, v_begin, v_count, d_vis, d_ndc, s);
+}
+
 int msh_visibility(msh_tree* t, const double* cams, size_t C, const double* normals, const double* sensors,
                    double min_dist, uint32_t* vis, double* ndc) {
     MSH_TRY(check_tree(t, kTriangles, "msh_visibility"));
@@ -609,9 +914,9 @@ int msh_visibility(msh_tree* t, const double* cams, size_t C, const double* norm
         if (sensors && (st = upload(ds, sensors, 9 * C, s)) != MSH_OK) break;
         if ((st = dv.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
         if ((st = dd.reserve(n * sizeof(double))) != MSH_OK) break;
-        if ((st = launch_visibility(t, dc.as<double>(), C, normals ? dn.as<double>() : nullptr,
-                                    sensors ? ds.as<double>() : nullptr, min_dist, dv.as<uint32_t>(), dd.as<double>(),
-                                    s)) != MSH_OK)
+        if ((st = msh_visibility_device(t, dc.as<double>(), C, normals ? dn.as<double>() : nullptr,
+                                        sensors ? ds.as<double>() : nullptr, min_dist, 0, t->P, dv.as<uint32_t>(),
+                                        dd.as<double>(), s)) != MSH_OK)
             break;
         hipError_t e;
         if ((e = hipMemcpyAsync(vis, dv.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
@@ -628,19 +933,85 @@ int msh_visibility(msh_tree* t, const double* cams, size_t C, const double* norm
 
 int msh_points_nearest(msh_tree* t, const double* q, size_t S, uint32_t* idx, double* dist) {
     MSH_TRY(check_tree(t, kPoints, "msh_points_nearest"));
+    MSH_TRY(check_count(S, "msh_points_nearest"));
     if (S == 0) return MSH_OK;
     hipStream_t s = t->stream;
     Workspace& ws = t->ws;
-    MSH_TRY(upload(ws.q, q, 3 * S, s));
-    MSH_TRY(ws.out_a.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.out_c.reserve(S * sizeof(double)));
-    const uint32_t* perm = nullptr;
-    MSH_TRY(sort_queries(t, ws.q.as<double>(), S, s, &perm));
-    MSH_TRY(launch_points_nearest(t, ws.q.as<double>(), perm, S, ws.out_a.as<uint32_t>(), ws.out_c.as<double>(), s));
-    MSH_HIP(hipMemcpyAsync(idx, ws.out_a.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    MSH_HIP(hipMemcpyAsync(dist, ws.out_c.ptr, S * sizeof(double), hipMemcpyDeviceToHost, s));
-    MSH_HIP(hipStreamSynchronize(s));
-    return MSH_OK;
+    int st = MSH_OK;
+    {
+        WsOrder order(t, s);
+        do {
+            if ((st = upload(ws.q, q, 3 * S, s)) != MSH_OK) break;
+            if ((st = ws.out_a.reserve(S * sizeof(uint32_t))) != MSH_OK) break;
+            if ((st = ws.out_c.reserve(S * sizeof(double))) != MSH_OK) break;
+            QueryOrder ord;
+            if ((st = sort_queries(t, ws.q.as<double>(), nullptr, S, s, &ord)) != MSH_OK) break;
+            if ((st = launch_points_nearest(t, ord, S, SlotOut{ws.out_a.as<uint32_t>(), nullptr, nullptr,
+                                                                ws.out_c.as<double>(), nullptr}, s)) != MSH_OK)
+                break;
+            hipError_t e;
+            if ((e = hipMemcpyAsync(idx, ws.out_a.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+                (e = hipMemcpyAsync(dist, ws.out_c.ptr, S * sizeof(double), hipMemcpyDeviceToHost, s)) != hipSuccess) {
+                set_error("points nearest: %s", hipGetErrorString(e));
+                st = MSH_EDEVICE;
+            }
+        } while (0);
+    }
+    if (hipStreamSynchronize(s) != hipSuccess && st == MSH_OK) {
+        set_error("points nearest: kernel failure");
+        st = MSH_EDEVICE;
+    }
+    return st;
+}
+
+// ---- mesh geometry ----
+int msh_vertex_normals_device(const double* d_v, size_t P, const uint32_t* d_f, size_t T, double* d_vn, void* stream) {
+    if (P && (!d_v || !d_vn)) { set_error("msh_vertex_normals_device: null argument"); return MSH_EINVAL; }
+    if (T && !d_f) { set_error("msh_vertex_normals_device: null faces"); return MSH_EINVAL; }
+    if (P > 0xFFFFFFFFull) { set_error("msh_vertex_normals_device: too many vertices"); return MSH_EINVAL; }
+    int dev = 0;
+    MSH_TRY(current_device(&dev));
+    MSH_TRY(use_device(dev));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    Workspace ws;
+    int st = vertex_normals(d_v, P, d_f, T, d_vn, ws, s);
+    hipError_t e = hipStreamSynchronize(s);  // the scratch below is released on return
+    ws.release();
+    if (st == MSH_OK && e != hipSuccess) {
+        set_error("vertex normals: %s", hipGetErrorString(e));
+        st = MSH_EDEVICE;
+    }
+    return st;
+}
+
+int msh_vertex_normals(const double* v, size_t P, const uint32_t* f, size_t T, double* vn) {
+    if (P && (!v || !vn)) { set_error("msh_vertex_normals: null argument"); return MSH_EINVAL; }
+    MSH_TRY(check_faces(f, T, P, "msh_vertex_normals"));
+    if (P == 0) return MSH_OK;
+    int dev = 0;
+    MSH_TRY(current_device(&dev));
+    MSH_TRY(use_device(dev));
+    hipStream_t s = nullptr;
+    MSH_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    DevBuf dv, df, dn;
+    int st = MSH_OK;
+    do {
+        if ((st = upload(dv, v, 3 * P, s)) != MSH_OK) break;
+        if ((st = upload(df, f, 3 * T, s)) != MSH_OK) break;
+        if ((st = dn.reserve(3 * P * sizeof(double))) != MSH_OK) break;
+        if ((st = msh_vertex_normals_device(dv.as<double>(), P, df.as<uint32_t>(), T, dn.as<double>(), s)) != MSH_OK)
+            break;
+        hipError_t e;
+        if ((e = hipMemcpyAsync(vn, dn.ptr, 3 * P * sizeof(double), hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipStreamSynchronize(s)) != hipSuccess) {
+            set_error("vertex normals: %s", hipGetErrorString(e));
+            st = MSH_EDEVICE;
+        }
+    } while (0);
+    (void)hipStreamSynchronize(s);
+    dv.release(); df.release(); dn.release();
+    (void)hipStreamDestroy(s);
+    return st;
 }
 
 // ---- blob (RCCL replication) ----
@@ -652,37 +1023,103 @@ struct BlobHeader {
     float scene_lo[3], scene_hi[3];
     uint64_t off_v, off_nodes, off_leaves, total;
     double origin[3];
+    uint32_t node_bytes, leaf_bytes;
 };
-static const uint64_t kBlobMagic = 0x4d53484c42564832ull;  // "MSHLBVH2"
+static const uint64_t kBlobMagic = 0x4d53484c42564833ull;  // "MSHLBVH3"
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static void blob_layout(const msh_tree* t, BlobHeader& h) {
+static void blob_layout_sizes(int kind, uint64_t P, uint64_t T, BlobHeader& h) {
     std::memset(&h, 0, sizeof(h));
     h.magic = kBlobMagic;
-    h.kind = t->kind;
-    h.max_depth = t->max_depth;
-    h.P = t->P;
-    h.T = t->T;
-    h.T_main = t->T_main;
+    h.kind = kind;
+    h.P = P;
+    h.T = T;
     // visibility trees keep the extra-mesh vertices after the main rows; only the main rows are needed
-    h.v_rows = t->P;
+    h.v_rows = P;
+    h.node_bytes = (uint32_t)sizeof(BNode);
+    h.leaf_bytes = (uint32_t)(kind == kPoints ? sizeof(PtRec) : sizeof(TriRec));
+    h.off_v = align256(sizeof(BlobHeader));
+    h.off_nodes = align256(h.off_v + h.v_rows * 3 * sizeof(double));
+    h.off_leaves = align256(h.off_nodes + (T > 1 ? (T - 1) * sizeof(BNode) : 0));
+    h.total = align256(h.off_leaves + T * h.leaf_bytes);
+}
+
+static void blob_layout(const msh_tree* t, BlobHeader& h) {
+    blob_layout_sizes(t->kind, t->P, t->T, h);
+    h.max_depth = t->max_depth;
+    h.T_main = t->T_main;
     h.eps = t->eps;
     for (int k = 0; k < 3; ++k) {
         h.scene_lo[k] = t->scene_lo[k];
         h.scene_hi[k] = t->scene_hi[k];
         h.origin[k] = t->origin[k];
     }
-    const size_t leaf = t->kind == kPoints ? sizeof(PtRec) : sizeof(TriRec);
-    h.off_v = align256(sizeof(BlobHeader));
-    h.off_nodes = align256(h.off_v + h.v_rows * 3 * sizeof(double));
-    h.off_leaves = align256(h.off_nodes + (t->T > 1 ? (t->T - 1) * sizeof(BNode) : 0));
-    h.total = align256(h.off_leaves + t->T * leaf);
+}
+
+static int blob_check(const BlobHeader& h, size_t bytes) {
+    BlobHeader want;
+    if (h.magic != kBlobMagic) {
+        set_error("not a meshsearch tree blob (magic %llx)", (unsigned long long)h.magic);
+        return MSH_EINVAL;
+    }
+    if (h.kind < 0 || h.kind > 2 || h.T == 0 || h.T > 0x7FFFFFFFull || h.P > 0xFFFFFFFFull) {
+        set_error("corrupt tree blob header (kind %d, P %llu, T %llu)", h.kind, (unsigned long long)h.P,
+                  (unsigned long long)h.T);
+        return MSH_EINVAL;
+    }
+    blob_layout_sizes(h.kind, h.P, h.T, want);
+    if (h.node_bytes != want.node_bytes || h.leaf_bytes != want.leaf_bytes || h.off_v != want.off_v ||
+        h.off_nodes != want.off_nodes || h.off_leaves != want.off_leaves || h.total != want.total) {
+        set_error("tree blob layout mismatch (built by a different library version?)");
+        return MSH_EINVAL;
+    }
+    if (h.total > bytes) {
+        set_error("tree blob truncated: header says %llu bytes, %zu given", (unsigned long long)h.total, bytes);
+        return MSH_EINVAL;
+    }
+    return MSH_OK;
+}
+
+static void blob_info_of(const BlobHeader& h, msh_blob_info* out) {
+    out->kind = h.kind;
+    out->max_depth = h.max_depth;
+    out->n_points = h.P;
+    out->n_faces = h.T;
+    out->n_main_faces = h.T_main;
+    out->off_vertices = h.off_v;
+    out->off_nodes = h.off_nodes;
+    out->off_leaves = h.off_leaves;
+    out->total = h.total;
+    out->node_bytes = h.node_bytes;
+    out->leaf_bytes = h.leaf_bytes;
+    for (int k = 0; k < 3; ++k) out->origin[k] = h.origin[k];
+}
+
+int msh_blob_header_write(int kind, uint64_t P, uint64_t T, uint64_t T_main, void* dst, size_t cap, msh_blob_info* info) {
+    if (!dst || kind < 0 || kind > 2 || T == 0) { set_error("msh_blob_header_write: bad argument"); return MSH_EINVAL; }
+    BlobHeader h;
+    blob_layout_sizes(kind, P, T, h);
+    h.T_main = T_main;
+    if (cap < sizeof(h)) { set_error("msh_blob_header_write: %zu bytes < header", cap); return MSH_EINVAL; }
+    std::memcpy(dst, &h, sizeof(h));
+    if (info) blob_info_of(h, info);
+    return MSH_OK;
+}
+
+int msh_blob_header_parse(const void* src, size_t bytes, msh_blob_info* info) {
+    if (!src || !info) { set_error("msh_blob_header_parse: null argument"); return MSH_EINVAL; }
+    BlobHeader h;
+    if (bytes < sizeof(h)) { set_error("tree blob shorter than its header (%zu bytes)", bytes); return MSH_EINVAL; }
+    std::memcpy(&h, src, sizeof(h));
+    MSH_TRY(blob_check(h, bytes));
+    blob_info_of(h, info);
+    return MSH_OK;
 }
 
 int msh_tree_blob_size(const msh_tree* t, size_t* bytes) {
     if (!t || !bytes) { set_error("null argument"); return MSH_EINVAL; }
-    if (t->B != 1) { set_error("msh_tree_blob_size: batched trees are not serialisable"); return MSH_EINVAL; }
+    if (t->B != 1 || t->d_boxes) { set_error("msh_tree_blob_size: batched trees are not serialisable"); return MSH_EINVAL; }
     BlobHeader h;
     blob_layout(t, h);
     *bytes = h.total;
@@ -691,7 +1128,7 @@ int msh_tree_blob_size(const msh_tree* t, size_t* bytes) {
 
 int msh_tree_blob_pack(const msh_tree* t, void* d_dst, void* stream) {
     if (!t || !d_dst) { set_error("null argument"); return MSH_EINVAL; }
-    if (t->B != 1) { set_error("msh_tree_blob_pack: batched trees are not serialisable"); return MSH_EINVAL; }
+    if (t->B != 1 || t->d_boxes) { set_error("msh_tree_blob_pack: batched trees are not serialisable"); return MSH_EINVAL; }
     MSH_TRY(use_device(t->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : t->stream;
     BlobHeader h;
@@ -701,8 +1138,7 @@ int msh_tree_blob_pack(const msh_tree* t, void* d_dst, void* stream) {
     if (h.v_rows) MSH_HIP(hipMemcpyAsync(dst + h.off_v, t->d_v, h.v_rows * 3 * sizeof(double), hipMemcpyDeviceToDevice, s));
     if (t->T > 1)
         MSH_HIP(hipMemcpyAsync(dst + h.off_nodes, t->d_nodes, (t->T - 1) * sizeof(BNode), hipMemcpyDeviceToDevice, s));
-    const size_t leaf = t->kind == kPoints ? sizeof(PtRec) : sizeof(TriRec);
-    MSH_HIP(hipMemcpyAsync(dst + h.off_leaves, t->d_leaves, t->T * leaf, hipMemcpyDeviceToDevice, s));
+    MSH_HIP(hipMemcpyAsync(dst + h.off_leaves, t->d_leaves, t->T * h.leaf_bytes, hipMemcpyDeviceToDevice, s));
     MSH_HIP(hipStreamSynchronize(s));
     return MSH_OK;
 }
@@ -712,13 +1148,11 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
     *out = nullptr;
     MSH_TRY(use_device(device));
     BlobHeader h;
+    if (bytes < sizeof(h)) { set_error("tree blob shorter than its header (%zu bytes)", bytes); return MSH_EINVAL; }
     hipStream_t us = static_cast<hipStream_t>(stream);
     MSH_HIP(hipMemcpyAsync(&h, d_src, sizeof(h), hipMemcpyDeviceToHost, us));
     MSH_HIP(hipStreamSynchronize(us));
-    if (h.magic != kBlobMagic || h.total > bytes) {
-        set_error("not a meshsearch tree blob (magic %llx, %zu bytes)", (unsigned long long)h.magic, bytes);
-        return MSH_EINVAL;
-    }
+    MSH_TRY(blob_check(h, bytes));
     const int prev = g_device;
     g_device = device;
     msh_tree* t = nullptr;
@@ -736,7 +1170,7 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
         t->origin[k] = h.origin[k];
     }
     const char* src = static_cast<const char*>(d_src);
-    const size_t leaf = h.kind == kPoints ? sizeof(PtRec) : sizeof(TriRec);
+    const size_t leaf = h.leaf_bytes;
     hipStream_t s = us ? us : t->stream;
     do {
         hipError_t e = hipMalloc(&t->d_v, std::max<uint64_t>(h.v_rows, 1) * 3 * sizeof(double));
@@ -860,53 +1294,76 @@ int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size
     return MSH_OK;
 }
 
-int msh_batch_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part, double* d_pt,
-                             void* stream) {
-    MSH_TRY(check_batch(t, "msh_batch_nearest_device"));
+static int batch_query(msh_tree* t, const double* d_q, size_t S, const SlotOut& o, void* stream, const char* fn) {
+    MSH_TRY(check_batch(t, fn));
     const size_t n = t->B * S;
     if (n == 0) return MSH_OK;
-    if (n > (size_t)0xFFFFFFFFu) { set_error("msh_batch_nearest: %zu queries exceed 2^32", n); return MSH_EINVAL; }
-    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : t->stream;
+    MSH_TRY(check_count(n, fn));
+    hipStream_t s = pick(t, stream);
+    WsOrder order(t, s);
+    QueryOrder ord;
+    MSH_TRY(sort_batch_queries(t, d_q, n, S, s, &ord));
+    return launch_nearest_batch(t, ord, n, S, o, s);
+}
+
+int msh_batch_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part, double* d_pt,
+                             void* stream) {
+    return batch_query(t, d_q, S, SlotOut{d_face, d_part, d_pt, nullptr, nullptr}, stream, "msh_batch_nearest_device");
+}
+
+int msh_batch_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, double* d_pt, double* d_w,
+                                  void* stream) {
+    if (!d_w) { set_error("msh_batch_nearest_bary_device: null weights"); return MSH_EINVAL; }
+    return batch_query(t, d_q, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_w}, stream, "msh_batch_nearest_bary_device");
+}
+
+static int batch_host(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt, double* w,
+                      const char* fn) {
+    MSH_TRY(check_batch(t, fn));
+    const size_t n = t->B * S;
+    if (n == 0) return MSH_OK;
+    MSH_TRY(check_count(n, fn));
+    if (!q || !face || !pt) { set_error("%s: null argument", fn); return MSH_EINVAL; }
+    hipStream_t s = t->stream;
     Workspace& ws = t->ws;
-    const uint32_t* perm = nullptr;
-    if (n >= kSortMin) {  // Morton order inside each mesh, meshes in order (two stable passes)
-        MSH_TRY(ws.keys.reserve(n * sizeof(uint32_t)));
-        MSH_TRY(ws.vals.reserve(n * sizeof(uint32_t)));
-        MSH_TRY(ws.keys_alt.reserve(n * sizeof(uint32_t)));
-        MSH_TRY(ws.vals_alt.reserve(n * sizeof(uint32_t)));
-        uint32_t* keys = ws.keys.as<uint32_t>();
-        uint32_t* vals = ws.vals.as<uint32_t>();
-        MSH_TRY(query_morton_batch(t, d_q, n, S, keys, vals, s));
-        MSH_TRY(radix_sort_pairs(keys, vals, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n, 30, ws, s));
-        if (t->B > 1) {
-            MSH_TRY(mesh_keys(vals, n, S, keys, s));
-            int bits = 0;
-            while (bits < 32 && ((size_t)1 << bits) < t->B) ++bits;
-            MSH_TRY(radix_sort_pairs(keys, vals, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n, bits, ws, s));
-        }
-        perm = vals;
+    int st = MSH_OK;
+    {
+        WsOrder order(t, s);
+        do {
+            if ((st = upload(ws.q, q, 3 * n, s)) != MSH_OK) break;
+            if ((st = ws.out_a.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
+            if ((st = ws.out_b.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
+            if ((st = ws.out_c.reserve(3 * n * sizeof(double))) != MSH_OK) break;
+            if (w && (st = ws.out_d.reserve(3 * n * sizeof(double))) != MSH_OK) break;
+            const SlotOut o{ws.out_a.as<uint32_t>(), part && !w ? ws.out_b.as<uint32_t>() : nullptr, ws.out_c.as<double>(),
+                            nullptr, w ? ws.out_d.as<double>() : nullptr};
+            QueryOrder ord;
+            if ((st = sort_batch_queries(t, ws.q.as<double>(), n, S, s, &ord)) != MSH_OK) break;
+            if ((st = launch_nearest_batch(t, ord, n, S, o, s)) != MSH_OK) break;
+            hipError_t e = hipMemcpyAsync(face, ws.out_a.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess && o.part) e = hipMemcpyAsync(part, ws.out_b.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(pt, ws.out_c.ptr, 3 * n * sizeof(double), hipMemcpyDeviceToHost, s);
+            if (e == hipSuccess && w) e = hipMemcpyAsync(w, ws.out_d.ptr, 3 * n * sizeof(double), hipMemcpyDeviceToHost, s);
+            if (e != hipSuccess) {
+                set_error("%s: %s", fn, hipGetErrorString(e));
+                st = MSH_EDEVICE;
+            }
+        } while (0);
     }
-    return launch_nearest_batch(t, d_q, perm, n, S, d_face, d_part, d_pt, s);
+    if (hipStreamSynchronize(s) != hipSuccess && st == MSH_OK) {
+        set_error("%s: kernel failure", fn);
+        st = MSH_EDEVICE;
+    }
+    return st;
 }
 
 int msh_batch_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
-    MSH_TRY(check_batch(t, "msh_batch_nearest"));
-    const size_t n = t->B * S;
-    if (n == 0) return MSH_OK;
-    if (!q || !face || !pt) { set_error("msh_batch_nearest: null argument"); return MSH_EINVAL; }
-    hipStream_t s = t->stream;
-    Workspace& ws = t->ws;
-    MSH_TRY(upload(ws.q, q, 3 * n, s));
-    MSH_TRY(ws.out_a.reserve(n * sizeof(uint32_t)));
-    MSH_TRY(ws.out_b.reserve(n * sizeof(uint32_t)));
-    MSH_TRY(ws.out_c.reserve(3 * n * sizeof(double)));
-    MSH_TRY(msh_batch_nearest_device(t, ws.q.as<double>(), S, ws.out_a.as<uint32_t>(),
-                                     part ? ws.out_b.as<uint32_t>() : nullptr, ws.out_c.as<double>(), s));
-    MSH_HIP(hipMemcpyAsync(face, ws.out_a.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    if (part) MSH_HIP(hipMemcpyAsync(part, ws.out_b.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-    MSH_HIP(hipMemcpyAsync(pt, ws.out_c.ptr, 3 * n * sizeof(double), hipMemcpyDeviceToHost, s));
-    MSH_HIP(hipStreamSynchronize(s));
-    return MSH_OK;
+    return batch_host(t, q, S, face, part, pt, nullptr, "msh_batch_nearest");
+}
+
+int msh_batch_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face, double* pt, double* w) {
+    if (!w) { set_error("msh_batch_nearest_bary: null weights"); return MSH_EINVAL; }
+    return batch_host(t, q, S, face, nullptr, pt, w, "msh_batch_nearest_bary");
 }
 
 }  // extern "C"

@@ -39,13 +39,48 @@ struct DevBuf {
     T* as() const { return static_cast<T*>(ptr); }
 };
 
-// Reusable per-handle scratch (query keys / permutation / sort temporaries / results).
+// Reusable per-handle scratch (query keys / permutation / sort temporaries / slot-order queries and
+// results / staging).
 struct Workspace {
-    DevBuf keys, vals, keys_alt, vals_alt, hist, scan, q, out_a, out_b, out_c, flags, counters, spill, stats, ranges;
+    DevBuf keys, vals, keys_alt, vals_alt, hist, scan, q, n, out_a, out_b, out_c, out_d, flags, counters, spill, stats,
+        ranges, qs, ns, inv, res, res_w;
     void release();
 };
 
 enum Kind { kTriangles = 0, kNormals = 1, kPoints = 2 };
+
+// 32-B slot-order result record written (coalesced) by the traversal kernels: face / index, part code,
+// point (or distance in x for point trees).
+struct alignas(16) QRes {
+    uint32_t face, part;
+    double x, y, z;
+};
+static_assert(sizeof(QRes) == 32, "QRes must be 32 B");
+// one record as two 16-B stores
+__device__ inline void store_qres(QRes* r, uint32_t face, uint32_t part, double x, double y, double z) {
+    const unsigned long long xb = (unsigned long long)__double_as_longlong(x);
+    reinterpret_cast<uint4*>(r)[0] = make_uint4(face, part, (uint32_t)xb, (uint32_t)(xb >> 32));
+    reinterpret_cast<double2*>(r)[1] = make_double2(y, z);
+}
+
+// Caller-order output arrays of a point query (nullptr = not wanted).  w: per-row extra doubles
+// (barycentric weights, or the ray distance).
+struct SlotOut {
+    uint32_t* face;
+    uint32_t* part;
+    double* pt;
+    double* dist;
+    double* w;
+};
+
+// Order in which a launch visits its queries: q (and n) are the rows in slot order; perm maps a slot
+// to the caller's row and inv back (both nullptr: identity, the caller's arrays are used directly).
+struct QueryOrder {
+    const double* q;
+    const double* n;
+    const uint32_t* perm;
+    const uint32_t* inv;
+};
 
 }  // namespace msh
 
@@ -64,7 +99,16 @@ struct msh_tree {
     double origin[3] = {0, 0, 0};  // fp64 scene-box centre: all fp32 node bounds are relative to it
     double* d_orgs = nullptr;      // (B,3) per-mesh origins on the device (B = 1: a copy of origin)
     double* d_boxes = nullptr;     // (B,6) per-mesh boxes (batched trees: query Morton codes)
+    uint32_t* d_vorder = nullptr;  // Morton order of the main vertices (lazily built for visibility)
     hipStream_t stream = nullptr;
+    hipEvent_t ws_done = nullptr;  // recorded after the last launch that used `ws` (stream ordering)
+    // host-call staging (lazily created, grow-only): two pinned host slabs, two device slabs, copy
+    // streams and their events (api.cpp pipelined())
+    void* h_stage[2] = {nullptr, nullptr};
+    void* d_stage[2] = {nullptr, nullptr};
+    size_t stage_bytes = 0;
+    hipStream_t s_up = nullptr, s_down = nullptr;
+    hipEvent_t e_up[2] = {nullptr, nullptr}, e_run[2] = {nullptr, nullptr}, e_down[2] = {nullptr, nullptr};
     double build_ms = 0.0;
     int max_depth = 0;             // deepest leaf (root children = 1)
     msh::Workspace ws;
@@ -109,29 +153,43 @@ int point_bounds(const double* d_v, size_t P, double* d_lo, double* d_hi, hipStr
 // ---- queries (nearest.hip) ----
 // 30-bit Morton codes of query points in the tree's scene box + iota values.
 int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* keys, uint32_t* vals, hipStream_t s);
-int launch_nearest(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S, uint32_t* d_face,
-                   uint32_t* d_part, double* d_pt, hipStream_t s);
-// batched trees: n = B*S queries, query i answered on mesh i / S
-int launch_nearest_batch(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t n, size_t S,
-                         uint32_t* d_face, uint32_t* d_part, double* d_pt, hipStream_t s);
-int launch_nearest_stats(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S,
-                         unsigned long long* d_counts, hipStream_t s);
-int launch_nnearest(const msh_tree* tree, const double* d_q, const double* d_n, const uint32_t* d_perm, size_t S,
-                    uint32_t* d_face, double* d_pt, hipStream_t s);
-int launch_points_nearest(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S,
-                          uint32_t* d_idx, double* d_dist, hipStream_t s);
+// slot i <- rows perm[i] of a (and b when non-null); inv[perm[i]] = i
+int gather_rows(const double* d_a, const double* d_b, const uint32_t* d_perm, size_t S, double* d_as, double* d_bs,
+                uint32_t* d_inv, hipStream_t s);
+// caller row j <- slot inv[j] (record fields + nw doubles per row from d_w)
+int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32_t* d_inv, size_t S, const SlotOut& o,
+                      hipStream_t s);
+// closest point: o.face, o.part (nullable), o.pt; with o.w (3 per row) the barycentric variant (part unused)
+int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s);
+// batched trees: n = B*S queries, slot i answered on mesh i / S (the batched sort is mesh-major)
+int launch_nearest_batch(const msh_tree* tree, const QueryOrder& ord, size_t n, size_t S, const SlotOut& o,
+                         hipStream_t s);
+int launch_nearest_stats(const msh_tree* tree, const QueryOrder& ord, size_t S, unsigned long long* d_counts,
+                         hipStream_t s);
+// normals metric: o.face, o.pt; ord.n = query normals in slot order
+int launch_nnearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s);
+// vertex NN: o.face (index), o.dist
+int launch_points_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s);
 
 // ---- rays (rays.hip) ----
-int launch_alongnormal(const msh_tree* tree, const double* d_p, const double* d_n, const uint32_t* d_perm, size_t S,
-                       double* d_dist, uint32_t* d_face, double* d_pt, hipStream_t s);
+// alongnormal: ord.q / ord.n = sources / normals in slot order; o.w = distance (1 per row), o.face, o.pt
+int launch_alongnormal(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s);
+// visibility of vertices [v0, v0 + nv) from C cameras: vis / ndc are (C, nv)
 int launch_visibility(const msh_tree* tree, const double* d_cams, size_t C, const double* d_normals,
-                      const double* d_sensors, double min_dist, uint32_t* d_vis, double* d_ndc, hipStream_t s);
+                      const double* d_sensors, double min_dist, size_t v0, size_t nv, uint32_t* d_vis, double* d_ndc,
+                      hipStream_t s);
 
 // ---- triangle-triangle (tritri.hip) ----
 // flags[i] = 1 iff query triangle i intersects any tree triangle (self: skip shared-vertex pairs and
 // the query triangles are the tree's own leaves in face order).
 int launch_tri_intersect(const msh_tree* tree, const TriRec* d_qtris, size_t Tq, int self_mode, uint32_t* d_flags,
                          hipStream_t s);
+
+// ---- mesh geometry (geometry.hip) ----
+// area-weighted vertex normals of (P,3) v over (T,3) f: sum of the faces' cross products in ascending
+// face order per vertex, normalised (mesh.py:208-216)
+int vertex_normals(const double* d_v, size_t P, const uint32_t* d_f, size_t T, double* d_vn, Workspace& ws,
+                   hipStream_t s);
 
 // ---- timing ----
 struct TimedLaunch {

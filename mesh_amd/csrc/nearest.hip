@@ -1,7 +1,15 @@
 // K2 + K3 — closest-point traversal with fused fp64 refinement (replaces
 // spatialsearchmodule.cpp:165-220 aabbtree_nearest and CGAL's closest_point_and_primitive), plus the
-// normal-weighted metric variant (K7, aabb_normals.cpp:112-190) and the vertex nearest-neighbour
-// variant (K8, search.ClosestPointTree).
+// normal-weighted metric variant (K7, aabb_normals.cpp:112-190), the vertex nearest-neighbour variant
+// (K8, search.ClosestPointTree) and the barycentric variant (K9: nearest + Heidrich weights of the
+// closest point, mesh.py:218-222 / geometry/barycentric_coordinates_of_projection.py:9-49).
+//
+// Query pipeline (S >= kSortMin queries):
+//   k_query_morton -> radix sort (sort.hip) -> k_gather_queries: the query rows are copied ONCE into
+//   Morton (slot) order, coalesced, and the inverse permutation is recorded.  The traversal kernels
+//   read slot-order queries and write one 32-B slot-order record per query (coalesced), and
+//   k_unpermute moves the records back to query order (coalesced writes, one 32-B gathered read).
+//   Below kSortMin the kernels read and write the caller's arrays directly.
 //
 // Execution shape (gfx950):
 //   Pass 1 (k_knn): persistent grid; each WAVE dequeues 64-query tiles from one of 8 XCD-group
@@ -11,10 +19,9 @@
 //     (one L2 line) bounds both children by max(fp32 AABB bound, fp32 oriented-box bound); the far
 //     child is pushed (16-entry LDS stack per lane, [depth][lane] layout, deeper entries spill to a
 //     per-lane global area sized from the tree depth).  Leaf children are parked and tested in
-//     wave-wide leaf phases (Aila & Laine's postponed leaves).  A leaf test is fp32 only: lower and
-//     upper bounds of its distance (tri_d2_bounds); the upper bound tightens the pruning limit, the
-//     leaf stays a candidate, and CGAL's exact fp64 construction runs at the end of the query on the
-//     candidates that can still win (TriCandPol; the normals metric and points test exactly).
+//     wave-wide leaf phases (Aila & Laine's postponed leaves): an fp32 lower bound of the leaf's
+//     distance first (tri_d2_lo), CGAL's exact fp64 construction only if that cannot reject it.
+//     The fp32 pruning radius is cached per lane and refreshed only when the best distance changes.
 //     A lane that exceeds `budget` node steps stops and appends its query (with its exact best so far)
 //     to a deferred list: queries near the centre of a closed surface are equidistant from most of it
 //     and would otherwise hold their whole wave for ~10^6 steps.
@@ -40,7 +47,7 @@
 namespace msh {
 
 struct DeferRec {
-    uint32_t qi;
+    uint32_t slot;
     uint32_t face;
     int32_t leaf;
     uint32_t pad;
@@ -49,22 +56,27 @@ struct DeferRec {
 };
 static_assert(sizeof(DeferRec) == 32, "DeferRec must be 32 B");
 
+// MODE: 0 closest point (face, part, point), 1 normals metric (face, point), 2 vertex NN (index,
+// distance), 3 closest point + barycentric weights (face, point, weights)
 struct KnnArgs {
     const BNode* nodes;
     const void* leaves;
     size_t T;
-    const double* q;
-    const double* n;
-    const uint32_t* perm;
+    const double* q;       // query rows in slot order (Morton-sorted copy, or the caller's array)
+    const double* n;       // MODE 1: query normals in slot order
+    const uint32_t* perm;  // slot -> caller's query index (nullptr: identity)
     size_t S;
+    QRes* res;             // slot-order records (sorted path); nullptr: write the caller's arrays below
+    double* res_w;         // MODE 3 slot-order barycentric weights (3 per slot)
     uint32_t* out_face;
     uint32_t* out_part;
     double* out_pt;
     double* out_dist;
+    double* out_w;
     double eps;
     double org[3];  // tree origin: fp32 node bounds are relative to it
-    // batched trees (msh_batch_build): query i belongs to mesh i / qper, whose root is node mesh * npm
-    // and whose origin is orgs[3 * mesh]; orgs == nullptr for a single tree (root 0, origin org)
+    // batched trees (msh_batch_build): slot i belongs to mesh i / qper (the batched sort is mesh-major),
+    // whose root is node mesh * npm and whose origin is orgs[3 * mesh]; orgs == nullptr: single tree
     const double* orgs;
     size_t qper;
     size_t npm;
@@ -79,10 +91,10 @@ struct KnnArgs {
     unsigned max_deferred;
 };
 
-// root node and fp32 query of query qi (batched trees: its mesh's root and origin)
-__device__ inline int query_root(const KnnArgs& a, size_t qi, const D3& q, QF& qf) {
+// root node and fp32 query of slot i (batched trees: its mesh's root and origin)
+__device__ inline int query_root(const KnnArgs& a, size_t i, const D3& q, QF& qf) {
     if (a.orgs) {
-        const size_t mb = qi / a.qper;
+        const size_t mb = i / a.qper;
         const double o[3] = {a.orgs[3 * mb], a.orgs[3 * mb + 1], a.orgs[3 * mb + 2]};
         qf = make_qf(q, o);
         return (int)(mb * a.npm);
@@ -105,12 +117,14 @@ __device__ inline unsigned dequeue_tile(unsigned* counters, unsigned ntiles, uns
     return ntiles;
 }
 
+__device__ inline bool finite3(const D3& q) { return isfinite(q.x) && isfinite(q.y) && isfinite(q.z); }
+
 // ---- leaf policies ----
 // limit(): squared radius (in box-distance units) inside which a primitive can still beat or tie the
 // best.  `shared` is a bound published by other lanes working on the same query (pass 2); it is always
-// >= the final best, so pruning with min(best, shared) keeps the result exact.  Every leaf first gets
-// the conservative fp32 lower bound (tri_d2_lo); the exact fp64 CGAL construction runs only if that
-// cannot reject it.
+// >= the final best, so pruning with min(best, shared) keeps the result exact.  limf caches
+// limit() rounded up to fp32 (the unit of the node bounds); relim() refreshes it whenever best or
+// shared changes, so a traversal step compares against a register instead of re-deriving it.
 __device__ inline void rel_f32(const D3& a, const D3& q, float& x, float& y, float& z) {
     x = (float)(a.x - q.x);
     y = (float)(a.y - q.y);
@@ -123,8 +137,9 @@ struct TriPol {
     double best, shared;
     uint32_t best_face;
     int best_leaf;
+    float limf;
     __device__ double limit() const { return fmin(best, shared) * kSlack; }
-    __device__ void flush() {}
+    __device__ void relim() { limf = __double2float_ru(limit()); }
     __device__ void test(int leaf) {
         D3 a, b, c;
         uint32_t face;
@@ -134,11 +149,7 @@ struct TriPol {
         rel_f32(b, q, bx, by, bz);
         rel_f32(c, q, cx, cy, cz);
         const float lo = tri_d2_lo(ax, ay, az, bx, by, bz, cx, cy, cz);
-        if (lo > __double2float_ru(limit())) return;  // NaN never rejects
-#ifdef MSH_DIAG_SKIP_EXACT  // timing diagnostic only: wrong results
-        if ((double)lo < best) { best = lo; best_face = face; best_leaf = leaf; }
-        return;
-#endif
+        if (lo > limf) return;  // NaN never rejects
         D3 o;
         int part;
         const double d2 = closest_on_triangle(q, a, b, c, o, part);
@@ -146,79 +157,7 @@ struct TriPol {
             best = d2;
             best_face = face;
             best_leaf = leaf;
-        }
-    }
-};
-
-// Pass-1 triangle policy with deferred exact tests.  A leaf first gets both fp32 bounds
-// (tri_d2_bounds: lo <= d2 <= hi for the fp64 CGAL value).  Its upper bound tightens the pruning
-// limit at once, and the leaf is kept as a candidate (lo) instead of running the fp64 construction;
-// candidates whose lo exceeds the limit later are dropped, and flush() runs the exact construction
-// on the survivors only.  Exactness: the winning leaf, and every leaf tied with it, has
-// lo <= d2* <= limit at all times, so it is never dropped.  Leaves without fp32 information
-// (slivers, degenerate, non-finite) and candidates that find the list full are tested exactly on
-// the spot.
-struct TriCandPol {
-    const TriRec* __restrict__ tris;
-    D3 q;
-    double best, shared;  // exact part (as TriPol)
-    uint32_t best_face;
-    int best_leaf;
-    unsigned n_exact;
-    float hi;              // smallest fp32 upper bound among the candidates seen
-    int c0, c1, c2, c3;    // candidate leaves (-1 = free slot)
-    float l0, l1, l2, l3;  // their lower bounds
-    __device__ double limit() const { return fmin(fmin(best, shared), (double)hi) * kSlack; }
-    __device__ void exact(int leaf) {
-        D3 a, b, c, o;
-        uint32_t face;
-        int part;
-        load_tri(tris, leaf, a, b, c, face);
-        ++n_exact;
-        const double d2 = closest_on_triangle(q, a, b, c, o, part);
-        if (d2 < best || (d2 == best && face < best_face)) {
-            best = d2;
-            best_face = face;
-            best_leaf = leaf;
-        }
-    }
-    __device__ void test(int leaf) {
-        D3 a, b, c;
-        uint32_t face;
-        load_tri(tris, leaf, a, b, c, face);
-        float ax, ay, az, bx, by, bz, cx, cy, cz;
-        rel_f32(a, q, ax, ay, az);
-        rel_f32(b, q, bx, by, bz);
-        rel_f32(c, q, cx, cy, cz);
-        float lo, h;
-        tri_d2_bounds(ax, ay, az, bx, by, bz, cx, cy, cz, lo, h);
-        if (lo > __double2float_ru(limit())) return;  // NaN never rejects
-        if (!(h < INFINITY)) {                          // no fp32 information: exact now
-            exact(leaf);
-            return;
-        }
-        hi = fminf(hi, h);
-        const float lim = __double2float_ru(limit());
-        if (l0 > lim) c0 = -1;
-        if (l1 > lim) c1 = -1;
-        if (l2 > lim) c2 = -1;
-        if (l3 > lim) c3 = -1;
-        if (c0 < 0) { c0 = leaf; l0 = lo; }
-        else if (c1 < 0) { c1 = leaf; l1 = lo; }
-        else if (c2 < 0) { c2 = leaf; l2 = lo; }
-        else if (c3 < 0) { c3 = leaf; l3 = lo; }
-        else exact(leaf);
-    }
-    // exact constructions for the surviving candidates; afterwards best/best_face/best_leaf are final
-    __device__ void flush() {
-        const float lim = __double2float_ru(limit());
-#pragma unroll 1
-        while (max(max(c0, c1), max(c2, c3)) >= 0) {  // rotate through one exact() call site
-            if (c0 >= 0 && l0 <= lim) exact(c0);
-            c0 = c1; l0 = l1;
-            c1 = c2; l1 = l2;
-            c2 = c3; l2 = l3;
-            c3 = -1;
+            relim();
         }
     }
 };
@@ -232,6 +171,7 @@ struct NrmPol {
     double best, shared;
     uint32_t best_face;
     int best_leaf;
+    float limf;
     __device__ double limit() const {
         const double b = fmin(best, shared);
         if (b == INFINITY) return INFINITY;
@@ -240,7 +180,7 @@ struct NrmPol {
         if (r < 0.0) r = 0.0;
         return r * r * kSlack;
     }
-    __device__ void flush() {}
+    __device__ void relim() { limf = __double2float_ru(limit()); }
     __device__ void test(int leaf) {
         D3 a, b, c;
         uint32_t face;
@@ -250,7 +190,7 @@ struct NrmPol {
         rel_f32(b, q, bx, by, bz);
         rel_f32(c, q, cx, cy, cz);
         const float lo = tri_d2_lo(ax, ay, az, bx, by, bz, cx, cy, cz);
-        if (lo > __double2float_ru(limit())) return;
+        if (lo > limf) return;
         D3 o;
         int part;
         const double d2 = closest_on_triangle(q, a, b, c, o, part);
@@ -263,6 +203,7 @@ struct NrmPol {
             best = met;
             best_face = face;
             best_leaf = leaf;
+            relim();
         }
     }
 };
@@ -273,8 +214,9 @@ struct PtPol {
     double best, shared;
     uint32_t best_face;
     int best_leaf;
+    float limf;
     __device__ double limit() const { return fmin(best, shared) * kSlack; }
-    __device__ void flush() {}
+    __device__ void relim() { limf = __double2float_ru(limit()); }
     __device__ void test(int leaf) {
         const double2* p = reinterpret_cast<const double2*>(pts + leaf);
         const double2 x0 = p[0], x1 = p[1];
@@ -284,6 +226,7 @@ struct PtPol {
             best = d2;
             best_face = idx;
             best_leaf = leaf;
+            relim();
         }
     }
 };
@@ -303,7 +246,7 @@ struct Walker {
         while (sp > 0) {
             --sp;
             const uint2 e = sp < kStack ? lds[sp * kBlock] : spill[sp - kStack];
-            if (__uint_as_float(e.y) <= __double2float_ru(pol.limit())) {
+            if (__uint_as_float(e.y) <= pol.limf) {
                 node = (int)e.x;
                 return true;
             }
@@ -321,22 +264,19 @@ struct Walker {
         float d0, d1;
         node_child_bounds(nd, qf, d0, d1);
         const int c0 = nd.child(0), c1 = nd.child(1);
-        float lim = __double2float_ru(pol.limit());
-        bool h0 = d0 <= lim, h1 = d1 <= lim;
+        bool h0 = d0 <= pol.limf, h1 = d1 <= pol.limf;
         if (h0 && c0 < 0) {
             pol.test(~c0);
             if (STATS) ++n_leaves;
             h0 = false;
-            lim = __double2float_ru(pol.limit());
         }
         if (h1 && c1 < 0) {
             pol.test(~c1);
             if (STATS) ++n_leaves;
             h1 = false;
-            lim = __double2float_ru(pol.limit());
         }
-        h0 = h0 && d0 <= lim;
-        h1 = h1 && d1 <= lim;
+        h0 = h0 && d0 <= pol.limf;
+        h1 = h1 && d1 <= pol.limf;
         if (h0 && h1) {
             int nearc = c0, farc = c1;
             float dfar = d1;
@@ -360,7 +300,7 @@ struct Walker {
         float d0, d1;
         node_child_bounds(nd, qf, d0, d1);
         const int c0 = nd.child(0), c1 = nd.child(1);
-        const float lim = __double2float_ru(pol.limit());
+        const float lim = pol.limf;
         bool h0 = d0 <= lim, h1 = d1 <= lim;
         if (h0 && c0 < 0) {
             p0 = ~c0;
@@ -385,40 +325,73 @@ struct Walker {
     }
 };
 
-// Outputs of one query from its policy (winner's leaf -> point / part recomputed exactly).
+// Heidrich's barycentric coordinates of p's projection into triangle (a, b, c), with the operation
+// order of the reference's numpy code (barycentric_coordinates_of_projection.py:31-47, called with
+// q = a, u = b - a, v = c - a by mesh.py:222): n = u x v, s = n.n (0 -> numpy.spacing(1)),
+// b2 = ((u x w).n) / s, b1 = ((w x v).n) / s with w = p - a, weights (1 - b1 - b2, b1, b2).
+__device__ inline D3 heidrich_bary(const D3& p, const D3& a, const D3& b, const D3& c) {
+    const D3 u = vsub(b, a), v = vsub(c, a);
+    const D3 n = vcross(u, v);
+    double s = n.x * n.x + n.y * n.y + n.z * n.z;
+    if (s == 0.0) s = 2.220446049250313e-16;  // numpy.spacing(1)
+    const double inv = 1.0 / s;
+    const D3 w = vsub(p, a);
+    const double b2 = vdot(vcross(u, w), n) * inv;
+    const double b1 = vdot(vcross(w, v), n) * inv;
+    return D3{1.0 - b1 - b2, b1, b2};
+}
+
+// Outputs of slot i from its policy (winner's leaf -> point / part recomputed exactly).
 template <int MODE, class Pol>
-__device__ inline void write_result(const KnnArgs& a, size_t qi, const D3& q, const Pol& pol) {
-    if (MODE == 2) {
-        a.out_face[qi] = pol.best_face;
-        a.out_dist[qi] = sqrt(pol.best);
+__device__ inline void write_result(const KnnArgs& a, size_t i, const D3& q, const Pol& pol) {
+    if constexpr (MODE == 2) {
+        const double dist = pol.best_leaf >= 0 ? sqrt(pol.best) : NAN;
+        if (a.res) store_qres(a.res + i, pol.best_face, 0u, dist, 0.0, 0.0);
+        else {
+            a.out_face[i] = pol.best_face;
+            a.out_dist[i] = dist;
+        }
         return;
     }
     const TriRec* tris = static_cast<const TriRec*>(a.leaves);
-    D3 ta, tb, tc, o = D3{NAN, NAN, NAN};
-    uint32_t face = 0xFFFFFFFFu;
+    D3 ta, tb, tc, o = D3{NAN, NAN, NAN}, w = D3{NAN, NAN, NAN};
+    uint32_t face = MSH_NO_FACE;
     int part = 0;
     if (pol.best_leaf >= 0) {  // < 0 only for a non-finite query
         load_tri(tris, pol.best_leaf, ta, tb, tc, face);
         closest_on_triangle(q, ta, tb, tc, o, part);
+        if (MODE == 3) w = heidrich_bary(o, ta, tb, tc);
     }
-    a.out_face[qi] = face;
-    if (MODE == 0 && a.out_part) a.out_part[qi] = (uint32_t)part;
-    a.out_pt[3 * qi] = o.x;
-    a.out_pt[3 * qi + 1] = o.y;
-    a.out_pt[3 * qi + 2] = o.z;
+    if (a.res) {
+        store_qres(a.res + i, face, (uint32_t)part, o.x, o.y, o.z);
+        if (MODE == 3) {
+            a.res_w[3 * i] = w.x;
+            a.res_w[3 * i + 1] = w.y;
+            a.res_w[3 * i + 2] = w.z;
+        }
+        return;
+    }
+    a.out_face[i] = face;
+    if (MODE == 0 && a.out_part) a.out_part[i] = (uint32_t)part;
+    a.out_pt[3 * i] = o.x;
+    a.out_pt[3 * i + 1] = o.y;
+    a.out_pt[3 * i + 2] = o.z;
+    if (MODE == 3) {
+        a.out_w[3 * i] = w.x;
+        a.out_w[3 * i + 1] = w.y;
+        a.out_w[3 * i + 2] = w.z;
+    }
 }
 
 template <int MODE>
-struct PolOf;
-template <>
-struct PolOf<0> { using T = TriPol; };
+struct PolOf { using T = TriPol; };
 template <>
 struct PolOf<1> { using T = NrmPol; };
 template <>
 struct PolOf<2> { using T = PtPol; };
 
 template <int MODE>
-__device__ inline typename PolOf<MODE>::T make_pol(const KnnArgs& a, size_t qi, const D3& q) {
+__device__ inline typename PolOf<MODE>::T make_pol(const KnnArgs& a, size_t i, const D3& q) {
     typename PolOf<MODE>::T pol;
     if constexpr (MODE == 2) {
         pol.pts = static_cast<const PtRec*>(a.leaves);
@@ -427,15 +400,16 @@ __device__ inline typename PolOf<MODE>::T make_pol(const KnnArgs& a, size_t qi, 
     }
     pol.q = q;
     if constexpr (MODE == 1) {
-        pol.qn = D3{a.n[3 * qi], a.n[3 * qi + 1], a.n[3 * qi + 2]};
+        pol.qn = D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]};
         const double nq = sqrt(vdot(pol.qn, pol.qn));
         pol.eps = a.eps;
         pol.pmin = fmin(a.eps * (1 - nq), a.eps * (1 + nq));
     }
     pol.best = INFINITY;
     pol.shared = INFINITY;
-    pol.best_face = 0xFFFFFFFFu;
+    pol.best_face = MSH_NO_FACE;
     pol.best_leaf = -1;
+    pol.limf = INFINITY;
     return pol;
 }
 
@@ -447,32 +421,7 @@ __device__ inline void test_pending(Pol& pol, int& p0, int& p1) {
     p0 = p1 = -1;
 }
 
-// pass-1 policy: candidate-deferring triangles for plain closest point, the exact policies otherwise
-// MSH_CAND=1 selects TriCandPol for pass 1.  Off by default: on C3 it cut exact constructions from 10
-// to 5.4 per query but cost 18 VGPRs (3 instead of 4 waves/SIMD) and 2% more node visits: 293M vs
-// 332M queries/s (10M queries, one MI355X).
-#ifndef MSH_CAND
-#define MSH_CAND 0
-#endif
-template <int MODE>
-__device__ inline auto make_pol1(const KnnArgs& a, size_t qi, const D3& q) {
-    if constexpr (MODE == 0 && MSH_CAND) {
-        TriCandPol pol;
-        pol.tris = static_cast<const TriRec*>(a.leaves);
-        pol.q = q;
-        pol.best = INFINITY;
-        pol.shared = INFINITY;
-        pol.best_face = 0xFFFFFFFFu;
-        pol.best_leaf = -1;
-        pol.n_exact = 0;
-        pol.hi = INFINITY;
-        pol.c0 = pol.c1 = pol.c2 = pol.c3 = -1;
-        pol.l0 = pol.l1 = pol.l2 = pol.l3 = 0.f;
-        return pol;
-    } else {
-        return make_pol<MODE>(a, qi, q);
-    }
-}
+__device__ inline D3 load_q(const KnnArgs& a, size_t i) { return D3{a.q[3 * i], a.q[3 * i + 1], a.q[3 * i + 2]}; }
 
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
@@ -482,7 +431,6 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     uint2* spill = a.spill ? a.spill + ((size_t)blockIdx.x * kBlock + tid) * (size_t)a.spill_depth : nullptr;
     const unsigned group = blockIdx.x & 7u;
     unsigned long long u_trav_it = 0, u_trav_lanes = 0, u_leaf_it = 0, u_leaf_lanes = 0;  // STATS: wave iterations
-    unsigned n_exact = 0;
     unsigned n_nodes = 0, n_leaves = 0;
     for (;;) {
         unsigned tile = 0;
@@ -491,15 +439,18 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         if (tile >= a.ntiles) break;
         const size_t i = (size_t)tile * 64 + lane;
         if (i >= a.S) continue;
-        const size_t qi = a.perm ? (size_t)a.perm[i] : i;
-        const D3 q = D3{a.q[3 * qi], a.q[3 * qi + 1], a.q[3 * qi + 2]};
-        auto pol = make_pol1<MODE>(a, qi, q);
+        const D3 q = load_q(a, i);
+        auto pol = make_pol<MODE>(a, i, q);
+        if (!finite3(q)) {  // no distance is defined: NO_FACE / NaN, no traversal
+            if (!STATS) write_result<MODE>(a, i, q, pol);
+            continue;
+        }
         if (a.T == 1) {
             pol.test(0);
             if (STATS) ++n_leaves;
         } else {
             QF qf;
-            const int root = query_root(a, qi, q, qf);
+            const int root = query_root(a, i, q, qf);
             Walker w{root, 0};
             bool active = true, deferred = false;
             int p0 = -1, p1 = -1;  // leaf children waiting for a wave-wide leaf phase
@@ -537,9 +488,8 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
                         if (slot < a.max_deferred) {
                             test_pending(pol, p0, p1);
-                            pol.flush();
                             DeferRec r;
-                            r.qi = (uint32_t)qi;
+                            r.slot = (uint32_t)i;
                             r.face = pol.best_face;
                             r.leaf = pol.best_leaf;
                             r.pad = 0;
@@ -555,12 +505,9 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             }
             if (deferred) continue;
         }
-        pol.flush();
-        if (!STATS) write_result<MODE>(a, qi, q, pol);
-        if constexpr (STATS && MODE == 0 && MSH_CAND) n_exact += pol.n_exact;
+        if (!STATS) write_result<MODE>(a, i, q, pol);
     }
     if (STATS) {
-        atomicAdd(&a.stats[6], (unsigned long long)n_exact);
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
         atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
         if (lane == 0) {
@@ -595,7 +542,7 @@ __device__ inline double wave_min(double x) {
 
 constexpr int kFront = 512;  // frontier entries per wave in pass 2
 
-template <int MODE>
+template <int MODE, bool STATS>
 __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
     __shared__ uint2 front[4][2][kFront];
@@ -607,17 +554,18 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
     unsigned n_nodes = 0, n_leaves = 0;
     for (unsigned item = blockIdx.x * 4 + wv; item < total; item += gridDim.x * 4) {
         const DeferRec r = a.deferred[item];
-        const size_t qi = r.qi;
-        const D3 q = D3{a.q[3 * qi], a.q[3 * qi + 1], a.q[3 * qi + 2]};
+        const size_t i = r.slot;
+        const D3 q = load_q(a, i);
         QF qf;
-        const int root = query_root(a, qi, q, qf);
-        auto pol = make_pol<MODE>(a, qi, q);
+        const int root = query_root(a, i, q, qf);
+        auto pol = make_pol<MODE>(a, i, q);
         pol.shared = r.best;  // pass-1 best: an upper bound of the final best
         if (lane == 0) {
             pol.best = r.best;
             pol.best_face = r.face;
             pol.best_leaf = r.leaf;
         }
+        pol.relim();
         // breadth-first expansion of the top of the tree into <= kFront subtrees
         int cur = 0, n = 1;
         if (lane == 0) front[wv][0][0] = make_uint2((unsigned)root, 0u);
@@ -625,22 +573,22 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         while (n > 0 && n <= kFront / 2) {
             int m = 0;
             for (int base = 0; base < n; base += 64) {
-                const int i = base + lane;
+                const int j = base + lane;
                 bool k0 = false, k1 = false;
                 uint2 e0, e1;
-                if (i < n) {
-                    const uint2 e = front[wv][cur][i];
-                    if (__uint_as_float(e.y) <= __double2float_ru(pol.limit())) {
+                if (j < n) {
+                    const uint2 e = front[wv][cur][j];
+                    if (__uint_as_float(e.y) <= pol.limf) {
                         const NodeV nd = load_node(a.nodes, (int)e.x);
                         ++n_nodes;
                         float d0, d1;
                         node_child_bounds(nd, qf, d0, d1);
                         const int c0 = nd.child(0), c1 = nd.child(1);
-                        if (d0 <= __double2float_ru(pol.limit())) {
+                        if (d0 <= pol.limf) {
                             if (c0 < 0) { pol.test(~c0); ++n_leaves; }
                             else { k0 = true; e0 = make_uint2((unsigned)c0, __float_as_uint(d0)); }
                         }
-                        if (d1 <= __double2float_ru(pol.limit())) {
+                        if (d1 <= pol.limf) {
                             if (c1 < 0) { pol.test(~c1); ++n_leaves; }
                             else { k1 = true; e1 = make_uint2((unsigned)c1, __float_as_uint(d1)); }
                         }
@@ -652,6 +600,7 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
                 if (k1) front[wv][cur ^ 1][p0 + (k0 ? 1 : 0)] = e1;
                 m += __popcll(b0) + __popcll(b1);
                 pol.shared = fmin(pol.shared, wave_min(pol.best));
+                pol.relim();
             }
             __builtin_amdgcn_wave_barrier();
             cur ^= 1;
@@ -665,25 +614,28 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         while (__any(active)) {
             if (active) active = w.step<decltype(pol), false>(a.nodes, qf, pol, lds, spill, n_nodes, n_leaves);
             pol.shared = fmin(pol.shared, wave_min(pol.best));
+            pol.relim();
         }
         double best = pol.best;
         uint32_t face = pol.best_face;
         int leaf = pol.best_leaf;
         wave_lexmin(best, face, leaf);
-        if (lane == 0) {
+        if (lane == 0 && !STATS) {
             pol.best = best;
             pol.best_face = face;
             pol.best_leaf = leaf;
-            write_result<MODE>(a, qi, q, pol);
+            write_result<MODE>(a, i, q, pol);
         }
         __builtin_amdgcn_wave_barrier();
     }
-    if (a.stats) {
+    if (STATS) {
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
         atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
+        if (lane == 0) atomicAdd(&a.stats[6], 1ull);  // waves x deferred items (pass-2 work units)
     }
 }
 
+// ---- query ordering: Morton codes, slot-order gather, scatter back ----
 __global__ __launch_bounds__(kBlock) void k_query_morton(const double* __restrict__ q, size_t S, float lx, float ly, float lz,
                                                          float hx, float hy, float hz, uint32_t* __restrict__ keys,
                                                          uint32_t* __restrict__ vals) {
@@ -717,6 +669,65 @@ int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* ke
     return MSH_OK;
 }
 
+// slot i <- row perm[i] of the caller's (S, 3) array (two arrays at once when b != nullptr);
+// inv[perm[i]] = i
+__global__ __launch_bounds__(kBlock) void k_gather_rows(const double* __restrict__ a, const double* __restrict__ b,
+                                                        const uint32_t* __restrict__ perm, size_t S,
+                                                        double* __restrict__ as, double* __restrict__ bs,
+                                                        uint32_t* __restrict__ inv) {
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= S) return;
+    const size_t j = perm[i];
+    as[3 * i] = a[3 * j];
+    as[3 * i + 1] = a[3 * j + 1];
+    as[3 * i + 2] = a[3 * j + 2];
+    if (b) {
+        bs[3 * i] = b[3 * j];
+        bs[3 * i + 1] = b[3 * j + 1];
+        bs[3 * i + 2] = b[3 * j + 2];
+    }
+    if (inv) inv[j] = (uint32_t)i;
+}
+
+int gather_rows(const double* d_a, const double* d_b, const uint32_t* d_perm, size_t S, double* d_as, double* d_bs,
+                uint32_t* d_inv, hipStream_t s) {
+    if (S == 0) return MSH_OK;
+    TimedLaunch tl("gather", s);
+    k_gather_rows<<<(unsigned)((S + kBlock - 1) / kBlock), kBlock, 0, s>>>(d_a, d_b, d_perm, S, d_as, d_bs, d_inv);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+// row j of the outputs <- slot inv[j]: face / part / point (or distance) from the 32-B record, nw
+// extra doubles per row from w
+__global__ __launch_bounds__(kBlock) void k_unpermute(const QRes* __restrict__ res, const double* __restrict__ w, int nw,
+                                                      const uint32_t* __restrict__ inv, size_t S, SlotOut o) {
+    const size_t j = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= S) return;
+    const size_t i = inv[j];
+    const uint4 r0 = reinterpret_cast<const uint4*>(res + i)[0];
+    const double2 r1 = reinterpret_cast<const double2*>(res + i)[1];
+    const double x = __longlong_as_double((long long)(((unsigned long long)r0.w << 32) | r0.z));
+    if (o.face) o.face[j] = r0.x;
+    if (o.part) o.part[j] = r0.y;
+    if (o.dist) o.dist[j] = x;
+    if (o.pt) {
+        o.pt[3 * j] = x;
+        o.pt[3 * j + 1] = r1.x;
+        o.pt[3 * j + 2] = r1.y;
+    }
+    for (int k = 0; k < nw; ++k) o.w[(size_t)nw * j + k] = w[(size_t)nw * i + k];
+}
+
+int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32_t* d_inv, size_t S, const SlotOut& o,
+                      hipStream_t s) {
+    if (S == 0) return MSH_OK;
+    TimedLaunch tl("unpermute", s);
+    k_unpermute<<<(unsigned)((S + kBlock - 1) / kBlock), kBlock, 0, s>>>(d_res, d_w, nw, d_inv, S, o);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
 static int device_cus(int dev) {
     static std::mutex mu;
     static int cache[64] = {0};
@@ -732,7 +743,8 @@ static int device_cus(int dev) {
 
 constexpr unsigned kBudget = 2048;  // pass-1 node steps per lane before a query is deferred
 
-// Common launch: grid, counters, spill area, deferred list; pass 1 then pass 2.
+// Common launch: grid, counters, spill area, deferred list; pass 1 then pass 2 (both also in STATS
+// mode, so the instrumented counts describe the traversal that is timed).
 template <int MODE, bool STATS>
 static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* timer) {
     if (a.S == 0) return MSH_OK;
@@ -758,67 +770,114 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         MSH_TRY(ws.spill.reserve((size_t)std::max(nblk, nblk2) * kBlock * (size_t)a.spill_depth * sizeof(uint2)));
         a.spill = ws.spill.as<uint2>();
     }
-    a.budget = STATS ? 0xFFFFFFFFu : kBudget;
+    a.budget = kBudget;
     a.max_deferred = (unsigned)std::min<size_t>(a.S, (a.S / 16) + 65536);
     DevBuf& dbuf = ws.flags;
     MSH_TRY(dbuf.reserve((size_t)a.max_deferred * sizeof(DeferRec)));
     a.deferred = dbuf.as<DeferRec>();
     {
         TimedLaunch tl(timer, s);
-        k_knn<MODE, STATS><<<nblk, kBlock, 0, s>>>(a);
-        MSH_HIP(hipGetLastError());
-        if (!STATS) {
-            k_knn_coop<MODE><<<nblk2, kBlock, 0, s>>>(a);
+        {
+            TimedLaunch t1(STATS ? "knn_pass1_stats" : "knn_pass1", s);
+            k_knn<MODE, STATS><<<nblk, kBlock, 0, s>>>(a);
+            MSH_HIP(hipGetLastError());
+        }
+        {
+            TimedLaunch t2(STATS ? "knn_pass2_stats" : "knn_pass2", s);
+            k_knn_coop<MODE, STATS><<<nblk2, kBlock, 0, s>>>(a);
             MSH_HIP(hipGetLastError());
         }
     }
     return MSH_OK;
 }
 
-int launch_nearest(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S, uint32_t* d_face,
-                   uint32_t* d_part, double* d_pt, hipStream_t s) {
-    KnnArgs a{};
-    a.nodes = tree->d_nodes; a.leaves = tree->d_leaves; a.T = tree->T;
-    a.q = d_q; a.perm = d_perm; a.S = S;
-    a.out_face = d_face; a.out_part = d_part; a.out_pt = d_pt;
-    return launch_knn<0, false>(const_cast<msh_tree*>(tree), a, s, "nearest");
+// Slot-order plumbing shared by the point-query launchers: with a permutation the kernels write 32-B
+// records (plus nw weights) into the workspace and k_unpermute scatters them to the caller's arrays.
+template <int MODE, bool STATS>
+static int run_knn(msh_tree* tree, KnnArgs a, const QueryOrder& ord, const SlotOut& o, int nw, hipStream_t s,
+                   const char* timer) {
+    if (a.S == 0) return MSH_OK;
+    a.q = ord.q;
+    a.perm = ord.perm;
+    Workspace& ws = tree->ws;
+    if (ord.perm && !STATS) {
+        MSH_TRY(ws.res.reserve(a.S * sizeof(QRes)));
+        a.res = ws.res.as<QRes>();
+        if (nw) {
+            MSH_TRY(ws.res_w.reserve(a.S * (size_t)nw * sizeof(double)));
+            a.res_w = ws.res_w.as<double>();
+        }
+    } else {
+        a.out_face = o.face;
+        a.out_part = o.part;
+        a.out_pt = o.pt;
+        a.out_dist = o.dist;
+        a.out_w = o.w;
+    }
+    MSH_TRY((launch_knn<MODE, STATS>(tree, a, s, timer)));
+    if (ord.perm && !STATS) MSH_TRY(unpermute_results(a.res, a.res_w, nw, ord.inv, a.S, o, s));
+    return MSH_OK;
 }
 
-int launch_nearest_batch(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t n, size_t S,
-                         uint32_t* d_face, uint32_t* d_part, double* d_pt, hipStream_t s) {
+static KnnArgs tree_args(const msh_tree* tree, size_t S) {
     KnnArgs a{};
-    a.nodes = tree->d_nodes; a.leaves = tree->d_leaves; a.T = tree->T;
-    a.q = d_q; a.perm = d_perm; a.S = n;
-    a.out_face = d_face; a.out_part = d_part; a.out_pt = d_pt;
-    a.orgs = tree->d_orgs; a.qper = S; a.npm = tree->T - 1;
-    return launch_knn<0, false>(const_cast<msh_tree*>(tree), a, s, "nearest_batch");
+    a.nodes = tree->d_nodes;
+    a.leaves = tree->d_leaves;
+    a.T = tree->T;
+    a.S = S;
+    return a;
 }
 
-int launch_nearest_stats(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S,
-                         unsigned long long* d_counts, hipStream_t s) {
-    KnnArgs a{};
-    a.nodes = tree->d_nodes; a.leaves = tree->d_leaves; a.T = tree->T;
-    a.q = d_q; a.perm = d_perm; a.S = S;
+int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s) {
+    KnnArgs a = tree_args(tree, S);
+    SlotOut oo = o;
+    oo.dist = nullptr;
+    if (o.w) {
+        oo.part = nullptr;
+        return run_knn<3, false>(const_cast<msh_tree*>(tree), a, ord, oo, 3, s, "nearest");
+    }
+    return run_knn<0, false>(const_cast<msh_tree*>(tree), a, ord, oo, 0, s, "nearest");
+}
+
+int launch_nearest_batch(const msh_tree* tree, const QueryOrder& ord, size_t n, size_t S, const SlotOut& o,
+                         hipStream_t s) {
+    KnnArgs a = tree_args(tree, n);
+    a.orgs = tree->d_orgs;
+    a.qper = S;
+    a.npm = tree->T - 1;
+    SlotOut oo = o;
+    oo.dist = nullptr;
+    if (o.w) {
+        oo.part = nullptr;
+        return run_knn<3, false>(const_cast<msh_tree*>(tree), a, ord, oo, 3, s, "nearest_batch");
+    }
+    return run_knn<0, false>(const_cast<msh_tree*>(tree), a, ord, oo, 0, s, "nearest_batch");
+}
+
+int launch_nearest_stats(const msh_tree* tree, const QueryOrder& ord, size_t S, unsigned long long* d_counts,
+                         hipStream_t s) {
+    KnnArgs a = tree_args(tree, S);
     a.stats = d_counts;
-    return launch_knn<0, true>(const_cast<msh_tree*>(tree), a, s, "nearest_stats");
+    return run_knn<0, true>(const_cast<msh_tree*>(tree), a, ord, SlotOut{}, 0, s, "nearest_stats");
 }
 
-int launch_nnearest(const msh_tree* tree, const double* d_q, const double* d_n, const uint32_t* d_perm, size_t S,
-                    uint32_t* d_face, double* d_pt, hipStream_t s) {
-    KnnArgs a{};
-    a.nodes = tree->d_nodes; a.leaves = tree->d_leaves; a.T = tree->T;
-    a.q = d_q; a.n = d_n; a.perm = d_perm; a.S = S; a.eps = tree->eps;
-    a.out_face = d_face; a.out_pt = d_pt;
-    return launch_knn<1, false>(const_cast<msh_tree*>(tree), a, s, "nnearest");
+int launch_nnearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s) {
+    KnnArgs a = tree_args(tree, S);
+    a.n = ord.n;
+    a.eps = tree->eps;
+    SlotOut oo = o;
+    oo.part = nullptr;
+    oo.dist = nullptr;
+    oo.w = nullptr;
+    return run_knn<1, false>(const_cast<msh_tree*>(tree), a, ord, oo, 0, s, "nnearest");
 }
 
-int launch_points_nearest(const msh_tree* tree, const double* d_q, const uint32_t* d_perm, size_t S, uint32_t* d_idx,
-                          double* d_dist, hipStream_t s) {
-    KnnArgs a{};
-    a.nodes = tree->d_nodes; a.leaves = tree->d_leaves; a.T = tree->T;
-    a.q = d_q; a.perm = d_perm; a.S = S;
-    a.out_face = d_idx; a.out_dist = d_dist;
-    return launch_knn<2, false>(const_cast<msh_tree*>(tree), a, s, "points_nearest");
+int launch_points_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s) {
+    KnnArgs a = tree_args(tree, S);
+    SlotOut oo{};
+    oo.face = o.face;
+    oo.dist = o.dist;
+    return run_knn<2, false>(const_cast<msh_tree*>(tree), a, ord, oo, 0, s, "points_nearest");
 }
 
 }  // namespace msh

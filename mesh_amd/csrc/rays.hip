@@ -7,11 +7,21 @@
 // (p, p + v) and its predicates use (p + v) - p as direction; the ray is closed (t >= 0) and so are
 // the triangles.  A ray hits a triangle iff its supporting line passes the three edges with consistent
 // orientation (edge determinants flip sign exactly for the shared edge of two triangles, so a ray
-// through a shared edge is never lost) and the plane crossing parameter is >= 0; a ray lying in the
-// triangle's plane enters it at the clipped parameter.
+// through a shared edge is never lost) and the plane crossing parameter is >= 0.
+// Hit point: CGAL's construction for a proper hit, intersection(Plane_3(a, b, c), Line_3(p, p + v))
+// (Intersections_3 Plane_3/Line_3: num = A px + B py + C pz + D, den = A dx + B dy + C dz,
+// point = ((den px - num dx) / den, ...)), with the plane from plane_from_pointsC3.  A ray lying in the
+// triangle's plane (CGAL returns a Segment_3) enters it at the clipped parameter; the reference's
+// segment branch (:295-307) is not restated: it intersects the segment's line with the ray's line in
+// the xy projection, but the segment lies ON the ray's line, so its denominator is the 2-D cross
+// product of two parallel vectors (0 up to rounding) and its point is not finite.
 //
-// Execution shape: one lane per ray, persistent near-first traversal over the same 64-B nodes as K2;
-// box tests are slab tests on the fp32 (outward-padded) boxes evaluated in fp64 with a relative margin.
+// Execution shape: one lane per ray, persistent near-first traversal over the same 128-B nodes as K2
+// (AABB part); box tests are fp64 slab tests on the fp32 (outward-padded) boxes with the ray's inverse
+// direction precomputed once per ray and a relative margin.  alongnormal rays are Morton-sorted by
+// their source and gathered into slot order like K2's queries; visibility rays run vertex-major per
+// camera over a Morton order of the vertices (cached per tree), so neighbouring lanes cast
+// neighbouring, nearly parallel rays.
 #include <algorithm>
 
 #include "internal.h"
@@ -45,42 +55,70 @@ __device__ inline bool coplanar_ray_tri(const D3& p, const D3& d, const D3& a, c
     return true;
 }
 
-__device__ inline bool ray_tri(const D3& p, const D3& d, const D3& a, const D3& b, const D3& c, double& tout) {
+// 0: miss; 1: proper hit at parameter t; 2: coplanar hit entering at parameter t
+__device__ inline int ray_tri(const D3& p, const D3& d, const D3& a, const D3& b, const D3& c, double& tout) {
     const D3 u = vsub(a, p), v = vsub(b, p), w = vsub(c, p);
     const double s0 = det3(u, v, d), s1 = det3(v, w, d), s2 = det3(w, u, d);
     const bool pos = s0 >= 0.0 && s1 >= 0.0 && s2 >= 0.0;
     const bool neg = s0 <= 0.0 && s1 <= 0.0 && s2 <= 0.0;
-    if (!pos && !neg) return false;
+    if (!pos && !neg) return 0;
     const D3 n = vcross(vsub(b, a), vsub(c, a));
     const double num = vdot(n, u);
     const double den = vdot(n, d);
     if (den == 0.0 || (s0 == 0.0 && s1 == 0.0 && s2 == 0.0)) {
-        if (num != 0.0) return false;
-        return coplanar_ray_tri(p, d, a, b, c, tout);
+        if (num != 0.0) return 0;
+        return coplanar_ray_tri(p, d, a, b, c, tout) ? 2 : 0;
     }
     const double t = num / den;
-    if (t < 0.0) return false;
+    if (t < 0.0) return 0;
     tout = t;
+    return 1;
+}
+
+// CGAL intersection(Plane_3(a, b, c), Line_3(p, p + v)) with direction d = (p + v) - p; false if the
+// line is parallel to the plane in this arithmetic
+__device__ inline bool cgal_plane_line(const D3& p, const D3& d, const D3& a, const D3& b, const D3& c, D3& out) {
+    double A, B, C, D;
+    plane_of(a, b, c, A, B, C, D);
+    const double num = A * p.x + B * p.y + C * p.z + D;
+    const double den = A * d.x + B * d.y + C * d.z;
+    if (den == 0.0) return false;
+    out = D3{(den * p.x - num * d.x) / den, (den * p.y - num * d.y) / den, (den * p.z - num * d.z) / den};
     return true;
 }
 
 __device__ inline D3 ray_dir(const D3& p, const D3& v) { return vsub(vadd(p, v), p); }
 
-// Slab test of the line p + t d, t in [tlo, thi], against an fp32 box; tnear = entry parameter.
-__device__ inline bool slab(const D3& p, const D3& d, float lx, float ly, float lz, float hx, float hy, float hz, double tlo,
+// Line p + t d with precomputed 1/d (inf for d == 0, zero flagged in `flat`).
+struct RayF {
+    D3 p, inv;
+    bool fx, fy, fz;
+};
+__device__ inline RayF make_rayf(const D3& p, const D3& d) {
+    RayF r;
+    r.p = p;
+    r.fx = d.x == 0.0;
+    r.fy = d.y == 0.0;
+    r.fz = d.z == 0.0;
+    r.inv = D3{r.fx ? 0.0 : 1.0 / d.x, r.fy ? 0.0 : 1.0 / d.y, r.fz ? 0.0 : 1.0 / d.z};
+    return r;
+}
+
+// Slab test of the line, t in [tlo, thi], against an fp32 box; tnear = entry parameter.
+__device__ inline bool slab(const RayF& r, float lx, float ly, float lz, float hx, float hy, float hz, double tlo,
                             double thi, double& tnear) {
-    const double po[3] = {p.x, p.y, p.z}, dd[3] = {d.x, d.y, d.z};
+    const double po[3] = {r.p.x, r.p.y, r.p.z}, iv[3] = {r.inv.x, r.inv.y, r.inv.z};
+    const bool fl[3] = {r.fx, r.fy, r.fz};
     const double lo[3] = {(double)lx, (double)ly, (double)lz}, hi[3] = {(double)hx, (double)hy, (double)hz};
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        if (dd[k] == 0.0) {
+        if (fl[k]) {
             if (po[k] < lo[k] || po[k] > hi[k]) return false;
         } else {
-            const double inv = 1.0 / dd[k];
-            double t1 = (lo[k] - po[k]) * inv, t2 = (hi[k] - po[k]) * inv;
-            if (t1 > t2) { const double x = t1; t1 = t2; t2 = x; }
-            tlo = fmax(tlo, t1);
-            thi = fmin(thi, t2);
+            double t1 = (lo[k] - po[k]) * iv[k], t2 = (hi[k] - po[k]) * iv[k];
+            const double a = fmin(t1, t2), b = fmax(t1, t2);
+            tlo = fmax(tlo, a);
+            thi = fmin(thi, b);
         }
     }
     tnear = tlo;
@@ -148,7 +186,8 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
 struct AlongPol {
     const TriRec* __restrict__ tris;
     D3 p, dp, dm;
-    D3 pr;  // p relative to the tree origin (node bounds are origin-relative)
+    RayF rf;      // the line through p (relative to the tree origin: node bounds are origin-relative)
+    D3 pr;
     double best;  // distance
     uint32_t best_face;
     D3 best_pt;
@@ -157,7 +196,7 @@ struct AlongPol {
         key = box_d2(pr, lx, ly, lz, hx, hy, hz);
         if (key > lim2()) return false;
         double tn;
-        return slab(pr, dp, lx, ly, lz, hx, hy, hz, -INFINITY, INFINITY, tn);
+        return slab(rf, lx, ly, lz, hx, hy, hz, -INFINITY, INFINITY, tn);
     }
     __device__ bool keep(double key) const { return key <= lim2(); }
     __device__ bool done() const { return false; }
@@ -169,8 +208,10 @@ struct AlongPol {
         for (int k = 0; k < 2; ++k) {
             const D3& d = k == 0 ? dp : dm;
             double t;
-            if (!ray_tri(p, d, a, b, c, t)) continue;
-            const D3 hit = vadd(p, vscale(t, d));
+            const int kind = ray_tri(p, d, a, b, c, t);
+            if (!kind) continue;
+            D3 hit;
+            if (kind == 2 || !cgal_plane_line(p, d, a, b, c, hit)) hit = vadd(p, vscale(t, d));
             const double dist = sqrt(sqdist(hit, p));
             if (dist < best || (dist == best && face < best_face)) {
                 best = dist;
@@ -185,10 +226,10 @@ struct AlongPol {
 struct AnyPol {
     const TriRec* __restrict__ tris;
     D3 src, d;
-    D3 sr;  // src relative to the tree origin
+    RayF rf;  // src relative to the tree origin
     bool hit;
     __device__ bool box(float lx, float ly, float lz, float hx, float hy, float hz, double& key) const {
-        return slab(sr, d, lx, ly, lz, hx, hy, hz, 0.0, INFINITY, key);
+        return slab(rf, lx, ly, lz, hx, hy, hz, 0.0, INFINITY, key);
     }
     __device__ bool keep(double) const { return !hit; }
     __device__ bool done() const { return hit; }
@@ -205,17 +246,19 @@ struct RayArgs {
     const BNode* nodes;
     const TriRec* tris;
     size_t T;
-    // alongnormal
+    // alongnormal (slot order when res != nullptr)
     const double* p;
     const double* n;
-    const uint32_t* perm;
     size_t S;
+    QRes* res;
+    double* res_w;
     double* out_dist;
     uint32_t* out_face;
     double* out_pt;
-    // visibility
+    // visibility: cameras x vertices [v0, v0 + nv); output row stride nv
     const double* v;
-    size_t P;
+    const uint32_t* vorder;  // Morton order of the vertices (nullptr: identity)
+    size_t P, v0, nv;
     const double* cams;
     const double* normals;
     const double* sensors;
@@ -243,6 +286,8 @@ __device__ inline unsigned dequeue_tile_r(unsigned* counters, unsigned ntiles, u
     return ntiles;
 }
 
+__device__ inline bool finite_d3(const D3& x) { return isfinite(x.x) && isfinite(x.y) && isfinite(x.z); }
+
 template <int MODE>  // 0 alongnormal, 1 visibility
 __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
@@ -250,39 +295,47 @@ __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
     uint2* lds = stk + tid;
     uint2* spill = a.spill ? a.spill + ((size_t)blockIdx.x * kBlock + tid) * (size_t)a.spill_depth : nullptr;
     const unsigned group = blockIdx.x & 7u;
-    const size_t total = MODE == 0 ? a.S : a.S;  // S = number of rays
+    const D3 org = D3{a.org[0], a.org[1], a.org[2]};
     for (;;) {
         unsigned tile = 0;
         if (lane == 0) tile = dequeue_tile_r(a.counters, a.ntiles, group);
         tile = __shfl(tile, 0);
         if (tile >= a.ntiles) break;
         const size_t i = (size_t)tile * 64 + lane;
-        if (i >= total) continue;
+        if (i >= a.S) continue;
         if (MODE == 0) {
-            const size_t qi = a.perm ? (size_t)a.perm[i] : i;
-            const D3 p = D3{a.p[3 * qi], a.p[3 * qi + 1], a.p[3 * qi + 2]};
-            const D3 n = D3{a.n[3 * qi], a.n[3 * qi + 1], a.n[3 * qi + 2]};
-            AlongPol pol{a.tris, p, ray_dir(p, n), ray_dir(p, D3{-n.x, -n.y, -n.z}),
-                         D3{p.x - a.org[0], p.y - a.org[1], p.z - a.org[2]}, INFINITY, 0xFFFFFFFFu,
+            const D3 p = D3{a.p[3 * i], a.p[3 * i + 1], a.p[3 * i + 2]};
+            const D3 n = D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]};
+            const D3 dp = ray_dir(p, n), pr = vsub(p, org);
+            AlongPol pol{a.tris, p, dp, ray_dir(p, D3{-n.x, -n.y, -n.z}), make_rayf(pr, dp), pr, INFINITY, MSH_NO_FACE,
                          D3{NAN, NAN, NAN}};
-            traverse_rays<AlongPol>(a.nodes, a.T, pol, lds, spill);
-            a.out_dist[qi] = pol.best == INFINITY ? 1e100 : pol.best;
-            a.out_face[qi] = pol.best_face;
-            a.out_pt[3 * qi] = pol.best_pt.x;
-            a.out_pt[3 * qi + 1] = pol.best_pt.y;
-            a.out_pt[3 * qi + 2] = pol.best_pt.z;
+            if (finite_d3(p) && finite_d3(dp)) traverse_rays<AlongPol>(a.nodes, a.T, pol, lds, spill);
+            const double dist = pol.best == INFINITY ? 1e100 : pol.best;
+            if (a.res) {
+                store_qres(a.res + i, pol.best_face, 0u, pol.best_pt.x, pol.best_pt.y, pol.best_pt.z);
+                a.res_w[i] = dist;
+            } else {
+                a.out_dist[i] = dist;
+                a.out_face[i] = pol.best_face;
+                a.out_pt[3 * i] = pol.best_pt.x;
+                a.out_pt[3 * i + 1] = pol.best_pt.y;
+                a.out_pt[3 * i + 2] = pol.best_pt.z;
+            }
         } else {
-            const size_t ic = i / a.P, iv = i - ic * a.P;
+            const size_t ic = i / a.nv, k = i - ic * a.nv;
+            const size_t iv = a.vorder ? (size_t)a.vorder[k] : a.v0 + k;  // vertex (global index)
+            const size_t o = ic * a.nv + (iv - a.v0);                        // output element
             const D3 cam = D3{a.cams[3 * ic], a.cams[3 * ic + 1], a.cams[3 * ic + 2]};
             const D3 vv = D3{a.v[3 * iv], a.v[3 * iv + 1], a.v[3 * iv + 2]};
             D3 dir = vsub(cam, vv);
             const double len = sqrt(vdot(dir, dir));
             dir = D3{dir.x / len, dir.y / len, dir.z / len};
             const D3 src = vadd(vv, vscale(a.min_dist, dir));
-            AnyPol pol{a.tris, src, ray_dir(src, dir), D3{src.x - a.org[0], src.y - a.org[1], src.z - a.org[2]}, false};
-            traverse_rays<AnyPol>(a.nodes, a.T, pol, lds, spill);
+            const D3 d = ray_dir(src, dir);
+            AnyPol pol{a.tris, src, d, make_rayf(vsub(src, org), d), false};
+            if (finite_d3(src) && finite_d3(d)) traverse_rays<AnyPol>(a.nodes, a.T, pol, lds, spill);
             const uint32_t reach = pol.hit ? 0u : 1u;
-            a.ndc[i] = a.normals ? vdot(D3{a.normals[3 * iv], a.normals[3 * iv + 1], a.normals[3 * iv + 2]}, dir) : 0.0;
+            a.ndc[o] = a.normals ? vdot(D3{a.normals[3 * iv], a.normals[3 * iv + 1], a.normals[3 * iv + 2]}, dir) : 0.0;
             uint32_t out = reach;
             if (a.sensors) {
                 const double* s = a.sensors + 9 * ic;
@@ -296,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
                     out = 0u;
                 }
             }
-            a.vis[i] = out;
+            a.vis[o] = out;
         }
     }
 }
@@ -318,7 +371,7 @@ static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, c
     for (int k = 0; k < 3; ++k) a.org[k] = tree->origin[k];
     a.ntiles = (unsigned)((nrays + 63) / 64);
     const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, (unsigned)device_cus_r(tree->device) * 5u);
-    MSH_TRY(tree->ws.counters.reserve(8 * 32 * sizeof(unsigned)));
+    MSH_TRY(tree->ws.counters.reserve(9 * 32 * sizeof(unsigned)));
     a.counters = tree->ws.counters.as<unsigned>();
     MSH_HIP(hipMemsetAsync(a.counters, 0, 8 * 32 * sizeof(unsigned), s));
     a.spill = nullptr;
@@ -334,23 +387,84 @@ static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, c
     return MSH_OK;
 }
 
-int launch_alongnormal(const msh_tree* tree, const double* d_p, const double* d_n, const uint32_t* d_perm, size_t S,
-                       double* d_dist, uint32_t* d_face, double* d_pt, hipStream_t s) {
+int launch_alongnormal(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s) {
+    msh_tree* t = const_cast<msh_tree*>(tree);
     RayArgs a{};
     a.nodes = tree->d_nodes; a.tris = static_cast<const TriRec*>(tree->d_leaves); a.T = tree->T;
-    a.p = d_p; a.n = d_n; a.perm = d_perm;
-    a.out_dist = d_dist; a.out_face = d_face; a.out_pt = d_pt;
-    return launch_rays<0>(const_cast<msh_tree*>(tree), a, S, s, "alongnormal");
+    a.p = ord.q; a.n = ord.n;
+    if (ord.perm) {
+        MSH_TRY(t->ws.res.reserve(S * sizeof(QRes)));
+        MSH_TRY(t->ws.res_w.reserve(S * sizeof(double)));
+        a.res = t->ws.res.as<QRes>();
+        a.res_w = t->ws.res_w.as<double>();
+    } else {
+        a.out_dist = o.w; a.out_face = o.face; a.out_pt = o.pt;
+    }
+    MSH_TRY(launch_rays<0>(t, a, S, s, "alongnormal"));
+    if (ord.perm) {
+        SlotOut oo{};
+        oo.face = o.face;
+        oo.pt = o.pt;
+        oo.w = o.w;
+        MSH_TRY(unpermute_results(a.res, a.res_w, 1, ord.inv, S, oo, s));
+    }
+    return MSH_OK;
+}
+
+// Morton order of the main-mesh vertices in the scene box (cached on the handle: visibility sources)
+__global__ __launch_bounds__(kBlock) void k_vertex_morton(const double* __restrict__ v, size_t P, float lx, float ly,
+                                                          float lz, float hx, float hy, float hz,
+                                                          uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= P) return;
+    const float e[3] = {hx - lx, hy - ly, hz - lz}, l[3] = {lx, ly, lz};
+    uint32_t c[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        float x = e[k] > 0.f ? ((float)v[3 * i + k] - l[k]) / e[k] : 0.5f;
+        x = fminf(fmaxf(x * 1024.f, 0.f), 1023.f);
+        uint32_t b = (uint32_t)x;
+        b = (b * 0x00010001u) & 0xFF0000FFu;
+        b = (b * 0x00000101u) & 0x0F00F00Fu;
+        b = (b * 0x00000011u) & 0xC30C30C3u;
+        b = (b * 0x00000005u) & 0x49249249u;
+        c[k] = b;
+    }
+    keys[i] = (c[0] << 2) | (c[1] << 1) | c[2];
+    vals[i] = (uint32_t)i;
+}
+
+static int vertex_order(msh_tree* t, hipStream_t s) {
+    if (t->d_vorder || t->P < 4096) return MSH_OK;
+    Workspace& ws = t->ws;
+    const size_t P = t->P;
+    MSH_TRY(ws.keys.reserve(P * sizeof(uint32_t)));
+    MSH_TRY(ws.keys_alt.reserve(P * sizeof(uint32_t)));
+    MSH_TRY(ws.vals_alt.reserve(P * sizeof(uint32_t)));
+    MSH_HIP(hipMalloc(&t->d_vorder, P * sizeof(uint32_t)));
+    k_vertex_morton<<<(unsigned)((P + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+        t->d_v, P, t->scene_lo[0], t->scene_lo[1], t->scene_lo[2], t->scene_hi[0], t->scene_hi[1], t->scene_hi[2],
+        ws.keys.as<uint32_t>(), t->d_vorder);
+    MSH_HIP(hipGetLastError());
+    return radix_sort_pairs(ws.keys.as<uint32_t>(), t->d_vorder, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(),
+                            P, 30, ws, s);
 }
 
 int launch_visibility(const msh_tree* tree, const double* d_cams, size_t C, const double* d_normals,
-                      const double* d_sensors, double min_dist, uint32_t* d_vis, double* d_ndc, hipStream_t s) {
+                      const double* d_sensors, double min_dist, size_t v0, size_t nv, uint32_t* d_vis, double* d_ndc,
+                      hipStream_t s) {
+    msh_tree* t = const_cast<msh_tree*>(tree);
     RayArgs a{};
     a.nodes = tree->d_nodes; a.tris = static_cast<const TriRec*>(tree->d_leaves); a.T = tree->T;
-    a.v = tree->d_v; a.P = tree->P; a.cams = d_cams; a.normals = d_normals; a.sensors = d_sensors;
+    a.v = tree->d_v; a.P = tree->P; a.v0 = v0; a.nv = nv;
+    a.cams = d_cams; a.normals = d_normals; a.sensors = d_sensors;
     a.min_dist = min_dist; a.vis = d_vis; a.ndc = d_ndc;
-    if (tree->P == 0) return MSH_OK;
-    return launch_rays<1>(const_cast<msh_tree*>(tree), a, C * tree->P, s, "visibility");
+    if (nv == 0 || C == 0) return MSH_OK;
+    if (v0 == 0 && nv == tree->P) {  // whole mesh: Morton-ordered sources
+        MSH_TRY(vertex_order(t, s));
+        a.vorder = t->d_vorder;
+    }
+    return launch_rays<1>(t, a, C * nv, s, "visibility");
 }
 
 }  // namespace msh

@@ -81,3 +81,59 @@ def nearest_device(tree, q, face, part, pt, stream=None):
 
 def as_numpy_u32(t):
     return t.cpu().numpy().view(np.uint32)
+
+
+def _stream(t, stream):
+    import torch
+    return torch.cuda.current_stream(t.device).cuda_stream if stream is None else stream
+
+
+def nearest_bary_device(tree, q, face, pt, w, stream=None):
+    """Device-resident closest point + barycentric weights (msh_tree_nearest_bary_device): q (S,3) f64,
+    face (S,) int32 viewed as uint32, pt (S,3) f64, w (S,3) f64."""
+    _native.check(_native.lib().msh_tree_nearest_bary_device(tree.ptr, q.data_ptr(), q.shape[0], face.data_ptr(),
+                                                             pt.data_ptr(), w.data_ptr(), _stream(q, stream)))
+
+
+def alongnormal_device(tree, p, n, dist, face, pt, stream=None):
+    """Device-resident nearest_alongnormal (msh_tree_nearest_alongnormal_device) on torch tensors:
+    p, n (S,3) f64 -> dist (S,) f64, face (S,) int32 viewed as uint32, pt (S,3) f64."""
+    _native.check(_native.lib().msh_tree_nearest_alongnormal_device(
+        tree.ptr, p.data_ptr(), n.data_ptr(), p.shape[0], dist.data_ptr(), face.data_ptr(), pt.data_ptr(),
+        _stream(p, stream)))
+
+
+def visibility_device(tree, cams, vis, ndc, normals=None, sensors=None, min_dist=1e-3, v_begin=0, v_count=None,
+                      stream=None):
+    """Device-resident visibility of main-mesh vertices [v_begin, v_begin + v_count) from every camera
+    (msh_visibility_device): cams (C,3) f64, normals (P,3) f64 (global vertex index) or None, sensors
+    (C,9) or None -> vis (C, v_count) int32 viewed as uint32, ndc (C, v_count) f64."""
+    if v_count is None:
+        v_count = int(tree.info().n_points) - v_begin
+    _native.check(_native.lib().msh_visibility_device(
+        tree.ptr, cams.data_ptr(), cams.shape[0], normals.data_ptr() if normals is not None else None,
+        sensors.data_ptr() if sensors is not None else None, float(min_dist), int(v_begin), int(v_count),
+        vis.data_ptr(), ndc.data_ptr(), _stream(cams, stream)))
+
+
+def visibility_sharded(tree, cams, normals=None, sensors=None, min_dist=1e-3, group=None):
+    """C5's multi-GPU split of visibility_compute (visibility.cpp:136-173 loops cameras x vertices):
+    every rank casts the rays of its contiguous vertex range for all cameras, then the (C, P) result is
+    assembled on every rank by one all_gather per output (vertex-range slabs, padded)."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    P = int(tree.info().n_points)
+    C = cams.shape[0]
+    v0, v1 = shard_range(P, rank, world)
+    vis = torch.empty((C, v1 - v0), dtype=torch.int32, device=cams.device)
+    ndc = torch.empty((C, v1 - v0), dtype=torch.float64, device=cams.device)
+    visibility_device(tree, cams, vis, ndc, normals, sensors, min_dist, v0, v1 - v0)
+    if world == 1:
+        return vis, ndc
+    # gather along the vertex axis: transpose so the sharded axis is first
+    vis_all = gather_results(vis.t().contiguous(), P, group).t().contiguous()
+    ndc_all = gather_results(ndc.t().contiguous(), P, group).t().contiguous()
+    return vis_all, ndc_all

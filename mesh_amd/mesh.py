@@ -4,6 +4,7 @@ mirrored; I/O, topology, texture and viewing are out of scope.
 """
 import numpy as np
 
+from . import _native as N
 from . import search
 
 
@@ -18,15 +19,16 @@ class Mesh(object):
 
     # ---- geometry helpers used by the callers (mesh.py:208-222) ----
     def estimate_vertex_normals(self):
-        """Area-weighted vertex normals (TriNormalsScaled summed per vertex, then normalised)."""
-        tri = self.v[self.f.astype(np.int64)]
-        fn = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
-        vn = np.zeros_like(self.v)
-        for k in range(3):
-            np.add.at(vn, self.f[:, k].astype(np.int64), fn)
-        norms = np.sqrt(np.sum(vn ** 2, axis=1))
-        norms[norms == 0] = 1.0
-        return vn / norms[:, None]
+        """Area-weighted vertex normals on the GPU (mesh.py:208-216): every vertex sums the scaled
+        normals of its faces in ascending face order (the reference's sparse face->vertex product over
+        TriNormalsScaled), then divides by the row norm (0 -> 1)."""
+        v = np.ascontiguousarray(self.v, dtype=np.float64).reshape(-1, 3)
+        f = np.ascontiguousarray(self.f, dtype=np.uint32).reshape(-1, 3)
+        if f.size and int(f.max()) >= v.shape[0]:
+            raise ValueError("face index out of range")
+        vn = np.empty_like(v)
+        N.check(N.lib().msh_vertex_normals(N.dptr(v), v.shape[0], N.uptr(f), f.shape[0], N.dptr(vn)))
+        return vn
 
     def barycentric_coordinates_for_points(self, points, face_indices):
         """(vertex indices, barycentric coordinates of the projection) — mesh.py:218-222."""

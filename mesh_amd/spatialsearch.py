@@ -62,6 +62,30 @@ def aabbtree_nearest(tree, q):
     return face, part, pt
 
 
+def aabbtree_nearest_barycentric(tree, q):
+    """(face (S,) uint32, point (S,3) float64, weights (S,3) float64) of the closest point.
+
+    One launch replaces ``aabbtree_nearest`` followed by ``Mesh.barycentric_coordinates_for_points``
+    (mesh.py:218-222; Heidrich's projection, geometry/barycentric_coordinates_of_projection.py:9-49), the
+    pair landmarks.py:58-63 calls: the weights are computed in the traversal kernel from the winning
+    triangle and refer to its vertices ``f[face]``.
+    """
+    tree = _tree(tree, "aabbtree_nearest_barycentric")
+    if not isinstance(q, np.ndarray):
+        raise TypeError("aabbtree_nearest_barycentric() argument 2 must be numpy.ndarray")
+    if q.ndim != 2 or q.shape[1] != 3:
+        raise ValueError("Input must be Nx3")
+    if tree.kind != "triangles":
+        raise TypeError("aabbtree_nearest_barycentric: handle is not a triangle tree")
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    S = q.shape[0]
+    face = np.empty(S, dtype=np.uint32)
+    pt = np.empty((S, 3), dtype=np.float64)
+    w = np.empty((S, 3), dtype=np.float64)
+    N.check(N.lib().msh_tree_nearest_bary(tree.ptr, N.dptr(q), S, N.uptr(face), N.dptr(pt), N.dptr(w)))
+    return face, pt, w
+
+
 def aabbtree_nearest_alongnormal(tree, p, n):
     """(dist (S,) float64, face (S,) uint32, point (S,3) float64): spatialsearchmodule.cpp:222-323."""
     tree = _tree(tree, "aabbtree_nearest_alongnormal")

@@ -494,22 +494,43 @@ inline bool coplanar_ray_tri(const P3& p, const P3& d, const P3& a, const P3& b,
     return true;
 }
 
-inline bool ray_tri(const P3& p, const P3& d, const P3& a, const P3& b, const P3& c, double& tout) {
+// 0: miss; 1: proper hit at parameter t; 2: coplanar hit (CGAL returns a Segment_3) entering at t
+inline int ray_tri_kind(const P3& p, const P3& d, const P3& a, const P3& b, const P3& c, double& tout) {
     const P3 u = vec(p, a), v = vec(p, b), w = vec(p, c);
     const double s0 = det3(u, v, d), s1 = det3(v, w, d), s2 = det3(w, u, d);
     const bool pos = s0 >= 0.0 && s1 >= 0.0 && s2 >= 0.0;
     const bool neg = s0 <= 0.0 && s1 <= 0.0 && s2 <= 0.0;
-    if (!pos && !neg) return false;
+    if (!pos && !neg) return 0;
     const P3 n = cross(vec(a, b), vec(a, c));
     const double num = dot(n, u);
     const double den = dot(n, d);
     if (den == 0.0 || (s0 == 0.0 && s1 == 0.0 && s2 == 0.0)) {
-        if (num != 0.0) return false;  // parallel, off-plane
-        return coplanar_ray_tri(p, d, a, b, c, tout);
+        if (num != 0.0) return 0;  // parallel, off-plane
+        return coplanar_ray_tri(p, d, a, b, c, tout) ? 2 : 0;
     }
     const double t = num / den;
-    if (t < 0.0) return false;
+    if (t < 0.0) return 0;
     tout = t;
+    return 1;
+}
+inline bool ray_tri(const P3& p, const P3& d, const P3& a, const P3& b, const P3& c, double& tout) {
+    return ray_tri_kind(p, d, a, b, c, tout) != 0;
+}
+
+// The point CGAL 4.7 returns for a proper Triangle_3 / Ray_3 hit: t3r3_intersection_aux intersects
+// r.supporting_line() = Line_3(p, p + v) (point p, direction d = (p + v) - p) with
+// t.supporting_plane() = Plane_3(a, b, c) (plane_from_pointsC3), Intersections_3 Plane_3/Line_3:
+//   num = A px + B py + C pz + D,  den = A dx + B dy + C dz,
+//   point = Point_3(den px - num dx, den py - num dy, den pz - num dz, den)  (homogeneous; /den).
+// Call sites: spatialsearchmodule.cpp:277-278 (all_intersections), visibility.cpp:93 (do_intersect).
+// false when den == 0 in this arithmetic (CGAL then returns the Line_3 itself, i.e. no Point_3).
+inline bool cgal_plane_line(const P3& p, const P3& d, const P3& a, const P3& b, const P3& c, P3& out) {
+    double A, B, C, D;
+    plane_of(a, b, c, A, B, C, D);
+    const double num = A * p.x + B * p.y + C * p.z + D;
+    const double den = A * d.x + B * d.y + C * d.z;
+    if (den == 0.0) return false;
+    out = P3{(den * p.x - num * d.x) / den, (den * p.y - num * d.y) / den, (den * p.z - num * d.z) / den};
     return true;
 }
 
@@ -774,8 +795,14 @@ void ora_brute_alongnormal(const double* v, size_t P, const uint32_t* f, size_t 
         for (size_t t = 0; t < T; ++t) {
             for (int k = 0; k < 2; ++k) {
                 double tt;
-                if (!ray_tri(pp, dirs[k], m.tri[3 * t], m.tri[3 * t + 1], m.tri[3 * t + 2], tt)) continue;
-                P3 hit = add(pp, scale(tt, dirs[k]));
+                const P3 &ta = m.tri[3 * t], &tb = m.tri[3 * t + 1], &tc = m.tri[3 * t + 2];
+                const int kind = ray_tri_kind(pp, dirs[k], ta, tb, tc, tt);
+                if (!kind) continue;
+                // proper hit: CGAL's plane/line construction; coplanar (Segment_3): entry point of the
+                // clipped ray (the reference's xy formula at :295-307 divides by the 2-D cross product of
+                // two parallel vectors and is not restated)
+                P3 hit;
+                if (kind == 2 || !cgal_plane_line(pp, dirs[k], ta, tb, tc, hit)) hit = add(pp, scale(tt, dirs[k]));
                 double d = std::sqrt(sqd(hit, pp));
                 if (d < best || (d == best && (uint32_t)t < bf)) { best = d; bf = (uint32_t)t; bp = hit; }
             }

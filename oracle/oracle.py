@@ -160,9 +160,16 @@ def brute_alongnormal(v, f, p, n, threads=0):
     return dist, face, pt
 
 
-def brute_visibility(v, f, cams, n=None, sensors=None, extra_v=None, extra_f=None, min_dist=1e-3, threads=0):
+def brute_visibility(v, f, cams, n=None, sensors=None, extra_v=None, extra_f=None, min_dist=1e-3, threads=0,
+                     src_idx=None):
+    """(vis (C,P'), ndc (C,P')); with src_idx only the rays from vertices v[src_idx] are cast (against
+    every triangle), n is then indexed like v."""
     v, f, cams = _d(v), _u(f), _d(cams).reshape(-1, 3)
     tris = v[f.astype(np.int64)].reshape(-1, 9)
+    if src_idx is not None:
+        v = _d(v[np.asarray(src_idx)])
+        if n is not None:
+            n = np.asarray(n)[np.asarray(src_idx)]
     if extra_v is not None and extra_f is not None:
         ev, ef = _d(extra_v), _u(extra_f)
         tris = np.vstack([tris, ev[ef.astype(np.int64)].reshape(-1, 9)])
@@ -202,3 +209,75 @@ def brute_vertex_nn(v, q, threads=0):
     dist = np.empty(S)
     lib().ora_brute_vertex_nn(_pd(v), v.shape[0], _pd(q), S, _pu(idx), _pd(dist), int(threads))
     return idx, dist
+
+
+# ---- geometry feeding the path (numpy/scipy restatements, operation for operation) ----------------
+def tri_normals_scaled(v, f):
+    """TriNormalsScaled (geometry/tri_normals.py:23-24, :40-44 _edges_for): cross(v[f1]-v[f0], v[f2]-v[f0])
+    with numpy's cross (geometry/cross_product.py delegates to the same component formulas)."""
+    v = np.asarray(v, dtype=np.float64).reshape(-1, 3)
+    f = np.asarray(f).astype(np.int64)
+    e1 = v[f[:, 1]] - v[f[:, 0]]
+    e2 = v[f[:, 2]] - v[f[:, 0]]
+    return np.cross(e1, e2)
+
+
+def estimate_vertex_normals(v, f):
+    """Mesh.estimate_vertex_normals (mesh.py:208-216) with faces_by_vertex(as_sparse_matrix=True)
+    (mesh.py:202-205): CSR (P,T) incidence times the scaled face normals, row norms via ``** 0.5``,
+    zero norms -> 1."""
+    import scipy.sparse as sp
+    v = np.asarray(v, dtype=np.float64).reshape(-1, 3)
+    f = np.asarray(f, dtype=np.uint32).reshape(-1, 3)
+    fn = tri_normals_scaled(v, f).reshape(-1, 3)
+    row = f.flatten()
+    col = np.array([range(f.shape[0])] * 3).T.flatten()
+    data = np.ones(len(col))
+    ftov = sp.csr_matrix((data, (row, col)), shape=(v.shape[0], f.shape[0]))
+    nsn = ftov * fn
+    norms = (np.sum(nsn ** 2.0, axis=1) ** 0.5).T
+    norms[norms == 0] = 1.0
+    return (nsn.T / norms).T
+
+
+def vert_normals(v, f):
+    """geometry/vert_normals.py:19-35 VertNormals (CSC (3P,3T) incidence, NormalizedNx3); the reference's
+    tests/test_geometry.py:61-68 requires estimate_vertex_normals to match it within 1e-15."""
+    import scipy.sparse as sp
+    v = np.asarray(v, dtype=np.float64).reshape(-1, 3)
+    f = np.asarray(f, dtype=np.uint32).reshape(-1, 3)
+    IS = f.flatten().astype(np.int64)
+    JS = np.array([range(f.shape[0])] * 3).T.flatten()
+    data = np.ones(len(JS))
+    IS = np.concatenate((IS * 3, IS * 3 + 1, IS * 3 + 2))
+    JS = np.concatenate((JS * 3, JS * 3 + 1, JS * 3 + 2))
+    data = np.concatenate((data, data, data))
+    m = sp.csc_matrix((data, (IS, JS)), shape=(v.size, f.size))
+    x = m.dot(tri_normals_scaled(v, f).flatten().reshape(-1, 1)).flatten()
+    x = x.reshape(-1, 3)
+    ss = np.sum(x ** 2, axis=1)
+    ss[ss == 0] = 1
+    return x / np.sqrt(ss).reshape(-1, 1)
+
+
+def barycentric_coordinates_of_projection(p, q, u, v):
+    """geometry/barycentric_coordinates_of_projection.py:9-49 (Heidrich, JGT 2005), same operation order."""
+    p, q, u, v = (np.asarray(a, dtype=np.float64).T for a in (p, q, u, v))
+    n = np.cross(u, v, axis=0)
+    s = np.sum(n * n, axis=0)
+    if np.isscalar(s):
+        s = s if s else np.spacing(1)
+    else:
+        s[s == 0] = np.spacing(1)
+    one_over_4a2 = 1.0 / s
+    w = p - q
+    b2 = np.sum(np.cross(u, w, axis=0) * n, axis=0) * one_over_4a2
+    b1 = np.sum(np.cross(w, v, axis=0) * n, axis=0) * one_over_4a2
+    return np.vstack((1 - b1 - b2, b1, b2)).T
+
+
+def barycentric_coordinates_for_points(v, f, points, face_indices):
+    """Mesh.barycentric_coordinates_for_points (mesh.py:218-222)."""
+    vi = np.asarray(f)[np.asarray(face_indices).flatten(), :]
+    a, b, c = v[vi[:, 0]], v[vi[:, 1]], v[vi[:, 2]]
+    return vi, barycentric_coordinates_of_projection(points, a, b - a, c - a)

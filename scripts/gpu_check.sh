@@ -15,7 +15,7 @@ STAGES=${STAGES:-"smoke pytest bench prof"}
 for s in $STAGES; do
   case $s in
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; ok smoke $? ;;
-    pytest) timeout -k 10 1200 python -m pytest tests -q -m gpu -x -p no:cacheprovider > gpurun_out/pytest_gpu.log 2>&1; ok pytest $? ;;
+    pytest) timeout -k 10 1200 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; ok pytest $? ;;
     bench_small) timeout -k 10 600 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_small.log 2>&1; ok bench_small $? ;;
     variants)  # tuning sweep: every build/variants/*.so through the 10M-query bench (env MESH_AMD_LIB)
       for so in build/variants/*.so; do

@@ -1,0 +1,118 @@
+"""Summarise the rocprofv3 passes of scripts/profile_pmc.sh into profiles/.
+
+Reads gpurun_out/pmc/<pass>/**/*counter_collection.csv (one --pmc pass per counter group) and
+*kernel_stats.csv (the --stats pass), and writes:
+  profiles/pmc_traffic.json  — what bench.py reads for roofline.traffic: HBM bytes per launch of the
+                               closest-point traversal (k_knn<0,false> pass 1 + k_knn_coop<0,false> pass 2),
+                               corrected as MI355X_MICROARCH.md §HBM prescribes (gfx950 FETCH_SIZE counts a
+                               coalesced 128-B request as 64 B: bytes = 2 * FETCH_SIZE + WRITE_SIZE, KB units),
+                               L2 hit rate, and per-kernel counter means;
+  profiles/<tag>_pmc.json    — every counter mean per kernel (all passes), for the record.
+
+    python scripts/pmc_summary.py --tag r02_c3_100M --code $(git rev-parse --short HEAD) [--queries 1e8]
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TRAVERSAL = ("msh::k_knn<0, false>", "msh::k_knn_coop<0, false>")
+
+
+def short(name):
+    m = re.search(r"(msh::[A-Za-z_0-9]+(<[^>]*>)?)", name)
+    return m.group(1) if m else name
+
+
+def counters(pmc_dir):
+    """{kernel: {counter: mean value per dispatch}} over every *counter_collection.csv under pmc_dir."""
+    vals = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))  # kernel -> counter -> dispatch -> sum
+    vgpr = {}
+    for path in glob.glob(os.path.join(pmc_dir, "**", "*counter_collection.csv"), recursive=True):
+        with open(path) as fh:
+            for row in csv.DictReader(fh):
+                k = short(row.get("Kernel_Name", ""))
+                c = row.get("Counter_Name")
+                d = (path, row.get("Dispatch_Id") or row.get("Correlation_Id"))
+                vals[k][c][d] += float(row.get("Counter_Value") or 0.0)
+                if row.get("VGPR_Count"):
+                    vgpr[k] = (int(float(row["VGPR_Count"])), int(float(row.get("Accum_VGPR_Count") or 0)),
+                               int(float(row.get("SGPR_Count") or 0)), int(float(row.get("LDS_Block_Size") or 0)))
+    out = {}
+    for k, cs in vals.items():
+        out[k] = {c: sum(ds.values()) / len(ds) for c, ds in cs.items()}
+        if k in vgpr:
+            out[k]["_vgpr_agpr_sgpr_lds"] = vgpr[k]
+    return out
+
+
+def kernel_stats(stats_dir):
+    """{kernel: (calls, average ns)} from the --stats pass."""
+    out = {}
+    for path in glob.glob(os.path.join(stats_dir, "**", "*kernel_stats.csv"), recursive=True):
+        with open(path) as fh:
+            for row in csv.DictReader(fh):
+                out[short(row["Name"])] = (int(row["Calls"]), float(row["AverageNs"]))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "gpurun_out", "pmc"))
+    ap.add_argument("--tag", required=True)
+    ap.add_argument("--code", required=True, help="commit whose kernels were profiled")
+    ap.add_argument("--queries", type=float, default=1e8)
+    ap.add_argument("--freq", type=int, default=224)
+    args = ap.parse_args()
+    S = int(args.queries)
+    allc = {}
+    for p in sorted(os.listdir(args.pmc)):
+        d = os.path.join(args.pmc, p)
+        if os.path.isdir(d) and p != "stats":
+            for k, cs in counters(d).items():
+                allc.setdefault(k, {}).update(cs)
+    stats = kernel_stats(os.path.join(args.pmc, "stats"))
+    T = 20 * args.freq ** 2
+    workload = "C3: geodesic icosphere freq %d (%d faces, %d vertices), %d uniform queries in [-1.1,1.1]^3 per GPU" % (
+        args.freq, T, 10 * args.freq ** 2 + 2, S)
+    kern = {}
+    tot_bytes, hit, miss, tot_ns = 0.0, 0.0, 0.0, 0.0
+    for k in TRAVERSAL:
+        c = allc.get(k, {})
+        fetch, write = c.get("FETCH_SIZE"), c.get("WRITE_SIZE")
+        b = None
+        if fetch is not None and write is not None:
+            b = (2.0 * fetch + write) * 1024.0
+            tot_bytes += b
+        hit += c.get("TCC_HIT_sum", 0.0)
+        miss += c.get("TCC_MISS_sum", 0.0)
+        ns = stats.get(k, (0, 0.0))[1]
+        tot_ns += ns
+        kern[k] = {"counters": c, "hbm_bytes_per_launch": b, "avg_ms": ns / 1e6,
+                   "hbm_GBps": (b / ns) if (b and ns) else None}
+    res = {
+        "workload": workload, "queries": S, "code": args.code,
+        "units": "FETCH_SIZE / WRITE_SIZE in KB per launch as rocprofv3 reports them; gfx950: bytes = "
+                 "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md §HBM); TCC_HIT/MISS summed over channels",
+        "kernels": kern,
+        "bytes_per_launch": tot_bytes or None,
+        "bytes_per_query": (tot_bytes / S) if tot_bytes else None,
+        "l2_hit_rate": hit / (hit + miss) if hit + miss > 0 else None,
+        "traversal_ms": tot_ns / 1e6,
+        "hbm_GBps": (tot_bytes / tot_ns) if (tot_bytes and tot_ns) else None,
+    }
+    os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
+    with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
+        json.dump(res, fh, indent=1)
+    with open(os.path.join(ROOT, "profiles", "%s_pmc_%s.json" % (args.tag, args.code)), "w") as fh:
+        json.dump({"code": args.code, "workload": workload, "kernel_stats_avg_ns": stats, "counters": allc}, fh,
+                  indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "kernels"}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

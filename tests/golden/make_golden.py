@@ -10,7 +10,8 @@ Outputs (data only — inputs and expected outputs, no reference source):
                    (`v x y z`, `f a[/t][/n] ...`, 1-based indices)
   ref_tests.json   the literal known answers of the reference's hot-path tests:
                    tests/test_mesh.py:89-109, tests/test_aabb_n_tree.py:29-89,
-                   tests/test_visibility.py:13-53, tests/test_intersections.py:27
+                   tests/test_visibility.py:13-53, tests/test_intersections.py:27,
+                   tests/test_geometry.py:61-104 and tests/test_mesh.py:111-118 (normals, barycentrics)
                    (the icosphere of mesh/sphere.py:19-57 is stored as data too)
   kdtree.npz       scipy.spatial.KDTree answers for ClosestPointTree (search.py:52-65) on the
                    sphere fixture (scipy is the third-party arithmetic that path uses)
@@ -99,6 +100,21 @@ REF_TESTS = {
         "vextra": [[.9, .9, .9], [-.9, .9, .9], [.9, -.9, .9], [-.9, -.9, .9]],
         "fextra1": [[1, 2, 3], [4, 3, 2]],
     },
+    # tests/test_geometry.py:70-104: barycentric_coordinates_of_projection vs the old matlab function
+    # (columns are points; tolerance 1e-3), plus the single-point call on column 0
+    "test_barycentric": {
+        "p": [[-120, 48, -30, 88, -80], [71, 102, 29, -114, -291], [161, 72, -78, -106, 142]],
+        "q": [[32, -169, 32, -3, 108], [-75, -10, 31, -16, 110], [136, -24, -86, 62, -86]],
+        "u": [[8, -1, 37, -108, 109], [-120, 152, -22, 3, 153], [-110, -76, 111, 55, 9]],
+        "v": [[-148, 233, -19, -139, -18], [-73, -61, 88, -141, -19], [-105, 74, -76, 48, 141]],
+        "b": [[1.5266, -0.8601, 1.3245, 2.4450, 1.3452], [-1.5346, 0.8556, -0.1963, -2.1865, -2.0794],
+              [1.0080, 1.0046, -0.1282, 0.7415, 1.7342]],
+        "tol": 1e-3,
+    },
+    # tests/test_mesh.py:111-118: sphere.obj centred; mean |vn - v/rad| < 0.05
+    "test_estimate_vertex_normals": {"mesh": "sphere", "mse_max": 0.05},
+    # tests/test_geometry.py:61-68: estimate_vertex_normals == VertNormals within 1e-15 (sphere fixture)
+    "test_vert_normals": {"mesh": "sphere", "tol": 1e-15},
     # tests/test_intersections.py:27 (disabled in the reference; verified by brute force in SURVEY §4)
     "test_intersections": {"q_center": [-1, 0, 0], "m_center": [1, 0, 0], "radius": 2,
                            "expected": [2, 4, 5, 6, 16, 25, 26, 27, 36, 37, 38, 40, 58, 60, 61, 63, 76, 77, 79]},

@@ -42,7 +42,7 @@ def test_library_is_gfx950_hip():
 def test_version_and_error_string():
     from mesh_amd import _native
     L = _native.lib()
-    assert L.msh_version() == 1
+    assert L.msh_version() == 2
     assert isinstance(L.msh_last_error(), bytes)
 
 

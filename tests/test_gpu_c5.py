@@ -1,0 +1,153 @@
+"""C5 (BASELINE configs[4]): nearest_alongnormal + visibility_compute on the 5,000,000-face bumped icosphere
+with 64 Fibonacci cameras, through the device entry points (msh_tree_nearest_alongnormal_device,
+msh_visibility_device) that the multi-GPU split uses.
+
+Parity, three ways:
+  * a sample of rays / (camera, vertex) pairs against the exhaustive oracle (every one of the 5M triangles),
+    bit-exact: same closed ray/triangle predicates, CGAL's Plane_3/Line_3 hit construction
+    (spatialsearchmodule.cpp:276-307, visibility.cpp:75-115);
+  * size-independent properties on ALL 10M rays and ALL 64 x 2.5M visibility rays (hit on its face's plane
+    and on the ray's line, dist = |hit - p|, dist <= |offset| since the line crosses its own sample face,
+    miss rows = 1e100 / NO_FACE / NaN; ndc = n . dir bit-exact; visibility monotone in min_dist);
+  * the vertex-range / ray-range shards of the multi-GPU split reproduce the unsharded answer bit for bit.
+Parity of nearest_alongnormal and sensor visibility is unpinned by reference tests: the oracle
+restates the constructions, it is not checked against CGAL output.
+"""
+import numpy as np
+import pytest
+
+import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c5():
+    import torch
+    from mesh_amd import _native, spatialsearch
+    _native.set_device(0)
+    v, f = W.c5_mesh()
+    assert f.shape[0] == 5_000_000 and v.shape[0] == 2_500_002
+    t = spatialsearch.aabbtree_compute(v, f)
+    diag = float(np.linalg.norm(v.max(0) - v.min(0)))
+    yield dict(v=v, f=f, tree=t, diag=diag)
+    del t
+    torch.cuda.empty_cache()
+
+
+def _along(tree, p, n):
+    import torch
+    from mesh_amd.distributed import alongnormal_device
+    dp, dn = torch.from_numpy(p).cuda(), torch.from_numpy(n).cuda()
+    S = p.shape[0]
+    d = torch.empty(S, dtype=torch.float64, device="cuda")
+    fc = torch.empty(S, dtype=torch.int32, device="cuda")
+    pt = torch.empty((S, 3), dtype=torch.float64, device="cuda")
+    alongnormal_device(tree, dp, dn, d, fc, pt)
+    torch.cuda.synchronize()
+    return d, fc, pt
+
+
+def test_c5_alongnormal_full(c5, oracle):
+    import torch
+    v, f, tree, diag = c5["v"], c5["f"], c5["tree"], c5["diag"]
+    p, n, delta, fi = W.c5_rays(v, f, 10_000_000, seed=5)
+    d, fc, pt = _along(tree, p, n)
+    # ---- sample vs the exhaustive oracle (bit-exact) ----
+    idx = np.random.default_rng(51).choice(p.shape[0], 128, replace=False)
+    bd, bf, bpt = oracle.brute_alongnormal(v, f, p[idx], n[idx])
+    sd, sf, spt = d[idx].cpu().numpy(), fc[idx].cpu().numpy().view(np.uint32), pt[idx].cpu().numpy()
+    assert np.array_equal(sd, bd) and np.array_equal(sf, bf)
+    hs = bd < 1e100
+    assert np.array_equal(spt[hs], bpt[hs])
+    # ---- properties on all 10M rays (on the device) ----
+    dp, dn = torch.from_numpy(p).cuda(), torch.from_numpy(n).cuda()
+    hit = d < 1e100
+    assert hit.float().mean().item() > 0.9999  # every line crosses its own sample face
+    miss = ~hit
+    assert (fc[miss] == -1).all() and torch.isnan(pt[miss]).all()
+    fcs = fc[hit].to(torch.int64) & 0xFFFFFFFF
+    assert (fcs < f.shape[0]).all()
+    ph, nh, hh, dh = dp[hit], dn[hit], pt[hit], d[hit]
+    assert torch.allclose(dh, torch.linalg.norm(hh - ph, dim=1), rtol=1e-14, atol=0)
+    dt = torch.from_numpy(delta).cuda()[hit].abs()
+    assert (dh <= dt * (1 + 1e-9) + 1e-12 * diag).all()
+    vt = torch.from_numpy(v).cuda()
+    ft = torch.from_numpy(f.astype(np.int64)).cuda()[fcs]
+    a, b, c = vt[ft[:, 0]], vt[ft[:, 1]], vt[ft[:, 2]]
+    nrm = torch.linalg.cross(b - a, c - a)
+    nrm = nrm / torch.linalg.norm(nrm, dim=1, keepdim=True)
+    assert ((hh - a) * nrm).sum(1).abs().max().item() < 1e-9 * diag       # on its face's plane
+    off = torch.linalg.cross(hh - ph, nh) / torch.linalg.norm(nh, dim=1, keepdim=True)
+    assert off.abs().max().item() < 1e-9 * diag                            # on the ray's line
+    # ---- the multi-GPU ray-range split: two shards == the whole ----
+    from mesh_amd.distributed import shard_range
+    for r in range(2):
+        s0, s1 = shard_range(p.shape[0], r, 2)
+        d2, f2, p2 = _along(tree, p[s0:s1], n[s0:s1])
+        assert torch.equal(d2, d[s0:s1]) and torch.equal(f2, fc[s0:s1])
+        assert torch.equal(torch.nan_to_num(p2, 7.0), torch.nan_to_num(pt[s0:s1], 7.0))
+
+
+def _vis(tree, cams, normals, min_dist=1e-3, v0=0, nv=None, sensors=None):
+    import torch
+    from mesh_amd.distributed import visibility_device
+    P = int(tree.info().n_points)
+    nv = P - v0 if nv is None else nv
+    C = cams.shape[0]
+    vis = torch.empty((C, nv), dtype=torch.int32, device="cuda")
+    ndc = torch.empty((C, nv), dtype=torch.float64, device="cuda")
+    visibility_device(tree, cams, vis, ndc, normals, sensors, min_dist, v0, nv)
+    torch.cuda.synchronize()
+    return vis, ndc
+
+
+def test_c5_visibility_full(c5, oracle):
+    import torch
+    from mesh_amd.mesh import Mesh
+    v, f, tree = c5["v"], c5["f"], c5["tree"]
+    P = v.shape[0]
+    cams = W.fibonacci_cameras(64, 3.0)
+    vn = Mesh(v=v, f=f).estimate_vertex_normals()
+    dc, dn = torch.from_numpy(cams).cuda(), torch.from_numpy(vn).cuda()
+    vis, ndc = _vis(tree, dc, dn)
+    assert vis.shape == (64, P)
+    frac = vis.double().mean().item()
+    assert 0.2 < frac < 0.8, frac
+    # ---- sample vs the exhaustive oracle ----
+    rng = np.random.default_rng(52)
+    ci = rng.choice(64, 2, replace=False)
+    vi = rng.choice(P, 128, replace=False)
+    bv, bn = oracle.brute_visibility(v, f, cams[ci], n=vn, src_idx=vi)
+    assert np.array_equal(vis[ci][:, vi].cpu().numpy().view(np.uint32), bv)
+    assert np.array_equal(ndc[ci][:, vi].cpu().numpy(), bn)
+    # ---- ndc = n . normalize(c - v), bit-exact, for 2 whole camera rows (numpy, no FMA) ----
+    for c in ci:
+        dx, dy, dz = cams[c, 0] - v[:, 0], cams[c, 1] - v[:, 1], cams[c, 2] - v[:, 2]
+        ln = np.sqrt(dx * dx + dy * dy + dz * dz)
+        want = vn[:, 0] * (dx / ln) + vn[:, 1] * (dy / ln) + vn[:, 2] * (dz / ln)
+        assert np.array_equal(ndc[c].cpu().numpy(), want)
+    # ---- visibility is monotone in min_dist (the longer-offset ray is a sub-ray) ----
+    vis2, _ = _vis(tree, dc, dn, min_dist=0.05)
+    worse = ((vis2 == 0) & (vis == 1)).double().mean().item()
+    assert worse < 1e-6, worse
+    assert vis2.double().mean().item() >= frac
+    # ---- the multi-GPU vertex-range split: 3 shards == the whole ----
+    from mesh_amd.distributed import shard_range
+    for r in range(3):
+        v0, v1 = shard_range(P, r, 3)
+        vs, ns = _vis(tree, dc, dn, v0=v0, nv=v1 - v0)
+        assert torch.equal(vs, vis[:, v0:v1]) and torch.equal(ns, ndc[:, v0:v1])
+
+
+def test_c5_visibility_sensors_sample(c5, oracle):
+    # sensor clipping (visibility.cpp:79-85,96-111) on a 2-camera subset, vs the oracle
+    import torch
+    v, f, tree = c5["v"], c5["f"], c5["tree"]
+    cams = W.fibonacci_cameras(64, 3.0)[:2]
+    sens = np.random.default_rng(53).normal(size=(2, 9))
+    vis, ndc = _vis(tree, torch.from_numpy(cams).cuda(), None, sensors=torch.from_numpy(sens).cuda())
+    vi = np.random.default_rng(54).choice(v.shape[0], 128, replace=False)
+    bv, bn = oracle.brute_visibility(v, f, cams, sensors=sens, src_idx=vi)
+    assert np.array_equal(vis[:, vi].cpu().numpy().view(np.uint32), bv)
+    assert (ndc == 0).all()

@@ -1,0 +1,144 @@
+"""GPU parity of the geometry that feeds and consumes the search path.
+
+* fused barycentrics: ``aabbtree_nearest_barycentric`` / ``AabbTreeBatch.nearest_barycentric`` return the
+  closest face and point (bit-exact vs the exhaustive oracle) plus Heidrich weights that must equal the
+  oracle's numpy restatement of ``Mesh.barycentric_coordinates_for_points`` (mesh.py:218-222,
+  geometry/barycentric_coordinates_of_projection.py:9-49) applied to that face and point, bit for bit.
+  The restatement itself is pinned by tests/test_geometry.py:70-104's known answers (test_oracle.py).
+* vertex normals: ``Mesh.estimate_vertex_normals`` (GPU) must equal the scipy-sparse restatement of
+  mesh.py:208-216 bit for bit, and meet tests/test_mesh.py:111-118 / test_geometry.py:61-68.
+"""
+import numpy as np
+import pytest
+
+import workloads as W
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _device():
+    from mesh_amd import _native
+    _native.set_device(0)
+
+
+def _check_bary(oracle, v, f, q):
+    from mesh_amd import spatialsearch
+    t = spatialsearch.aabbtree_compute(np.ascontiguousarray(v, np.float64), np.ascontiguousarray(f, np.uint32))
+    face, pt, w = spatialsearch.aabbtree_nearest_barycentric(t, q)
+    assert face.shape == (q.shape[0],) and face.dtype == np.uint32
+    assert pt.shape == w.shape == (q.shape[0], 3) and w.dtype == np.float64
+    bf, _, bpt, _ = oracle.brute_nearest(v, f, q)
+    assert np.array_equal(face, bf)
+    assert np.array_equal(pt, bpt)
+    vi, bw = oracle.barycentric_coordinates_for_points(v, f, pt, face)
+    assert np.array_equal(w, bw), np.abs(w - bw).max()
+    # the point lies in its triangle: weights reconstruct it and are (nearly) a convex combination
+    rec = np.einsum("sk,skd->sd", w, v[vi.astype(np.int64)])
+    diag = float(np.linalg.norm(v.max(0) - v.min(0)))
+    assert np.abs(rec - pt).max() < 1e-9 * diag
+    assert w.min() > -1e-6 and abs(w.sum(1) - 1).max() < 1e-9
+    # the same faces/points as the plain nearest call
+    f2, _, p2 = spatialsearch.aabbtree_nearest(t, q)
+    assert np.array_equal(f2[0], face) and np.array_equal(p2, pt)
+    return face, pt, w
+
+
+def test_barycentric_sphere(oracle, meshes):
+    v, f = meshes["sphere_v"], meshes["sphere_f"]
+    _check_bary(oracle, v, f, W.c1_queries(20000))
+
+
+def test_barycentric_near_surface(oracle):
+    v, f = W.c2_mesh()
+    q, _ = W.surface_samples(v, f, 20000, seed=31, sigma=0.01)
+    _check_bary(oracle, v, f, q)
+
+
+def test_barycentric_landmarks_flow(oracle, ref_tests):
+    # landmarks.py:58-63: closest_faces_and_points then barycentric_coordinates_for_points
+    from mesh_amd.mesh import Mesh
+    t = ref_tests["test_aabb_tree"]
+    v, f = np.array(t["v"], dtype=np.float64), np.array(t["f"], dtype=np.uint32)
+    q = np.array(t["q"], dtype=np.float64)
+    m = Mesh(v=v, f=f)
+    faces, pts = m.closest_faces_and_points(q)
+    vi, coeff = m.barycentric_coordinates_for_points(pts, faces)
+    face, pt, w = _check_bary(oracle, v, f, q)
+    assert np.array_equal(face, faces[0]) and np.array_equal(vi, f[face])
+    assert np.array_equal(w, coeff)
+
+
+def test_barycentric_device_and_nonfinite(oracle):
+    import torch
+    from mesh_amd import spatialsearch
+    from mesh_amd.distributed import nearest_bary_device
+    v, f = W.geodesic_icosphere(20)
+    q = W.uniform_in_box([-1.1] * 3, [1.1] * 3, 50000, seed=32, margin=0)
+    q[7] = [np.nan, 0, 0]
+    t = spatialsearch.aabbtree_compute(v, f)
+    face, pt, w = spatialsearch.aabbtree_nearest_barycentric(t, q)
+    assert face[7] == 0xFFFFFFFF and np.isnan(pt[7]).all() and np.isnan(w[7]).all()
+    dq = torch.from_numpy(q).cuda()
+    dface = torch.empty(q.shape[0], dtype=torch.int32, device="cuda")
+    dpt = torch.empty_like(dq)
+    dw = torch.empty_like(dq)
+    nearest_bary_device(t, dq, dface, dpt, dw)
+    torch.cuda.synchronize()
+    assert np.array_equal(dface.cpu().numpy().view(np.uint32), face)
+    assert np.array_equal(dpt.cpu().numpy(), pt, equal_nan=True)
+    assert np.array_equal(dw.cpu().numpy(), w, equal_nan=True)
+
+
+def test_batch_barycentric(oracle):
+    from mesh_amd.search import AabbTreeBatch
+    v, f, q = W.c4_batch(B=6, S=3000, seed=33)
+    bt = AabbTreeBatch(v, f)
+    face, pt, w = bt.nearest_barycentric(q)
+    assert face.shape == (6, 3000) and pt.shape == w.shape == (6, 3000, 3)
+    for b in range(6):
+        bf, _, bpt, _ = oracle.brute_nearest(v[b], f, q[b])
+        assert np.array_equal(face[b], bf) and np.array_equal(pt[b], bpt)
+        _, bw = oracle.barycentric_coordinates_for_points(v[b], f, pt[b], face[b])
+        assert np.array_equal(w[b], bw)
+
+
+# ---------------------------------------------------------------- vertex normals
+def test_vertex_normals_known_answer(meshes, ref_tests):
+    from mesh_amd.mesh import Mesh
+    t = ref_tests["test_estimate_vertex_normals"]
+    m = Mesh(v=meshes[t["mesh"] + "_v"], f=meshes[t["mesh"] + "_f"])
+    m.v -= np.mean(m.v, axis=0)
+    rad = np.linalg.norm(m.v[0])
+    vn = np.array(m.estimate_vertex_normals())
+    assert np.mean(np.sqrt(np.sum((vn - m.v / rad) ** 2, axis=1))) < t["mse_max"]
+
+
+@pytest.mark.parametrize("name", ["sphere", "c2", "bumpy", "degenerate"])
+def test_vertex_normals_bit_exact(oracle, meshes, ref_tests, name):
+    from mesh_amd.mesh import Mesh
+    if name == "sphere":
+        v, f = meshes["sphere_v"], meshes["sphere_f"]
+    elif name == "c2":
+        v, f = W.c2_mesh()
+    elif name == "bumpy":
+        v, f = W.geodesic_icosphere(60)
+        v = v * (1 + 0.1 * np.sin(7 * v[:, [0]]) * np.cos(5 * v[:, [1]]))
+    else:
+        # an isolated vertex (zero norm -> 1 -> a zero normal) and a zero-area face
+        v, f = W.geodesic_icosphere(3)
+        v = np.vstack([v, [[5.0, 5.0, 5.0]]])
+        f = np.vstack([f, [[0, 1, 1]]]).astype(np.uint32)
+    vn = Mesh(v=v, f=f).estimate_vertex_normals()
+    ref = oracle.estimate_vertex_normals(v, f)
+    assert np.array_equal(vn, ref), np.abs(vn - ref).max()
+    assert np.max(np.abs(oracle.vert_normals(v, f) - vn)) < ref_tests["test_vert_normals"]["tol"]
+
+
+def test_vertex_normals_c5_size(oracle):
+    # 5M faces / 2.5M vertices (the C5 mesh feeding visibility_compute): bit-exact on the whole mesh
+    from mesh_amd.mesh import Mesh
+    v, f = W.c5_mesh()
+    vn = Mesh(v=v, f=f).estimate_vertex_normals()
+    ref = oracle.estimate_vertex_normals(v, f)
+    assert np.array_equal(vn, ref)

@@ -171,3 +171,55 @@ def test_tri_tri_symmetric(oracle):
     assert oracle.tri_tri_overlap([0, 0, 0, 1, 0, 0, 0, 1, 0], [0, 0, 0, -1, 0, 0, 0, 0, 1])
     assert oracle.tri_tri_overlap([0, 0, 0, 2, 0, 0, 0, 2, 0], [0.5, 0.5, 0, 3, 0.5, 0, 0.5, 3, 0])
     assert not oracle.tri_tri_overlap([0, 0, 0, 1, 0, 0, 0, 1, 0], [0, 0, 1, 1, 0, 1, 0, 1, 1])
+
+
+# ---- geometry restatements feeding the path ----
+def test_barycentric_known_answer(oracle, ref_tests):
+    # tests/test_geometry.py:70-104 (columns are points)
+    t = ref_tests["test_barycentric"]
+    p, q, u, v, b = (np.array(t[k], dtype=np.float64).T for k in ("p", "q", "u", "v", "b"))
+    est = oracle.barycentric_coordinates_of_projection(p, q, u, v)
+    assert np.max(np.abs(est.flatten('F') - b.flatten('F'))) < t["tol"]
+    est1 = oracle.barycentric_coordinates_of_projection(p[0], q[0], u[0], v[0])
+    assert np.max(np.abs(np.ravel(est1) - b[0])) < t["tol"]
+
+
+def test_barycentric_reconstructs_projection(oracle):
+    rng = np.random.default_rng(5)
+    a, e1, e2, p = (rng.normal(size=(200, 3)) for _ in range(4))
+    w = oracle.barycentric_coordinates_of_projection(p, a, e1, e2)
+    proj = w[:, [0]] * a + w[:, [1]] * (a + e1) + w[:, [2]] * (a + e2)
+    n = np.cross(e1, e2)
+    # p - proj is along the normal: the weights are those of p's orthogonal projection
+    assert np.allclose(np.cross(p - proj, n), 0, atol=1e-9)
+    assert np.allclose(w.sum(1), 1.0)
+
+
+def test_vertex_normals_known_answer(oracle, meshes, ref_tests):
+    # tests/test_mesh.py:111-118 and tests/test_geometry.py:61-68
+    t = ref_tests["test_estimate_vertex_normals"]
+    v = meshes[t["mesh"] + "_v"].copy()
+    f = meshes[t["mesh"] + "_f"]
+    v -= np.mean(v, axis=0)
+    rad = np.linalg.norm(v[0])
+    vn = oracle.estimate_vertex_normals(v, f)
+    assert np.mean(np.sqrt(np.sum((vn - v / rad) ** 2, axis=1))) < t["mse_max"]
+    assert np.max(np.abs(oracle.vert_normals(v, f) - vn)) < ref_tests["test_vert_normals"]["tol"]
+
+
+def test_alongnormal_point_is_cgal_plane_line(oracle):
+    # the oracle's hit point on a proper hit is CGAL's Plane_3/Line_3 construction: it lies on the
+    # face's plane and on the ray's line (to rounding), at distance |hit - p|
+    v, f = W.geodesic_icosphere(6)
+    p, fi = W.surface_samples(v, f, 400, seed=21, sigma=0.05)
+    n = np.random.default_rng(22).normal(size=p.shape)
+    d, face, pt = oracle.brute_alongnormal(v, f, p, n)
+    hit = d < 1e100
+    assert hit.mean() > 0.5
+    tri = v[f[face[hit]].astype(np.int64)]
+    nrm = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
+    nrm /= np.linalg.norm(nrm, axis=1)[:, None]
+    assert np.abs(np.sum((pt[hit] - tri[:, 0]) * nrm, axis=1)).max() < 1e-12
+    assert np.allclose(d[hit], np.linalg.norm(pt[hit] - p[hit], axis=1), rtol=0, atol=0)
+    off = np.cross(pt[hit] - p[hit], n[hit]) / np.linalg.norm(n[hit], axis=1)[:, None]
+    assert np.abs(off).max() < 1e-12

@@ -170,3 +170,30 @@ def c4_batch(B=4096, S=10_000, seed=4):
         diag = float(np.linalg.norm(v[i].max(0) - v[i].min(0)))
         q[i] = surface_samples(v[i], f, S, seed=seed * 100003 + i, sigma=0.005 * diag)[0]
     return v, f, q
+
+
+def fibonacci_cameras(C=64, radius=3.0):
+    """C5 cameras: C points of a Fibonacci sphere of the given radius."""
+    k = np.arange(C) + 0.5
+    z = 1 - 2 * k / C
+    r = np.sqrt(1 - z * z)
+    ph = np.pi * (1 + 5 ** 0.5) * k
+    return radius * np.stack([r * np.cos(ph), r * np.sin(ph), z], 1)
+
+
+def c5_rays(v, f, n=10_000_000, seed=5, sigma=0.01):
+    """C5 nearest_alongnormal rays: area-weighted surface samples s on face fi, offset by delta ~ N(0, sigma)
+    along the unit face normal nrm; the ray direction is nrm.  Returns p = s + delta * nrm, nrm, delta, fi."""
+    rng = np.random.default_rng(seed)
+    tri = v[f.astype(np.int64)]
+    cr = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
+    area = np.linalg.norm(cr, axis=1)
+    fi = rng.choice(f.shape[0], size=n, p=area / area.sum())
+    r1 = np.sqrt(rng.uniform(size=n))
+    r2 = rng.uniform(size=n)
+    t = tri[fi]
+    s = (1 - r1)[:, None] * t[:, 0] + (r1 * (1 - r2))[:, None] * t[:, 1] + (r1 * r2)[:, None] * t[:, 2]
+    del t
+    nrm = cr[fi] / area[fi][:, None]
+    delta = rng.normal(scale=sigma, size=n)
+    return s + delta[:, None] * nrm, nrm, delta, fi
