@@ -116,6 +116,12 @@ int msh_tree_nearest_alongnormal(msh_tree* tree, const double* p, const double* 
                                  uint32_t* face, double* pt);
 int msh_tree_nearest_alongnormal_device(msh_tree* tree, const double* d_p, const double* d_n, size_t S,
                                         double* d_dist, uint32_t* d_face, double* d_pt, void* stream);
+/* Instrumented ray traversals (not timed; same traversal as the entry points above): total internal nodes
+ * loaded and leaf triangles tested, for the algorithmic-bytes figure of the ray roofline. */
+int msh_tree_nearest_alongnormal_stats(msh_tree* tree, const double* d_p, const double* d_n, size_t S, uint64_t* nodes,
+                                       uint64_t* leaves);
+int msh_visibility_stats(msh_tree* tree, const double* d_cams, size_t C, double min_dist, uint64_t* nodes,
+                         uint64_t* leaves);
 
 /* aabbtree_intersections_indices(tree, qv, qf) -> ascending query-face indices (K,) u32 whose
  * triangle intersects any mesh triangle: spatialsearchmodule.cpp:326-417 (unregistered there,

@@ -43,6 +43,8 @@ SIGNATURES = [
     ("msh_tree_nearest_bary_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     ("msh_tree_nearest_alongnormal", _i, [_vp, _c_double_p, _c_double_p, _sz, _c_double_p, _c_u32_p, _c_double_p]),
     ("msh_tree_nearest_alongnormal_device", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    ("msh_tree_nearest_alongnormal_stats", _i, [_vp, _vp, _vp, _sz, _c_u64_p, _c_u64_p]),
+    ("msh_visibility_stats", _i, [_vp, _vp, _sz, ctypes.c_double, _c_u64_p, _c_u64_p]),
     ("msh_tree_intersections", _i, [_vp, _c_double_p, _sz, _c_u32_p, _sz, _c_u32_p, ctypes.POINTER(_sz)]),
     ("msh_ntree_build", _i, [_c_double_p, _sz, _c_u32_p, _sz, ctypes.c_double, ctypes.POINTER(_vp)]),
     ("msh_ntree_nearest", _i, [_vp, _c_double_p, _c_double_p, _sz, _c_u32_p, _c_double_p]),

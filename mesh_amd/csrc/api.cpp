@@ -761,6 +761,50 @@ int msh_tree_nearest_alongnormal_device(msh_tree* t, const double* d_p, const do
     return launch_alongnormal(t, ord, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_dist}, s);
 }
 
+static int read_stats(msh_tree* t, hipStream_t s, uint64_t* nodes, uint64_t* leaves) {
+    unsigned long long h[2] = {0, 0};
+    MSH_HIP(hipMemcpyAsync(h, t->ws.stats.ptr, sizeof(h), hipMemcpyDeviceToHost, s));
+    MSH_HIP(hipStreamSynchronize(s));
+    *nodes = h[0];
+    *leaves = h[1];
+    return MSH_OK;
+}
+
+int msh_tree_nearest_alongnormal_stats(msh_tree* t, const double* d_p, const double* d_n, size_t S, uint64_t* nodes,
+                                       uint64_t* leaves) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_alongnormal_stats"));
+    MSH_TRY(check_count(S, "msh_tree_nearest_alongnormal_stats"));
+    if (!nodes || !leaves) { set_error("msh_tree_nearest_alongnormal_stats: null argument"); return MSH_EINVAL; }
+    *nodes = *leaves = 0;
+    if (S == 0) return MSH_OK;
+    hipStream_t s = t->stream;
+    {
+        WsOrder order(t, s);
+        QueryOrder ord;
+        MSH_TRY(sort_queries(t, d_p, d_n, S, s, &ord));
+        MSH_TRY(t->ws.stats.reserve(8 * sizeof(unsigned long long)));
+        MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, 8 * sizeof(unsigned long long), s));
+        MSH_TRY(launch_alongnormal_stats(t, ord, S, t->ws.stats.as<unsigned long long>(), s));
+    }
+    return read_stats(t, s, nodes, leaves);
+}
+
+int msh_visibility_stats(msh_tree* t, const double* d_cams, size_t C, double min_dist, uint64_t* nodes,
+                         uint64_t* leaves) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_visibility_stats"));
+    if (!nodes || !leaves || (C && !d_cams)) { set_error("msh_visibility_stats: null argument"); return MSH_EINVAL; }
+    *nodes = *leaves = 0;
+    if (C == 0 || t->P == 0) return MSH_OK;
+    hipStream_t s = t->stream;
+    {
+        WsOrder order(t, s);
+        MSH_TRY(t->ws.stats.reserve(8 * sizeof(unsigned long long)));
+        MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, 8 * sizeof(unsigned long long), s));
+        MSH_TRY(launch_visibility_stats(t, d_cams, C, min_dist, t->ws.stats.as<unsigned long long>(), s));
+    }
+    return read_stats(t, s, nodes, leaves);
+}
+
 int msh_tree_nearest_alongnormal(msh_tree* t, const double* p, const double* n, size_t S, double* dist, uint32_t* face,
                                  double* pt) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_alongnormal"));

@@ -265,10 +265,16 @@ __device__ inline void node_child_bounds(const NodeV& nd, const QF& q, float& d0
         e1[k] = nd.at(kObb[1] + k);
     }
     const int a0 = kAabb[0], a1 = kAabb[1];
+#ifdef MSH_OBB_ONLY  // tuning experiment: oriented-box bound only
+    (void)a0; (void)a1;
+    d0 = obb_d2_lo(q, n, t, b, e0);
+    d1 = obb_d2_lo(q, n, t, b, e1);
+#else
     d0 = fmaxf(box_d2_lo(q, nd.at(a0), nd.at(a0 + 1), nd.at(a0 + 2), nd.at(a0 + 3), nd.at(a0 + 4), nd.at(a0 + 5)),
                obb_d2_lo(q, n, t, b, e0));
     d1 = fmaxf(box_d2_lo(q, nd.at(a1), nd.at(a1 + 1), nd.at(a1 + 2), nd.at(a1 + 3), nd.at(a1 + 4), nd.at(a1 + 5)),
                obb_d2_lo(q, n, t, b, e1));
+#endif
 }
 
 // Leaf pretest of the exact policies.  Lower bound of the squared distance from the origin to

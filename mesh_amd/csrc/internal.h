@@ -179,6 +179,12 @@ int launch_visibility(const msh_tree* tree, const double* d_cams, size_t C, cons
                       const double* d_sensors, double min_dist, size_t v0, size_t nv, uint32_t* d_vis, double* d_ndc,
                       hipStream_t s);
 
+// instrumented (untimed, outputs not written): d_counts[0] += internal nodes loaded, [1] += leaf tests
+int launch_alongnormal_stats(const msh_tree* tree, const QueryOrder& ord, size_t S, unsigned long long* d_counts,
+                             hipStream_t s);
+int launch_visibility_stats(const msh_tree* tree, const double* d_cams, size_t C, double min_dist,
+                            unsigned long long* d_counts, hipStream_t s);
+
 // ---- triangle-triangle (tritri.hip) ----
 // flags[i] = 1 iff query triangle i intersects any tree triangle (self: skip shared-vertex pairs and
 // the query triangles are the tree's own leaves in face order).

@@ -86,6 +86,11 @@ struct KnnArgs {
     int spill_depth;
     unsigned long long* stats;
     unsigned budget;
+    // leader / follower ordering (sorted closest-point launches, MODE 0 and 3): phase 0 = every slot,
+    // unhinted; phase 1 = leader slots (i % kLead == 0); phase 2 = the other slots, each starting from the
+    // upper bound given by its 64-slot tile's leaders (see hint_from_leaders)
+    int phase;
+    size_t nunits;  // work units of this phase (slots it covers)
     DeferRec* deferred;
     unsigned* n_deferred;
     unsigned max_deferred;
@@ -237,7 +242,7 @@ struct Walker {
     int sp;
     __device__ inline void push(uint2 e, uint2* __restrict__ lds, uint2* __restrict__ spill) {
         if (sp < kStack) lds[sp * kBlock] = e;
-        else spill[sp - kStack] = e;
+        else spill[(sp - kStack) * kBlock] = e;
         ++sp;
     }
     // pop until an entry survives the current limit; false when the stack is exhausted
@@ -245,7 +250,7 @@ struct Walker {
     __device__ inline bool pop(const Pol& pol, uint2* __restrict__ lds, uint2* __restrict__ spill) {
         while (sp > 0) {
             --sp;
-            const uint2 e = sp < kStack ? lds[sp * kBlock] : spill[sp - kStack];
+            const uint2 e = sp < kStack ? lds[sp * kBlock] : spill[(sp - kStack) * kBlock];
             if (__uint_as_float(e.y) <= pol.limf) {
                 node = (int)e.x;
                 return true;
@@ -423,12 +428,54 @@ __device__ inline void test_pending(Pol& pol, int& p0, int& p1) {
 
 __device__ inline D3 load_q(const KnnArgs& a, size_t i) { return D3{a.q[3 * i], a.q[3 * i + 1], a.q[3 * i + 2]}; }
 
+#ifndef MSH_LEAD
+#define MSH_LEAD 8
+#endif
+constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: leader ordering off)
+
+// slot of work unit k in the launch's phase
+__device__ inline size_t slot_of(const KnnArgs& a, size_t k) {
+    if (a.phase == 1) return k * kLead;
+    if (a.phase == 2) {
+        const size_t g = k / (kLead - 1);
+        return g * kLead + (k - g * (kLead - 1)) + 1;
+    }
+    return k;
+}
+
+// Upper bound of slot i's squared distance from the closest points its tile's leaders found: a leader's
+// point p_L lies on a mesh triangle, so d*(q) <= |q - p_L|.  The bound is widened by 2^-30 relative and
+// (2^-40 M)^2 absolute (M = largest |coordinate|) against the rounding of the fp64 constructions; the
+// caller still re-runs the query unhinted whenever its final best exceeds the bound, so a bound that is
+// too tight costs time, never correctness.  Leaders of another mesh (batched trees), deferred leaders
+// (NO_FACE until pass 2 runs) and non-finite ones are skipped.
+__device__ inline double hint_from_leaders(const KnnArgs& a, size_t i, const D3& q) {
+    const size_t base = i & ~(size_t)63;
+    const size_t mesh = a.orgs ? i / a.qper : 0;
+    double h = INFINITY;
+    for (unsigned L = 0; L < 64; L += kLead) {
+        const size_t li = base + L;
+        if (li >= a.S) break;
+        if (a.orgs && li / a.qper != mesh) continue;
+        const uint4 r0 = reinterpret_cast<const uint4*>(a.res + li)[0];
+        if (r0.x == MSH_NO_FACE) continue;
+        const double2 r1 = reinterpret_cast<const double2*>(a.res + li)[1];
+        const double x = __longlong_as_double((long long)(((unsigned long long)r0.w << 32) | r0.z));
+        const double dx = q.x - x, dy = q.y - r1.x, dz = q.z - r1.y;
+        h = fmin(h, dx * dx + dy * dy + dz * dz);
+    }
+    if (h == INFINITY) return h;
+    const double M = fmax(fmax(fabs(q.x), fabs(q.y)), fabs(q.z));
+    const double e = M * 9.094947017729282e-13;  // 2^-40 M
+    return h * (1.0 + 9.313225746154785e-10) + e * e;  // 1 + 2^-30
+}
+
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
     const int tid = threadIdx.x, lane = tid & 63;
     uint2* lds = stk + tid;
-    uint2* spill = a.spill ? a.spill + ((size_t)blockIdx.x * kBlock + tid) * (size_t)a.spill_depth : nullptr;
+    uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
     const unsigned group = blockIdx.x & 7u;
     unsigned long long u_trav_it = 0, u_trav_lanes = 0, u_leaf_it = 0, u_leaf_lanes = 0;  // STATS: wave iterations
     unsigned n_nodes = 0, n_leaves = 0;
@@ -437,13 +484,23 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         if (lane == 0) tile = dequeue_tile(a.counters, a.ntiles, group);
         tile = __shfl(tile, 0);
         if (tile >= a.ntiles) break;
-        const size_t i = (size_t)tile * 64 + lane;
+        const size_t k = (size_t)tile * 64 + lane;
+        if (k >= a.nunits) continue;
+        const size_t i = slot_of(a, k);
         if (i >= a.S) continue;
         const D3 q = load_q(a, i);
         auto pol = make_pol<MODE>(a, i, q);
         if (!finite3(q)) {  // no distance is defined: NO_FACE / NaN, no traversal
-            if (!STATS) write_result<MODE>(a, i, q, pol);
+            if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
             continue;
+        }
+        double hint = INFINITY;
+        if constexpr (MODE == 0 || MODE == 3) {
+            if (a.phase == 2) {
+                hint = hint_from_leaders(a, i, q);
+                pol.shared = hint;
+                pol.relim();
+            }
         }
         if (a.T == 1) {
             pol.test(0);
@@ -460,6 +517,15 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             // expensive fp64 leaf path executes for many lanes at once instead of stalling the wave
             // on one lane every iteration (Aila & Laine 2009, "postponed leaf" while-while).
             for (;;) {
+                // a hinted lane whose result is not below its hint re-runs unhinted (hint_from_leaders)
+                if (!active && !deferred && p0 < 0 && hint != INFINITY && !(pol.best <= hint)) {
+                    hint = INFINITY;
+                    pol.shared = INFINITY;
+                    pol.relim();
+                    w = Walker{root, 0};
+                    steps = 0;
+                    active = true;
+                }
                 const bool parked = p0 >= 0;
                 const unsigned long long bp = __ballot(parked);
                 const unsigned long long bt = __ballot(active && !parked);
@@ -488,6 +554,10 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
                         if (slot < a.max_deferred) {
                             test_pending(pol, p0, p1);
+                            if (a.phase == 1) {  // followers must not take a hint from this leader yet
+                                D3 nq = D3{NAN, NAN, NAN};
+                                if (a.res) store_qres(a.res + i, MSH_NO_FACE, 0u, nq.x, nq.y, nq.z);
+                            }
                             DeferRec r;
                             r.slot = (uint32_t)i;
                             r.face = pol.best_face;
@@ -505,7 +575,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             }
             if (deferred) continue;
         }
-        if (!STATS) write_result<MODE>(a, i, q, pol);
+        if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
     }
     if (STATS) {
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
@@ -548,7 +618,7 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
     __shared__ uint2 front[4][2][kFront];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     uint2* lds = stk + tid;
-    uint2* spill = a.spill ? a.spill + ((size_t)blockIdx.x * kBlock + tid) * (size_t)a.spill_depth : nullptr;
+    uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
     const unsigned total = min(*a.n_deferred, a.max_deferred);
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     unsigned n_nodes = 0, n_leaves = 0;
@@ -742,6 +812,10 @@ static int device_cus(int dev) {
 }
 
 constexpr unsigned kBudget = 2048;  // pass-1 node steps per lane before a query is deferred
+#ifndef MSH_KNN_BPC
+#define MSH_KNN_BPC 4
+#endif
+constexpr unsigned kKnnBlocksPerCU = MSH_KNN_BPC;  // resident pass-1 blocks per CU (persistent grid)
 
 // Common launch: grid, counters, spill area, deferred list; pass 1 then pass 2 (both also in STATS
 // mode, so the instrumented counts describe the traversal that is timed).
@@ -749,17 +823,18 @@ template <int MODE, bool STATS>
 static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* timer) {
     if (a.S == 0) return MSH_OK;
     for (int k = 0; k < 3; ++k) a.org[k] = tree->origin[k];
-    const unsigned ntiles = (unsigned)((a.S + 63) / 64);
-    const unsigned want = (ntiles + 3) / 4;
     const unsigned ncu = (unsigned)device_cus(tree->device);
-    const unsigned nblk = std::min<unsigned>(want, ncu * 4u);
-    a.ntiles = ntiles;
     Workspace& ws = tree->ws;
     // counters: 8 group counters (one 128-B line each) + the deferred count
     MSH_TRY(ws.counters.reserve(9 * 32 * sizeof(unsigned)));
     a.counters = ws.counters.as<unsigned>();
     a.n_deferred = a.counters + 8 * 32;
     MSH_HIP(hipMemsetAsync(a.counters, 0, 9 * 32 * sizeof(unsigned), s));
+    // leader ordering: closest-point launches over a Morton-sorted slot order (records in a.res)
+    const bool lead = kLead > 1 && (MODE == 0 || MODE == 3) && a.res != nullptr && a.S >= 64 * (size_t)kLead;
+    const size_t n_lead = (a.S + kLead - 1) / kLead;
+    const unsigned max_tiles = (unsigned)((a.S + 63) / 64);
+    const unsigned nblk_max = std::min<unsigned>((max_tiles + 3) / 4, ncu * kKnnBlocksPerCU);
     // pass 2 lanes carry up to kFront/64 dealt subtrees on top of a depth-first path
     const unsigned nblk2 = ncu * 2u;
     const int need = tree->max_depth + 1 + kFront / 64 + 1;
@@ -767,7 +842,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     a.spill_depth = 0;
     if (need > kStack) {
         a.spill_depth = need - kStack + 1;
-        MSH_TRY(ws.spill.reserve((size_t)std::max(nblk, nblk2) * kBlock * (size_t)a.spill_depth * sizeof(uint2)));
+        MSH_TRY(ws.spill.reserve((size_t)std::max(nblk_max, nblk2) * kBlock * (size_t)a.spill_depth * sizeof(uint2)));
         a.spill = ws.spill.as<uint2>();
     }
     a.budget = kBudget;
@@ -775,12 +850,28 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     DevBuf& dbuf = ws.flags;
     MSH_TRY(dbuf.reserve((size_t)a.max_deferred * sizeof(DeferRec)));
     a.deferred = dbuf.as<DeferRec>();
+    auto pass1 = [&](int phase, size_t nunits, const char* name) -> int {
+        a.phase = phase;
+        a.nunits = nunits;
+        a.ntiles = (unsigned)((nunits + 63) / 64);
+        const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, ncu * kKnnBlocksPerCU);
+        if (nblk == 0) return MSH_OK;
+        TimedLaunch t1(name, s);
+        k_knn<MODE, STATS><<<nblk, kBlock, 0, s>>>(a);
+        MSH_HIP(hipGetLastError());
+        return MSH_OK;
+    };
     {
         TimedLaunch tl(timer, s);
         {
             TimedLaunch t1(STATS ? "knn_pass1_stats" : "knn_pass1", s);
-            k_knn<MODE, STATS><<<nblk, kBlock, 0, s>>>(a);
-            MSH_HIP(hipGetLastError());
+            if (lead) {
+                MSH_TRY(pass1(1, n_lead, STATS ? "knn_lead_stats" : "knn_lead"));
+                MSH_HIP(hipMemsetAsync(a.counters, 0, 8 * 32 * sizeof(unsigned), s));  // group counters only
+                MSH_TRY(pass1(2, a.S - n_lead, STATS ? "knn_follow_stats" : "knn_follow"));
+            } else {
+                MSH_TRY(pass1(0, a.S, STATS ? "knn_all_stats" : "knn_all"));
+            }
         }
         {
             TimedLaunch t2(STATS ? "knn_pass2_stats" : "knn_pass2", s);
@@ -800,7 +891,7 @@ static int run_knn(msh_tree* tree, KnnArgs a, const QueryOrder& ord, const SlotO
     a.q = ord.q;
     a.perm = ord.perm;
     Workspace& ws = tree->ws;
-    if (ord.perm && !STATS) {
+    if (ord.perm) {  // STATS launches keep the records too: followers take their hints from them
         MSH_TRY(ws.res.reserve(a.S * sizeof(QRes)));
         a.res = ws.res.as<QRes>();
         if (nw) {

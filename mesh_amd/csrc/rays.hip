@@ -126,16 +126,18 @@ __device__ inline bool slab(const RayF& r, float lx, float ly, float lz, float h
 }
 
 // ---- generic traversal: the policy decides box hits (and ordering key) and leaf tests ----
-template <class Pol>
+template <class Pol, bool STATS>
 __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, Pol& pol, uint2* __restrict__ lds,
-                                     uint2* __restrict__ spill) {
+                                     uint2* __restrict__ spill, unsigned& n_nodes, unsigned& n_leaves) {
     if (T == 1) {
         pol.test(0);
+        if (STATS) ++n_leaves;
         return;
     }
     int node = 0, sp = 0;
     for (size_t guard = 0; guard < T; ++guard) {
         const NodeV nd = load_node(nodes, node);
+        if (STATS) ++n_nodes;
         double k0, k1;
         float l0[3], u0[3], l1[3], u1[3];
         node_aabb(nd, 0, l0, u0);
@@ -145,11 +147,13 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
         const int c0 = nd.child(0), c1 = nd.child(1);
         if (h0 && c0 < 0) {
             pol.test(~c0);
+            if (STATS) ++n_leaves;
             h0 = false;
             if (pol.done()) return;
         }
         if (h1 && c1 < 0) {
             pol.test(~c1);
+            if (STATS) ++n_leaves;
             h1 = false;
             if (pol.done()) return;
         }
@@ -161,7 +165,7 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
             if (k1 < k0) { nearc = c1; farc = c0; kf = k0; }
             const uint2 e = make_uint2((unsigned)farc, __float_as_uint(__double2float_rd(kf)));
             if (sp < kStack) lds[sp * kBlock] = e;
-            else spill[sp - kStack] = e;
+            else spill[(sp - kStack) * kBlock] = e;
             ++sp;
             node = nearc;
             continue;
@@ -171,7 +175,7 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
         bool found = false;
         while (sp > 0) {
             --sp;
-            const uint2 e = sp < kStack ? lds[sp * kBlock] : spill[sp - kStack];
+            const uint2 e = sp < kStack ? lds[sp * kBlock] : spill[(sp - kStack) * kBlock];
             if (pol.keep((double)__uint_as_float(e.y))) {
                 node = (int)e.x;
                 found = true;
@@ -266,6 +270,7 @@ struct RayArgs {
     uint32_t* vis;
     double* ndc;
     // common
+    unsigned long long* stats;  // STATS launches: [0] nodes loaded, [1] leaf tests (outputs not written)
     unsigned* counters;
     unsigned ntiles;
     uint2* spill;
@@ -288,12 +293,13 @@ __device__ inline unsigned dequeue_tile_r(unsigned* counters, unsigned ntiles, u
 
 __device__ inline bool finite_d3(const D3& x) { return isfinite(x.x) && isfinite(x.y) && isfinite(x.z); }
 
-template <int MODE>  // 0 alongnormal, 1 visibility
+template <int MODE, bool STATS>  // MODE 0 alongnormal, 1 visibility
 __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
+    unsigned n_nodes = 0, n_leaves = 0;
     __shared__ uint2 stk[kStack * kBlock];
     const int tid = threadIdx.x, lane = tid & 63;
     uint2* lds = stk + tid;
-    uint2* spill = a.spill ? a.spill + ((size_t)blockIdx.x * kBlock + tid) * (size_t)a.spill_depth : nullptr;
+    uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
     const unsigned group = blockIdx.x & 7u;
     const D3 org = D3{a.org[0], a.org[1], a.org[2]};
     for (;;) {
@@ -309,7 +315,9 @@ __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
             const D3 dp = ray_dir(p, n), pr = vsub(p, org);
             AlongPol pol{a.tris, p, dp, ray_dir(p, D3{-n.x, -n.y, -n.z}), make_rayf(pr, dp), pr, INFINITY, MSH_NO_FACE,
                          D3{NAN, NAN, NAN}};
-            if (finite_d3(p) && finite_d3(dp)) traverse_rays<AlongPol>(a.nodes, a.T, pol, lds, spill);
+            if (finite_d3(p) && finite_d3(dp))
+                traverse_rays<AlongPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
+            if (STATS) continue;
             const double dist = pol.best == INFINITY ? 1e100 : pol.best;
             if (a.res) {
                 store_qres(a.res + i, pol.best_face, 0u, pol.best_pt.x, pol.best_pt.y, pol.best_pt.z);
@@ -333,7 +341,9 @@ __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
             const D3 src = vadd(vv, vscale(a.min_dist, dir));
             const D3 d = ray_dir(src, dir);
             AnyPol pol{a.tris, src, d, make_rayf(vsub(src, org), d), false};
-            if (finite_d3(src) && finite_d3(d)) traverse_rays<AnyPol>(a.nodes, a.T, pol, lds, spill);
+            if (finite_d3(src) && finite_d3(d))
+                traverse_rays<AnyPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
+            if (STATS) continue;
             const uint32_t reach = pol.hit ? 0u : 1u;
             a.ndc[o] = a.normals ? vdot(D3{a.normals[3 * iv], a.normals[3 * iv + 1], a.normals[3 * iv + 2]}, dir) : 0.0;
             uint32_t out = reach;
@@ -352,6 +362,10 @@ __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
             a.vis[o] = out;
         }
     }
+    if (STATS) {
+        atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
+        atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
+    }
 }
 
 static int device_cus_r(int dev) {
@@ -360,7 +374,7 @@ static int device_cus_r(int dev) {
     return n;
 }
 
-template <int MODE>
+template <int MODE, bool STATS>
 static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, const char* timer) {
     if (nrays == 0) return MSH_OK;
     if (nrays > (size_t)0xFFFFFFFFull * 64) {
@@ -382,7 +396,7 @@ static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, c
         a.spill = tree->ws.spill.as<uint2>();
     }
     TimedLaunch tl(timer, s);
-    k_rays<MODE><<<nblk, kBlock, 0, s>>>(a);
+    k_rays<MODE, STATS><<<nblk, kBlock, 0, s>>>(a);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }
@@ -400,7 +414,7 @@ int launch_alongnormal(const msh_tree* tree, const QueryOrder& ord, size_t S, co
     } else {
         a.out_dist = o.w; a.out_face = o.face; a.out_pt = o.pt;
     }
-    MSH_TRY(launch_rays<0>(t, a, S, s, "alongnormal"));
+    MSH_TRY((launch_rays<0, false>(t, a, S, s, "alongnormal")));
     if (ord.perm) {
         SlotOut oo{};
         oo.face = o.face;
@@ -464,7 +478,31 @@ int launch_visibility(const msh_tree* tree, const double* d_cams, size_t C, cons
         MSH_TRY(vertex_order(t, s));
         a.vorder = t->d_vorder;
     }
-    return launch_rays<1>(t, a, C * nv, s, "visibility");
+    return launch_rays<1, false>(t, a, C * nv, s, "visibility");
+}
+
+int launch_alongnormal_stats(const msh_tree* tree, const QueryOrder& ord, size_t S, unsigned long long* d_counts,
+                             hipStream_t s) {
+    msh_tree* t = const_cast<msh_tree*>(tree);
+    RayArgs a{};
+    a.nodes = tree->d_nodes; a.tris = static_cast<const TriRec*>(tree->d_leaves); a.T = tree->T;
+    a.p = ord.q; a.n = ord.n;
+    a.stats = d_counts;
+    return launch_rays<0, true>(t, a, S, s, "alongnormal_stats");
+}
+
+int launch_visibility_stats(const msh_tree* tree, const double* d_cams, size_t C, double min_dist,
+                            unsigned long long* d_counts, hipStream_t s) {
+    msh_tree* t = const_cast<msh_tree*>(tree);
+    RayArgs a{};
+    a.nodes = tree->d_nodes; a.tris = static_cast<const TriRec*>(tree->d_leaves); a.T = tree->T;
+    a.v = tree->d_v; a.P = tree->P; a.v0 = 0; a.nv = tree->P;
+    a.cams = d_cams; a.min_dist = min_dist;
+    a.stats = d_counts;
+    if (C == 0 || tree->P == 0) return MSH_OK;
+    MSH_TRY(vertex_order(t, s));
+    a.vorder = t->d_vorder;
+    return launch_rays<1, true>(t, a, C * tree->P, s, "visibility_stats");
 }
 
 }  // namespace msh

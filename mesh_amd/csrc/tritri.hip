@@ -148,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
     const int tid = threadIdx.x;
     uint2* lds = stk + tid;
     for (size_t i = (size_t)blockIdx.x * kBlock + tid; i < a.Tq; i += (size_t)gridDim.x * kBlock) {
-        uint2* spill = a.spill ? a.spill + ((size_t)blockIdx.x * kBlock + tid) * (size_t)a.spill_depth : nullptr;
+        uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
         D3 qa, qb, qc;
         uint32_t qface;
         load_tri(a.q, (int)i, qa, qb, qc, qface);
@@ -187,7 +187,7 @@ __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
                 if (h0 && h1) {
                     const uint2 e = make_uint2((unsigned)c1, 0u);
                     if (sp < kStack) lds[sp * kBlock] = e;
-                    else spill[sp - kStack] = e;
+                    else spill[(sp - kStack) * kBlock] = e;
                     ++sp;
                     node = c0;
                     continue;
@@ -196,7 +196,7 @@ __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
                 if (h1) { node = c1; continue; }
                 if (sp == 0) break;
                 --sp;
-                node = (int)(sp < kStack ? lds[sp * kBlock] : spill[sp - kStack]).x;
+                node = (int)(sp < kStack ? lds[sp * kBlock] : spill[(sp - kStack) * kBlock]).x;
             }
         }
         a.flags[i] = hit ? 1u : 0u;

@@ -3,7 +3,7 @@ is RCCL on ROCm; xGMI between MI355X GPUs).
 
 The path partitions by query: every rank holds the same mesh + BVH and answers a contiguous shard of
 the queries.  The BVH is built once (on `src`) and replicated with ONE RCCL broadcast of its packed
-blob (mesh vertices + 64-B nodes + 80-B leaves), instead of every rank rebuilding it.  Results stay
+blob (mesh vertices + 128-B nodes + 80-B leaves), instead of every rank rebuilding it.  Results stay
 sharded in each rank's HBM; `gather_results` concatenates shards where a caller needs them in one
 place (one all_gather per output array, padded to the largest shard).
 """
@@ -21,32 +21,62 @@ def shard_range(n, rank, world):
     return start, start + base + (1 if rank < rem else 0)
 
 
+def broadcast_bytes(blob, src=0, group=None, device=None):
+    """Broadcast a uint8 tensor from rank `src` (its size first, then the bytes) and return this rank's
+    copy.  `blob` is the tensor on `src` (ignored elsewhere); the copy lives on `device` (default: the
+    device of `blob` on src, the current CUDA device elsewhere when the backend is nccl, else the CPU)."""
+    import torch
+    import torch.distributed as dist
+
+    rank = dist.get_rank(group)
+    if device is None:
+        if rank == src:
+            device = blob.device
+        elif dist.get_backend(group) == "nccl":
+            device = torch.device("cuda", torch.cuda.current_device())
+        else:
+            device = torch.device("cpu")
+    nbytes = torch.zeros(1, dtype=torch.int64, device=device)
+    if rank == src:
+        nbytes[0] = blob.numel()
+    dist.broadcast(nbytes, src, group=group)
+    out = blob if rank == src else torch.empty(int(nbytes.item()), dtype=torch.uint8, device=device)
+    dist.broadcast(out, src, group=group)
+    return out
+
+
+def blob_info(header_bytes):
+    """Parse + validate a packed tree blob's header (host bytes, at least the header) with the library's
+    msh_blob_header_parse (no device needed) -> dict of the layout fields."""
+    import ctypes
+    buf = np.frombuffer(bytes(header_bytes), dtype=np.uint8).copy()
+    inf = _native.BlobInfo()
+    _native.check(_native.lib().msh_blob_header_parse(buf.ctypes.data, buf.size, ctypes.byref(inf)))
+    return {name: (list(getattr(inf, name)) if name == "origin" else getattr(inf, name)) for name, _ in inf._fields_}
+
+
 def replicate_tree(tree, src=0, device=None, group=None):
     """Broadcast a built tree from rank `src` to every rank (RCCL over xGMI); returns this rank's handle.
 
-    `tree` is the handle on `src` (ignored elsewhere).  The blob is staged in a torch uint8 tensor
-    on the rank's current CUDA (HIP) device.
+    `tree` is the handle on `src` (ignored elsewhere).  The blob is packed into a torch uint8 tensor on
+    the rank's current CUDA (HIP) device, broadcast once, and unpacked in place on the receivers.
     """
     import torch
     import torch.distributed as dist
 
     rank = dist.get_rank(group)
     dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
-    nbytes = torch.zeros(1, dtype=torch.int64, device=dev)
+    blob = None
     if rank == src:
-        nbytes[0] = _native.blob_size(tree)
-    dist.broadcast(nbytes, src, group=group)
-    n = int(nbytes.item())
-    blob = torch.empty(n, dtype=torch.uint8, device=dev)
-    if rank == src:
+        blob = torch.empty(_native.blob_size(tree), dtype=torch.uint8, device=dev)
         _native.blob_pack(tree, blob.data_ptr(), None)
     torch.cuda.synchronize(dev)
-    dist.broadcast(blob, src, group=group)
+    blob = broadcast_bytes(blob, src, group, device=dev)
     torch.cuda.synchronize(dev)
     if rank == src:
         return tree
     kind = {0: "triangles", 1: "normals", 2: "points"}
-    h = _native.blob_unpack(blob.data_ptr(), n, dev.index, None)
+    h = _native.blob_unpack(blob.data_ptr(), blob.numel(), dev.index, None)
     h.kind = kind.get(int(h.info().kind), "triangles")
     return h
 
@@ -116,6 +146,13 @@ def visibility_device(tree, cams, vis, ndc, normals=None, sensors=None, min_dist
         vis.data_ptr(), ndc.data_ptr(), _stream(cams, stream)))
 
 
+def gather_columns(local, total, group=None):
+    """All-gather a 2-D tensor sharded along its LAST axis (this rank holds the columns
+    shard_range(total, rank, world)) into the whole (rows, total) tensor on every rank."""
+    t = local.t().contiguous()
+    return gather_results(t, total, group).t().contiguous()
+
+
 def visibility_sharded(tree, cams, normals=None, sensors=None, min_dist=1e-3, group=None):
     """C5's multi-GPU split of visibility_compute (visibility.cpp:136-173 loops cameras x vertices):
     every rank casts the rays of its contiguous vertex range for all cameras, then the (C, P) result is
@@ -133,7 +170,63 @@ def visibility_sharded(tree, cams, normals=None, sensors=None, min_dist=1e-3, gr
     visibility_device(tree, cams, vis, ndc, normals, sensors, min_dist, v0, v1 - v0)
     if world == 1:
         return vis, ndc
-    # gather along the vertex axis: transpose so the sharded axis is first
-    vis_all = gather_results(vis.t().contiguous(), P, group).t().contiguous()
-    ndc_all = gather_results(ndc.t().contiguous(), P, group).t().contiguous()
-    return vis_all, ndc_all
+    return gather_columns(vis, P, group), gather_columns(ndc, P, group)
+
+
+def alongnormal_sharded(tree, p, n, group=None):
+    """C5's split of nearest_alongnormal: rank r answers the rays shard_range(S, r, world) of the (S,3)
+    device tensors p, n; the (dist, face, point) slabs are all-gathered."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    S = p.shape[0]
+    a, b = shard_range(S, rank, world)
+    d = torch.empty(b - a, dtype=torch.float64, device=p.device)
+    fc = torch.empty(b - a, dtype=torch.int32, device=p.device)
+    pt = torch.empty((b - a, 3), dtype=torch.float64, device=p.device)
+    alongnormal_device(tree, p[a:b].contiguous(), n[a:b].contiguous(), d, fc, pt)
+    if world == 1:
+        return d, fc, pt
+    return gather_results(d, S, group), gather_results(fc, S, group), gather_results(pt, S, group)
+
+
+def batch_nearest_sharded(v, f, q, group=None, device=None):
+    """C4's multi-GPU split (BASELINE configs[3]): the B meshes of one topology are sharded by mesh range
+    with no broadcast — rank r builds the batched tree of meshes shard_range(B, r, world) from its own
+    host slice and answers their queries (the reference builds one AabbTree per mesh, search.py:21-30).
+    v (B,P,3), f (T,3), q (B,S,3) host arrays -> (face (B,S) u32, part (B,S) u32, point (B,S,3) f64) numpy
+    arrays on every rank (one all_gather per output over the mesh axis)."""
+    import torch
+    import torch.distributed as dist
+    from .search import AabbTreeBatch
+
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    B, S = q.shape[0], q.shape[1]
+    b0, b1 = shard_range(B, rank, world)
+    if b1 > b0:
+        face, part, pt = AabbTreeBatch(v[b0:b1], f).nearest(q[b0:b1], nearest_part=True)
+    else:
+        face, part, pt = np.empty((0, S), np.uint32), np.empty((0, S), np.uint32), np.empty((0, S, 3))
+    if world == 1:
+        return face, part, pt
+    return gather_mesh_slabs((face, part, pt), B, group, device)
+
+
+def gather_mesh_slabs(arrays, B, group=None, device=None):
+    """All-gather host numpy slabs sharded over the mesh axis (rank r holds meshes shard_range(B, r, world))
+    -> the whole (B, ...) arrays on every rank.  uint32 arrays travel as int32 bit patterns."""
+    import torch
+    import torch.distributed as dist
+
+    if device is None:
+        device = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+    out = []
+    for a in arrays:
+        u32 = a.dtype == np.uint32
+        t = torch.from_numpy(np.ascontiguousarray(a.view(np.int32) if u32 else a)).to(device)
+        g = gather_results(t, B, group).cpu().numpy()
+        out.append(g.view(np.uint32) if u32 else g)
+    return tuple(out)

@@ -1,8 +1,9 @@
 """Secondary measurements for BASELINE.md configs C1, C2, C4, C5 (bench.py measures C3, the headline).
 
-One JSON line per config on stdout.  Every number comes from the GPU path through the numpy API (the
-reference's entry points: host arrays in, host arrays out) with the kernel time from the library's
-HIP-event timers beside it.  Inputs are the seeded synthetic workloads of workloads.py.
+One JSON line per config on stdout: the GPU path through the numpy API (the reference's entry points:
+host arrays in, host arrays out), the device-resident rate (inputs already in HBM) where it differs, the
+kernel time from the library's HIP-event timers, and the oracle's CGAL-faithful CPU restatement on a
+sample (1 thread and all host threads).  Inputs are the seeded synthetic workloads of workloads.py.
 
     python scripts/bench_configs.py [--configs c1,c2,c4,c5] [--reps 3]
 """
@@ -37,6 +38,36 @@ def kernel_ms(name):
     return ms / max(n, 1)
 
 
+def host_threads():
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return len(os.sched_getaffinity(0))
+
+
+def cpu_rates(v, f, q, budget_s=6.0):
+    """Oracle CGAL-tree restatement on a sample of q: (1-thread q/s, all-thread q/s, threads); median of
+    5 timed chunks after 2 warm-ups per mode (shortened for the secondary configs)."""
+    from oracle import oracle as O
+    tree = O.CgalTree(v, f, hint=True)
+    out = []
+    for threads in (1, host_threads()):
+        n = min(q.shape[0], 1000 * threads)
+        t0 = time.perf_counter()
+        tree.nearest(q[:n], threads=threads)
+        rate = n / max(time.perf_counter() - t0, 1e-6)
+        chunk = int(min(max(rate * budget_s / 2 / 7, 200), q.shape[0]))
+        rates = []
+        for k in range(7):
+            sel = q[(k * chunk) % max(q.shape[0] - chunk, 1):][:chunk]
+            t0 = time.perf_counter()
+            tree.nearest(sel, threads=threads)
+            if k >= 2:
+                rates.append(sel.shape[0] / (time.perf_counter() - t0))
+        out.append(float(np.median(rates)))
+    return out[0], out[1], host_threads()
+
+
 def c1(reps):
     from mesh_amd.search import AabbTree
     from mesh_amd.mesh import Mesh
@@ -45,13 +76,17 @@ def c1(reps):
     q = W.c1_queries()
     tree = AabbTree(Mesh(v=v, f=f))
     _, wall = timed(lambda: tree.nearest(q, nearest_part=True), reps)
+    c1t, cmt, th = cpu_rates(v, f, q)
     return {"config": "C1 sphere.obj (840 faces), 100k queries, AabbTree.nearest(nearest_part=True)",
             "queries_per_s_numpy_api": q.shape[0] / wall, "ms_numpy_api": wall * 1e3,
-            "ms_traversal_kernel": kernel_ms("nearest")}
+            "ms_traversal_kernel": kernel_ms("nearest"),
+            "cpu_ref_1t_qps": c1t, "cpu_ref_omp_qps": cmt, "cpu_threads": th}
 
 
 def c2(reps):
+    import torch
     from mesh_amd import spatialsearch
+    from mesh_amd.distributed import nearest_device
     import workloads as W
     v, f = W.c2_mesh()
     q = W.c2_queries()
@@ -59,13 +94,23 @@ def c2(reps):
     tree = spatialsearch.aabbtree_compute(v, f)
     build_wall = time.perf_counter() - t0
     _, wall = timed(lambda: spatialsearch.aabbtree_nearest(tree, q), reps)
+    S = q.shape[0]
+    dq = torch.from_numpy(q).cuda()
+    face = torch.empty(S, dtype=torch.int32, device="cuda")
+    part = torch.empty(S, dtype=torch.int32, device="cuda")
+    pt = torch.empty((S, 3), dtype=torch.float64, device="cuda")
+    wall_d = _device_timed(lambda: nearest_device(tree, dq, face, part, pt), reps)
+    c1t, cmt, th = cpu_rates(v, f, q)
     return {"config": "C2 SMPL-topology stand-in (6,890 v / 13,776 f), 10M near-surface queries",
-            "queries_per_s_numpy_api": q.shape[0] / wall, "ms_numpy_api": wall * 1e3,
-            "ms_traversal_kernel": kernel_ms("nearest"), "build_ms_gpu": tree.info().build_ms,
-            "build_ms_wall": build_wall * 1e3}
+            "queries_per_s_device": S / wall_d, "ms_traversal_kernel": kernel_ms("nearest"),
+            "queries_per_s_numpy_api": S / wall, "ms_numpy_api": wall * 1e3,
+            "build_ms_gpu": tree.info().build_ms, "build_ms_wall": build_wall * 1e3,
+            "cpu_ref_1t_qps": c1t, "cpu_ref_omp_qps": cmt, "cpu_threads": th}
 
 
 def c4(reps):
+    import torch
+    from mesh_amd import _native
     from mesh_amd.search import AabbTreeBatch
     import workloads as W
     t0 = time.perf_counter()
@@ -78,41 +123,101 @@ def c4(reps):
 
     (tree, _), wall = timed(run, reps)
     n = q.shape[0] * q.shape[1]
+    B, S = q.shape[0], q.shape[1]
+    dq = torch.from_numpy(q).cuda()
+    face = torch.empty((B, S), dtype=torch.int32, device="cuda")
+    part = torch.empty((B, S), dtype=torch.int32, device="cuda")
+    pt = torch.empty((B, S, 3), dtype=torch.float64, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    h = tree.cpp_handle
+    wall_d = _device_timed(lambda: _native.check(_native.lib().msh_batch_nearest_device(
+        h.ptr, dq.data_ptr(), S, face.data_ptr(), part.data_ptr(), pt.data_ptr(), stream)), reps)
+    # CPU: one CGAL-restatement tree per mesh (the reference's per-mesh AabbTree), 8 sampled meshes
+    r1, rm = [], []
+    for b in np.linspace(0, B - 1, 8).astype(int):
+        a1, am, th = cpu_rates(v[b], f, q[b], budget_s=2.0)
+        r1.append(a1)
+        rm.append(am)
     return {"config": "C4 4096 meshes (5,042 v / 10,080 f, shared topology) x 10k scan points: batched build + query",
-            "queries_per_s_numpy_api": n / wall, "ms_build_plus_query_numpy_api": wall * 1e3,
+            "queries_per_s_numpy_api_build_plus_query": n / wall, "ms_build_plus_query_numpy_api": wall * 1e3,
+            "queries_per_s_device_query_only": n / wall_d, "ms_device_query": wall_d * 1e3,
             "build_ms_gpu": tree.cpp_handle.info().build_ms, "ms_traversal_kernel": kernel_ms("nearest_batch"),
-            "input_generation_s": gen_s}
+            "input_generation_s": gen_s, "cpu_ref_1t_qps_query_only": float(np.median(r1)),
+            "cpu_ref_omp_qps_query_only": float(np.median(rm)), "cpu_threads": th,
+            "cpu_note": "median over 8 sampled meshes of one CGAL-restatement tree each; tree builds excluded"}
+
+
+def _device_timed(fn, reps):
+    import torch
+    from mesh_amd import _native
+    fn()
+    torch.cuda.synchronize()
+    _native.timing_reset()
+    _native.timing_enable(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        fn()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / reps
+    _native.timing_enable(False)
+    return wall
 
 
 def c5(reps):
-    from mesh_amd import spatialsearch
-    from mesh_amd.visibility import visibility_compute
+    """C5: 10M nearest_alongnormal rays + visibility of 2.5M vertices from 64 cameras on the 5M-face bumped
+    icosphere.  Device-resident rays/s (inputs in HBM) with the ray-kernel roofline, plus the numpy-API
+    (end-to-end) rate of alongnormal."""
+    import torch
+    from mesh_amd import _native, spatialsearch
+    from mesh_amd.distributed import alongnormal_device, visibility_device
+    from mesh_amd.mesh import Mesh
     import workloads as W
     v, f = W.c5_mesh()
     tree = spatialsearch.aabbtree_compute(v, f)
-    rng = np.random.default_rng(5)
-    p, fi = W.surface_samples(v, f, 10_000_000, seed=5, sigma=0.0)
-    tri = v[f[fi].astype(np.int64)]
-    nrm = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
-    nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
-    p = p + nrm * rng.normal(scale=0.01, size=(p.shape[0], 1))
-    _, wall_r = timed(lambda: spatialsearch.aabbtree_nearest_alongnormal(tree, p, nrm), reps)
+    info = tree.info()
+    nb, lb = int(info.node_bytes), int(info.leaf_bytes)
+    p, n, _, _ = W.c5_rays(v, f, 10_000_000, seed=5)
+    S = p.shape[0]
+    _, wall_np = timed(lambda: spatialsearch.aabbtree_nearest_alongnormal(tree, p, n), reps)
+    dp, dn = torch.from_numpy(p).cuda(), torch.from_numpy(n).cuda()
+    d = torch.empty(S, dtype=torch.float64, device="cuda")
+    fc = torch.empty(S, dtype=torch.int32, device="cuda")
+    pt = torch.empty((S, 3), dtype=torch.float64, device="cuda")
+    wall_r = _device_timed(lambda: alongnormal_device(tree, dp, dn, d, fc, pt), reps)
     k_r = kernel_ms("alongnormal")
-    # 64 cameras on a Fibonacci sphere of radius 3, vertex normals
-    k = np.arange(64) + 0.5
-    phi = np.arccos(1 - 2 * k / 64)
-    th = np.pi * (1 + 5 ** 0.5) * k
-    cams = 3.0 * np.stack([np.cos(th) * np.sin(phi), np.sin(th) * np.sin(phi), np.cos(phi)], axis=1)
-    vn = np.zeros_like(v)
-    fn = np.cross(v[f[:, 1]] - v[f[:, 0]], v[f[:, 2]] - v[f[:, 0]])
-    for c in range(3):
-        np.add.at(vn, f[:, c], fn)
-    vn /= np.linalg.norm(vn, axis=1, keepdims=True)
-    (vis, _), wall_v = timed(lambda: visibility_compute(cams=cams, tree=tree, n=vn), 1)
-    return {"config": "C5 bumped icosphere (5,000,000 faces): 10M nearest_alongnormal rays; visibility 64 cams x 2.5M v",
-            "rays_per_s_alongnormal_numpy_api": p.shape[0] / wall_r, "ms_alongnormal_kernel": k_r,
-            "rays_per_s_visibility_numpy_api": vis.size / wall_v, "ms_visibility_kernel": kernel_ms("visibility"),
-            "visible_fraction": float(vis.mean())}
+    nodes, leaves = _native.ctypes.c_uint64(0), _native.ctypes.c_uint64(0)
+    _native.check(_native.lib().msh_tree_nearest_alongnormal_stats(tree.ptr, dp.data_ptr(), dn.data_ptr(), S,
+                                                                    _native.ctypes.byref(nodes),
+                                                                    _native.ctypes.byref(leaves)))
+    nn_r, nl_r = nodes.value / S, leaves.value / S
+    b_r = 48 + 36 + nb * nn_r + lb * nl_r  # SURVEY §8(d): 48 B in + 36 B out per ray + nodes + leaves
+    del d, fc, pt
+    # visibility: 64 Fibonacci cameras, vertex normals (GPU), all vertices
+    cams = W.fibonacci_cameras(64, 3.0)
+    vn = Mesh(v=v, f=f).estimate_vertex_normals()
+    dc, dvn = torch.from_numpy(cams).cuda(), torch.from_numpy(vn).cuda()
+    P, C = v.shape[0], cams.shape[0]
+    vis = torch.empty((C, P), dtype=torch.int32, device="cuda")
+    ndc = torch.empty((C, P), dtype=torch.float64, device="cuda")
+    wall_v = _device_timed(lambda: visibility_device(tree, dc, vis, ndc, dvn), reps)
+    k_v = kernel_ms("visibility")
+    _native.check(_native.lib().msh_visibility_stats(tree.ptr, dc.data_ptr(), C, 1e-3, _native.ctypes.byref(nodes),
+                                                      _native.ctypes.byref(leaves)))
+    R = C * P
+    nn_v, nl_v = nodes.value / R, leaves.value / R
+    b_v = 12 + 48.0 / C + nb * nn_v + lb * nl_v  # 12 B out per ray, 48 B in amortised over C cameras
+    return {"config": "C5 bumped icosphere (5,000,000 faces / 2,500,002 v): 10M nearest_alongnormal rays; "
+                      "visibility 64 Fibonacci cameras x 2.5M vertices (160M rays), vertex normals",
+            "alongnormal": {"rays_per_s_device": S / wall_r, "kernel_ms": k_r, "wall_ms_device": wall_r * 1e3,
+                            "rays_per_s_numpy_api": S / wall_np, "nodes_per_ray": nn_r, "leaves_per_ray": nl_r,
+                            "bytes_per_ray": b_r, "achieved_GBps": S * b_r / (k_r / 1e3) / 1e9,
+                            "frac_of_8TBps": S * b_r / (k_r / 1e3) / 8e12},
+            "visibility": {"rays_per_s_device": R / wall_v, "kernel_ms": k_v, "wall_ms_device": wall_v * 1e3,
+                           "nodes_per_ray": nn_v, "leaves_per_ray": nl_v, "bytes_per_ray": b_v,
+                           "achieved_GBps": R * b_v / (k_v / 1e3) / 1e9,
+                           "frac_of_8TBps": R * b_v / (k_v / 1e3) / 8e12,
+                           "visible_fraction": float(vis.double().mean().item())},
+            "build_ms_gpu": info.build_ms}
 
 
 def main():

@@ -20,9 +20,12 @@ for s in $STAGES; do
     variants)  # tuning sweep: every build/variants/*.so through the 10M-query bench (env MESH_AMD_LIB)
       for so in build/variants/*.so; do
         n=$(basename $so .so)
-        MESH_AMD_LIB=$PWD/$so timeout -k 10 300 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/var_$n.log 2>&1; ok var_$n $?
+        MESH_AMD_LIB=$PWD/$so timeout -k 10 300 python bench.py --queries ${VQ:-10000000} --steps ${VSTEPS:-5} --warmup 2 --no-cpu > gpurun_out/var_$n.log 2>&1; ok var_$n $?
       done ;;
     bench_wide) MESH_AMD_TRAVERSAL=wide timeout -k 10 600 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_wide.log 2>&1; ok bench_wide $? ;;
+    split)  MESH_AMD_STATS_DUMP=1 timeout -k 10 600 python scripts/c3_split.py > gpurun_out/split.log 2>&1; ok split $? ;;
+    pytest_quick) timeout -k 10 600 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread -k "spill or cooperative or c1 or c2 or c3 or rays or alongnormal or visibility" > gpurun_out/pytest_quick.log 2>&1; ok pytest_quick $? ;;
+    c5)     timeout -k 10 900 python scripts/bench_configs.py --configs c5 --reps 3 > gpurun_out/bench_c5.log 2>&1; ok c5 $? ;;
     configs) timeout -k 10 900 python scripts/bench_configs.py > gpurun_out/bench_configs.log 2>&1; ok configs $? ;;
     bench)  timeout -k 10 900 python bench.py > gpurun_out/bench.log 2>&1; ok bench $? ;;
     prof_small) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof_small" -o run -- python3 "$OLDPWD/bench.py" --queries 10000000 --steps 2 --warmup 1 --no-cpu > "$OLDPWD/gpurun_out/prof_small.log" 2>&1); ok prof_small $? ;;

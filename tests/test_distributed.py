@@ -70,3 +70,87 @@ def test_gather_and_broadcast_world2():
         assert (gf == np.arange(1001)).all()
         assert (gp == np.arange(1001)[:, None] * np.array([1.0, 2.0, 3.0])).all()
         assert bsum == want_sum
+
+
+# ---- blob replication path end to end (host side) and the C4 / C5 shard + gather index math ----
+def _worker_blob_and_shards(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import ctypes
+        from mesh_amd import _native
+        from mesh_amd.distributed import (blob_info, broadcast_bytes, gather_columns, gather_mesh_slabs,
+                                          shard_range)
+        res = {}
+        # (1) rank 0 lays out a tree blob with the library (header + payload pattern), broadcasts it;
+        #     every rank parses and validates the header with msh_blob_header_parse (no device)
+        blob = None
+        if rank == 0:
+            inf = _native.BlobInfo()
+            hdr = np.zeros(4096, np.uint8)
+            _native.check(_native.lib().msh_blob_header_write(0, 50002, 100000, 100000, hdr.ctypes.data, hdr.size,
+                                                              ctypes.byref(inf)))
+            payload = np.zeros(int(inf.total), np.uint8)
+            payload[:4096] = hdr[:4096]
+            payload[int(inf.off_nodes):] = (np.arange(payload.size - int(inf.off_nodes)) % 251).astype(np.uint8)
+            blob = torch.from_numpy(payload)
+        got = broadcast_bytes(blob, 0)
+        full = got.numpy()
+        info = blob_info(full.tobytes())
+        res["info"] = info
+        res["tail_sum"] = int(full[int(info["off_nodes"]):].astype(np.int64).sum())
+        # a truncated blob is rejected by the same parser
+        try:
+            blob_info(full[: int(info["total"]) - 1].tobytes())
+            res["truncated_rejected"] = False
+        except ValueError:
+            res["truncated_rejected"] = True
+        # (2) C5 visibility: (C, P) assembled from vertex-range column slabs
+        C, P = 3, 1001
+        v0, v1 = shard_range(P, rank, world)
+        cols = torch.arange(v0, v1, dtype=torch.float64)[None, :] + 10000.0 * torch.arange(C)[:, None]
+        res["vis"] = gather_columns(cols, P).numpy()
+        # (3) C4: meshes sharded by range, host slabs gathered over the mesh axis (uint32 + float64)
+        B, S = 7, 5
+        b0, b1 = shard_range(B, rank, world)
+        face = (np.arange(b0, b1)[:, None] * 100 + np.arange(S)[None, :]).astype(np.uint32)
+        face[:, 0] = 0xFFFFFFFF  # a NO_FACE row survives the int32 transport
+        pt = np.arange(b0, b1, dtype=np.float64)[:, None, None] * np.ones((1, S, 3))
+        gf, gp = gather_mesh_slabs((face, pt), B)
+        res["face"], res["pt"] = gf, gp
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_blob_and_shards_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_blob_and_shards, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    infos = [r["info"] for _, r in res]
+    assert infos[0] == infos[1]
+    info = infos[0]
+    assert info["kind"] == 0 and info["n_points"] == 50002 and info["n_faces"] == 100000
+    assert info["node_bytes"] == 128 and info["leaf_bytes"] == 80
+    assert info["off_nodes"] >= info["off_vertices"] + 50002 * 24
+    assert info["off_leaves"] >= info["off_nodes"] + (100000 - 1) * info["node_bytes"]
+    assert info["total"] >= info["off_leaves"] + 100000 * 80
+    n = info["total"] - info["off_nodes"]
+    want = int((np.arange(n) % 251).sum())
+    C, P, B, S = 3, 1001, 7, 5
+    for _, r in res:
+        assert r["tail_sum"] == want and r["truncated_rejected"]
+        assert (r["vis"] == np.arange(P)[None, :] + 10000.0 * np.arange(C)[:, None]).all()
+        wf = (np.arange(B)[:, None] * 100 + np.arange(S)[None, :]).astype(np.uint32)
+        wf[:, 0] = 0xFFFFFFFF
+        assert r["face"].dtype == np.uint32 and (r["face"] == wf).all()
+        assert (r["pt"] == np.arange(B, dtype=np.float64)[:, None, None]).all()

@@ -449,6 +449,22 @@ def test_batch_matches_single_trees():
         assert np.array_equal(face[b], sf[0]) and np.array_equal(part[b], sp[0]) and np.array_equal(pt[b], spt)
 
 
+def test_batch_of_one_off_origin_mesh(oracle):
+    # a B == 1 batch is a batched handle (bounds relative to the per-mesh origin); it must answer
+    # correctly through the batch entry points and be refused by the single-tree ones
+    from mesh_amd import spatialsearch
+    from mesh_amd.search import AabbTreeBatch
+    v, f = W.c4_mesh(3)
+    v = v + np.array([40.0, -25.0, 13.0])  # far from the scene origin
+    q = W.uniform_in_box(v.min(0), v.max(0), 20000, seed=61)
+    bt = AabbTreeBatch(v[None], f)
+    face, part, pt = bt.nearest(q[None], nearest_part=True)
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q)
+    assert np.array_equal(face[0], bf) and np.array_equal(part[0], bp) and np.array_equal(pt[0], bpt)
+    with pytest.raises(ValueError):
+        spatialsearch.aabbtree_nearest(bt.cpp_handle, q)
+
+
 def test_c4_full_size(oracle):
     # BASELINE configs[3]: 4096 meshes x 10k scan points; exact vs brute force on 6 meshes, properties on all
     from mesh_amd.search import AabbTreeBatch

@@ -329,10 +329,27 @@ double obb_d2(const double* q, const OBB& o) {
 }
 }  // namespace
 
+extern "C" void model_counts_obb_init(const double* v, const uint32_t* f, int T, const double* q, long S, int mode,
+                                      uint32_t* nodes_out, uint32_t* leaves_out, const double* init_best);
 extern "C" void model_counts_obb(const double* v, const uint32_t* f, int T, const double* q, long S, int mode,
                                  uint32_t* nodes_out, uint32_t* leaves_out) {
-    Tree tr = mode >= 10 ? build_median(v, f, T) : build_lbvh(v, f, T);  // mode + 10: median-split tree
-    mode %= 10;
+    model_counts_obb_init(v, f, T, q, S, mode, nodes_out, leaves_out, nullptr);
+}
+// init_best (nullable): per-query initial squared bound (an upper bound of the answer)
+static thread_local int* g_first_leaf = nullptr;
+extern "C" void model_counts_obb_first(const double* v, const uint32_t* f, int T, const double* q, long S, int mode,
+                                       uint32_t* nodes_out, uint32_t* leaves_out, const double* init_best,
+                                       int* first_face);
+extern "C" void model_counts_obb_init(const double* v, const uint32_t* f, int T, const double* q, long S, int mode,
+                                      uint32_t* nodes_out, uint32_t* leaves_out, const double* init_best) {
+    model_counts_obb_first(v, f, T, q, S, mode, nodes_out, leaves_out, init_best, nullptr);
+}
+// first_face (nullable): face of the first leaf each query tests
+extern "C" void model_counts_obb_first(const double* v, const uint32_t* f, int T, const double* q, long S, int mode,
+                                       uint32_t* nodes_out, uint32_t* leaves_out, const double* init_best,
+                                       int* first_face) {
+    Tree tr = (mode % 100) >= 10 ? build_median(v, f, T) : build_lbvh(v, f, T);  // mode + 10: median-split tree
+    mode = (mode / 100) * 100 + (mode % 10);
     std::vector<OBB> ob(2 * (T - 1));
     for (int x = 0; x < T - 1; ++x) {
         int pb, pe;
@@ -360,10 +377,15 @@ extern "C" void model_counts_obb(const double* v, const uint32_t* f, int T, cons
             }
         }
     }
+    const bool hint = mode >= 100;  // mode + 100: second pass starting from the final best distance
+    mode %= 100;
 #pragma omp parallel for schedule(dynamic, 64)
     for (long i = 0; i < S; ++i) {
-        const double* qq = q + 3 * i;
-        double best = std::numeric_limits<double>::infinity();
+      const double* qq = q + 3 * i;
+      double final_best = std::numeric_limits<double>::infinity();
+      for (int pass = 0; pass < (hint ? 2 : 1); ++pass) {
+        double best = pass == 1 ? final_best * (1 + 1e-12) : std::numeric_limits<double>::infinity();
+        if (init_best) best = init_best[i];
         uint32_t nn = 0, nl = 0;
         std::vector<std::pair<int, double>> st;
         int node = 0;
@@ -380,6 +402,7 @@ extern "C" void model_counts_obb(const double* v, const uint32_t* f, int T, cons
                     int fc = tr.order[~n.c[s]];
                     const uint32_t* ff = f + 3 * fc;
                     best = std::min(best, tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                    if (first_face && nl == 0) first_face[i] = fc;
                     ++nl;
                     h[s] = false;
                 }
@@ -402,8 +425,10 @@ extern "C" void model_counts_obb(const double* v, const uint32_t* f, int T, cons
             }
             if (!found) break;
         }
+        final_best = best;
         nodes_out[i] = nn;
         leaves_out[i] = nl;
+      }
     }
 }
 
