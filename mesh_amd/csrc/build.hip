@@ -9,15 +9,15 @@
 //   5. k_karras                        Karras (HPG 2012) internal-node emission; codes made unique by
 //                                      augmenting them with the sorted position; also records each
 //                                      node's contiguous leaf range and split
-//   6. k_refit                         bottom-up AABB refit, one lane per leaf, the second arrival at
-//                                      each node continues upward (agent-scope release/acquire hand-off,
-//                                      cdna_hip_programming.md §6 Guideline 16)
-//   7. k_depth                         max leaf depth (sizes the traversal stack spill)
-//   8. (after leaf packing) k_obb      one wave per node over its Morton leaf range: area-weighted
+//   6. k_depth                         max leaf depth (sizes the traversal stack spill)
+//   7. (after leaf packing) k_obb      one wave per node over its Morton leaf range: area-weighted
 //                                      normal -> node frame (n, t, b = n x t), then both children's vertex
-//                                      extents along the frame (oriented boxes, thin along the surface)
-// All fp32 bounds are rounded outward (round-down lo / round-up hi, then one more ulp), so every fp64
-// primitive lies inside the bounds of every ancestor.
+//                                      extents along the frame (oriented boxes, thin along the surface),
+//                                      quantised to 8 bits against a per-node base and power-of-two scale
+// All bounds are rounded outward (fp32 round-down lo / round-up hi plus one ulp, then the quantised code
+// rounds down / up, checked against the decoder), so every fp64 primitive lies inside the bounds of
+// every ancestor.  Round 1 also stored an fp32 AABB per child (128-B nodes, filled by a bottom-up refit);
+// the oriented boxes alone traverse faster.
 #include <algorithm>
 #include <memory>
 
@@ -204,51 +204,6 @@ __device__ inline float up1(float x) { return nextafterf(x, INFINITY); }
 __device__ inline float out_lo(double x) { return down1(__double2float_rd(x)); }
 __device__ inline float out_hi(double x) { return up1(__double2float_ru(x)); }
 
-__device__ inline void store_aabb(BNode* nodes, int node, int side, const float* lo, const float* hi) {
-    float* p = nodes[node].f + kAabb[side];  // 8 or 20: 16-B aligned, then an 8-B aligned pair
-    *reinterpret_cast<float4*>(p) = make_float4(lo[0], lo[1], lo[2], hi[0]);
-    *reinterpret_cast<float2*>(p + 4) = make_float2(hi[1], hi[2]);
-}
-
-__global__ __launch_bounds__(kBlock) void k_refit(const double* __restrict__ plo, const double* __restrict__ phi,
-                                                  const uint32_t* __restrict__ order, int B, int n, BNode* nodes,
-                                                  const uint32_t* __restrict__ parent, uint32_t* flags,
-                                                  const double* __restrict__ orgs) {
-    const long long leaf = (long long)blockIdx.x * kBlock + threadIdx.x;
-    if (leaf >= (long long)B * n) return;
-    const int mb = (int)(leaf / n);
-    const int root = mb * (n - 1);
-    const uint32_t pr = order[leaf];
-    const double org[3] = {orgs[3 * mb], orgs[3 * mb + 1], orgs[3 * mb + 2]};
-    float lo[3], hi[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        lo[k] = out_lo(plo[3 * (size_t)pr + k] - org[k]);
-        hi[k] = out_hi(phi[3 * (size_t)pr + k] - org[k]);
-    }
-    uint32_t p = parent[(size_t)B * (n - 1) + leaf];
-    for (int guard = 0; guard < 4096; ++guard) {  // bounded: a tree is never 4096 levels deep
-        const int node = (int)(p >> 1), side = (int)(p & 1u);
-        store_aabb(nodes, node, side, lo, hi);
-        // release: every store of this lane is performed and written back past this XCD's L2
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const uint32_t old = __hip_atomic_fetch_add(&flags[node], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (old == 0u) return;  // first arrival: the sibling's lane finishes this node
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        const float* a = nodes[node].f + kAabb[0];
-        const float* b = nodes[node].f + kAabb[1];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            lo[k] = fminf(a[k], b[k]);
-            hi[k] = fmaxf(a[3 + k], b[3 + k]);
-        }
-        if (node == root) return;
-        p = parent[node];
-    }
-}
-
 // depth of every leaf (root's children = 1); out = max
 __global__ __launch_bounds__(kBlock) void k_depth(const uint32_t* __restrict__ parent, int B, int n,
                                                   unsigned* __restrict__ out) {
@@ -353,10 +308,46 @@ __global__ __launch_bounds__(kBlock) void k_obb(const void* __restrict__ leaves,
             float* f = nodes[node].f;
             *reinterpret_cast<float4*>(f) = make_float4(n32[0], n32[1], n32[2], t32[0]);
             *reinterpret_cast<float2*>(f + 4) = make_float2(t32[1], t32[2]);
-            *reinterpret_cast<float2*>(f + kObb[0]) = make_float2(ext[0][0], ext[0][1]);  // 14: 8-B aligned
-            *reinterpret_cast<float4*>(f + kObb[0] + 2) = make_float4(ext[0][2], ext[0][3], ext[0][4], ext[0][5]);
-            *reinterpret_cast<float2*>(f + kObb[1]) = make_float2(ext[1][0], ext[1][1]);  // 26
-            *reinterpret_cast<float4*>(f + kObb[1] + 2) = make_float4(ext[1][2], ext[1][3], ext[1][4], ext[1][5]);
+            // quantise both children's extents against base = min lower bound, scale 2^e per axis with
+            // 254 * 2^e >= range; lower codes round down and upper codes up, checked with the decoder's
+            // own expression, so the decoded box contains the fp32 one
+            float base[3];
+            int ex[3];
+            uint32_t u[12];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                base[k] = fminf(ext[0][k], ext[1][k]);
+                const double top = fmax((double)ext[0][3 + k], (double)ext[1][3 + k]);
+                const double range = top - (double)base[k];
+                int e = -126;
+                if (!(range < 1e38)) e = 127;
+                else
+                    while (e < 127 && 254.0 * (double)exp2_scale(e) < range) ++e;
+                ex[k] = e;
+                const float sc = exp2_scale(e);
+#pragma unroll
+                for (int side = 0; side < 2; ++side) {
+                    const float lo = ext[side][k], hi = ext[side][3 + k];
+                    double ql = floor(((double)lo - (double)base[k]) / (double)sc);
+                    double qh = ceil(((double)hi - (double)base[k]) / (double)sc);
+                    uint32_t ul = (uint32_t)fmin(fmax(ql, 0.0), 255.0), uh = (uint32_t)fmin(fmax(qh, 0.0), 255.0);
+                    while (ul > 0u && dequant(ul, sc, base[k]) > lo) --ul;
+                    while (uh < 255u && dequant(uh, sc, base[k]) < hi) ++uh;
+                    u[6 * side + k] = ul;
+                    u[6 * side + 3 + k] = uh;
+                }
+            }
+            f[kBase] = base[0];
+            f[kBase + 1] = base[1];
+            f[kBase + 2] = base[2];
+            uint32_t w[4];
+#pragma unroll
+            for (int j = 0; j < 3; ++j) w[j] = u[4 * j] | (u[4 * j + 1] << 8) | (u[4 * j + 2] << 16) | (u[4 * j + 3] << 24);
+            w[3] = ((uint32_t)(uint8_t)(int8_t)ex[0]) | ((uint32_t)(uint8_t)(int8_t)ex[1] << 8) |
+                   ((uint32_t)(uint8_t)(int8_t)ex[2] << 16);
+            *reinterpret_cast<float4*>(f + 11) = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]),
+                                                             __uint_as_float(w[2]), __uint_as_float(w[3]));
+            f[15] = 0.0f;
         }
     }
 }
@@ -503,11 +494,8 @@ int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T,
     uint32_t* parent = ws.vals.as<uint32_t>();
     k_karras<<<nblocks(T - 1), kBlock, 0, s>>>(keys, 1, (int)T, tree->d_nodes, parent, ws.ranges.as<int4>());
     MSH_HIP(hipGetLastError());
-    // refit
+    // node bounds come from k_obb (build_obb), after the leaves are packed
     uint32_t* flags = ws.flags.as<uint32_t>();
-    MSH_HIP(hipMemsetAsync(flags, 0, T * sizeof(uint32_t) + 64, s));
-    k_refit<<<nblocks(T), kBlock, 0, s>>>(d_lo, d_hi, d_order, 1, (int)T, tree->d_nodes, parent, flags, tree->d_orgs);
-    MSH_HIP(hipGetLastError());
     unsigned* d_depth = flags + T;
     MSH_HIP(hipMemsetAsync(d_depth, 0, sizeof(unsigned), s));
     k_depth<<<nblocks(T), kBlock, 0, s>>>(parent, 1, (int)T, d_depth);
@@ -577,10 +565,6 @@ int build_lbvh_batch(msh_tree* tree, const double* d_lo, const double* d_hi, siz
     MSH_HIP(hipGetLastError());
     MSH_TRY(ws.flags.reserve(nn * sizeof(uint32_t) + 64));
     uint32_t* flags = ws.flags.as<uint32_t>();
-    MSH_HIP(hipMemsetAsync(flags, 0, nn * sizeof(uint32_t) + 64, s));
-    k_refit<<<nblocks(n), kBlock, 0, s>>>(d_lo, d_hi, d_order, (int)B, (int)T, tree->d_nodes, parent, flags,
-                                          tree->d_orgs);
-    MSH_HIP(hipGetLastError());
     unsigned* d_depth = flags + nn;
     MSH_HIP(hipMemsetAsync(d_depth, 0, sizeof(unsigned), s));
     k_depth<<<nblocks(n), kBlock, 0, s>>>(parent, (int)B, (int)T, d_depth);

@@ -1,13 +1,14 @@
 // Shared device-side definitions for the MI355X (gfx950) point-to-mesh search engine.
 //
 // Data layout in HBM:
-//   BNode  — one LBVH internal node, 128 B = one L2 line: a node frame (unit normal n and tangent t of
-//            the node's triangles, area-weighted; b = n x t is recomputed), and for BOTH children an fp32
-//            AABB and the fp32 extents of the child's vertices along (n, t, b) — an oriented box that is
-//            thin along the surface normal — plus both child references.  All fp32 bounds are relative
-//            to the tree's fp64 `origin` (scene-box centre) and rounded outward, so every fp64 primitive
-//            lies inside every ancestor's bounds.  A traversal step is one coalesced 128-B read
-//            (8 x 16-B loads) that tests two children.
+//   BNode  — one LBVH internal node, 64 B: a node frame (unit normal n and tangent t of the node's
+//            triangles, area-weighted; b = n x t is recomputed), both child references, and for BOTH
+//            children the extents of the child's vertices along (n, t, b) — an oriented box that is thin
+//            along the surface normal — quantised to 8 bits per bound against a per-node fp32 base and a
+//            power-of-two scale per axis.  All bounds are relative to the tree's fp64 `origin`
+//            (scene-box centre) and rounded outward (the decoded fp32 value base + u * 2^e is <= every
+//            lower and >= every upper projection), so every fp64 primitive lies inside every ancestor's
+//            boxes.  A traversal step is one 64-B read (4 x 16-B loads) that bounds two children.
 //   TriRec — one leaf triangle, 80 B: the 9 fp64 vertex coordinates (exact copies of the input) +
 //            the original face index.  Leaves are stored in Morton order, so a subtree's
 //            triangles are contiguous.
@@ -28,15 +29,25 @@ constexpr int kBlock = 256;          // 4 waves of 64 lanes
 constexpr int kStack = MSH_STACK;           // per-lane LDS stack entries; deeper entries spill to global memory
 constexpr double kSlack = 1.0 + 9.094947017729282e-13;  // 1 + 2^-40: fp64 rounding margin for culls
 
-// float index within a node:  0-2 n | 3-5 t | 6 child0 | 7 child1 |
-//   8-13 child0 AABB (lo xyz, hi xyz) | 14-19 child0 oriented extents (lo n t b, hi n t b) |
-//  20-25 child1 AABB                  | 26-31 child1 oriented extents
+// float index within a node:  0-2 n | 3-5 t | 6 child0 | 7 child1 | 8-10 base (n, t, b) |
+//   bytes 44-55: u[side][6] quantised extents (lo n t b, hi n t b) of child 0 then child 1 |
+//   bytes 56-58: scale exponents e[3] (int8; scale = 2^e) | 59-63 zero
 struct alignas(16) BNode {
-    float f[32];
+    float f[16];
 };
-static_assert(sizeof(BNode) == 128, "BNode must be 128 B");
-constexpr int kAabb[2] = {8, 20};
-constexpr int kObb[2] = {14, 26};
+static_assert(sizeof(BNode) == 64, "BNode must be 64 B");
+constexpr int kBase = 8;      // float index of base[3]
+constexpr int kQuant = 44;    // byte offset of u[2][6]
+constexpr int kExp = 56;      // byte offset of e[3]
+
+// 2^e as an fp32 (e in [-126, 127])
+__host__ __device__ inline float exp2_scale(int e) {
+    union { uint32_t u; float f; } c;
+    c.u = (uint32_t)(e + 127) << 23;
+    return c.f;
+}
+// decoded bound: base + u * 2^e, one rounding (u * 2^e is exact); the build encodes with this expression
+__host__ __device__ inline float dequant(uint32_t u, float scale, float base) { return fmaf((float)u, scale, base); }
 
 struct alignas(16) TriRec {
     double v[9];
@@ -80,22 +91,38 @@ __host__ __device__ inline void frame_b(const float* n, const float* t, float* b
 
 // ---- node loads ----
 struct NodeV {
-    float4 q[8];
+    float4 q[4];
     __device__ float at(int i) const { return reinterpret_cast<const float*>(q)[i]; }
+    __device__ uint32_t word(int i) const { return __float_as_uint(at(i)); }
     __device__ int child(int s) const { return __float_as_int(at(6 + s)); }
+    // frame axes n, t and b = n x t
+    __device__ void frame(float* n, float* t, float* b) const {
+        n[0] = at(0); n[1] = at(1); n[2] = at(2);
+        t[0] = at(3); t[1] = at(4); t[2] = at(5);
+        frame_b(n, t, b);
+    }
+    // decoded oriented extents of both children: e0/e1 = lo n t b, hi n t b
+    __device__ void extents(float* e0, float* e1) const {
+        const uint32_t w0 = word(11), w1 = word(12), w2 = word(13), w3 = word(14);
+        const float sc[3] = {exp2_scale((int)(int8_t)(w3 & 0xffu)), exp2_scale((int)(int8_t)((w3 >> 8) & 0xffu)),
+                             exp2_scale((int)(int8_t)((w3 >> 16) & 0xffu))};
+        const float bs[3] = {at(kBase), at(kBase + 1), at(kBase + 2)};
+        const uint32_t u[12] = {w0 & 0xffu, (w0 >> 8) & 0xffu, (w0 >> 16) & 0xffu, w0 >> 24,
+                                w1 & 0xffu, (w1 >> 8) & 0xffu, (w1 >> 16) & 0xffu, w1 >> 24,
+                                w2 & 0xffu, (w2 >> 8) & 0xffu, (w2 >> 16) & 0xffu, w2 >> 24};
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            e0[k] = dequant(u[k], sc[k % 3], bs[k % 3]);
+            e1[k] = dequant(u[6 + k], sc[k % 3], bs[k % 3]);
+        }
+    }
 };
 __device__ inline NodeV load_node(const BNode* __restrict__ nodes, int i) {
     const float4* p = reinterpret_cast<const float4*>(nodes + i);
     NodeV n;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) n.q[k] = p[k];
+    for (int k = 0; k < 4; ++k) n.q[k] = p[k];
     return n;
-}
-// children and AABBs only (first 48 + 16 B are not enough: the AABBs sit at floats 8-13 and 20-25)
-__device__ inline void node_aabb(const NodeV& n, int s, float* lo, float* hi) {
-    const int o = kAabb[s];
-    lo[0] = n.at(o); lo[1] = n.at(o + 1); lo[2] = n.at(o + 2);
-    hi[0] = n.at(o + 3); hi[1] = n.at(o + 4); hi[2] = n.at(o + 5);
 }
 
 __device__ inline void load_tri(const TriRec* __restrict__ tris, int i, D3& a, D3& b, D3& c, uint32_t& face) {
@@ -252,29 +279,44 @@ __host__ __device__ inline float obb_d2_lo(const QF& q, const float* n, const fl
     return (gn * gn + gt * gt + gb * gb) * 0.999996185302734375f;  // 1 - 2^-18
 }
 
-// Both children's lower bounds from one node: max(AABB bound, oriented-box bound).
+// Both children's lower bounds from one node: the oriented-box bound of each child.  (Round 1 also kept
+// an fp32 AABB per child and used max(AABB, OBB): 4 % fewer node visits, but 9 % slower on C3 and twice
+// the node bytes.)
 __device__ inline void node_child_bounds(const NodeV& nd, const QF& q, float& d0, float& d1) {
-    const float n[3] = {nd.at(0), nd.at(1), nd.at(2)};
-    const float t[3] = {nd.at(3), nd.at(4), nd.at(5)};
-    float b[3];
-    frame_b(n, t, b);
-    float e0[6], e1[6];
-#pragma unroll
-    for (int k = 0; k < 6; ++k) {
-        e0[k] = nd.at(kObb[0] + k);
-        e1[k] = nd.at(kObb[1] + k);
-    }
-    const int a0 = kAabb[0], a1 = kAabb[1];
-#ifdef MSH_OBB_ONLY  // tuning experiment: oriented-box bound only
-    (void)a0; (void)a1;
+    float n[3], t[3], b[3], e0[6], e1[6];
+    nd.frame(n, t, b);
+    nd.extents(e0, e1);
     d0 = obb_d2_lo(q, n, t, b, e0);
     d1 = obb_d2_lo(q, n, t, b, e1);
-#else
-    d0 = fmaxf(box_d2_lo(q, nd.at(a0), nd.at(a0 + 1), nd.at(a0 + 2), nd.at(a0 + 3), nd.at(a0 + 4), nd.at(a0 + 5)),
-               obb_d2_lo(q, n, t, b, e0));
-    d1 = fmaxf(box_d2_lo(q, nd.at(a1), nd.at(a1 + 1), nd.at(a1 + 2), nd.at(a1 + 3), nd.at(a1 + 4), nd.at(a1 + 5)),
-               obb_d2_lo(q, n, t, b, e1));
-#endif
+}
+
+// fp64 oriented-box tools for the ray and triangle kernels (fp32 frame and extents widen exactly to fp64).
+// Projections of a point relative to the tree origin onto the node frame.
+struct FrameD {
+    D3 a[3];
+};
+__device__ inline FrameD frame_d(const NodeV& nd) {
+    float n[3], t[3], b[3];
+    nd.frame(n, t, b);
+    FrameD f;
+    f.a[0] = D3{n[0], n[1], n[2]};
+    f.a[1] = D3{t[0], t[1], t[2]};
+    f.a[2] = D3{b[0], b[1], b[2]};
+    return f;
+}
+// Lower bound of the squared distance from p (projections pp[3] onto the frame) to the oriented box ext:
+// gaps shrunk by a 2^-40 relative margin of the projections, the sum divided by lambda_max(A A^T) <= 1 + 1e-6
+// (covered by 1 - 2^-18).
+__device__ inline double obb_d2_lo_d(const double* pp, const float* ext) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double lo = ext[k], hi = ext[3 + k];
+        double g = fmax(fmax(lo - pp[k], pp[k] - hi), 0.0);
+        g = fmax(g - 9.094947017729282e-13 * (fabs(pp[k]) + fabs(lo) + fabs(hi)), 0.0);
+        s += g * g;
+    }
+    return s * 0.999996185302734375;  // 1 - 2^-18
 }
 
 // Leaf pretest of the exact policies.  Lower bound of the squared distance from the origin to

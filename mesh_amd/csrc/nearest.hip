@@ -429,7 +429,7 @@ __device__ inline void test_pending(Pol& pol, int& p0, int& p1) {
 __device__ inline D3 load_q(const KnnArgs& a, size_t i) { return D3{a.q[3 * i], a.q[3 * i + 1], a.q[3 * i + 2]}; }
 
 #ifndef MSH_LEAD
-#define MSH_LEAD 8
+#define MSH_LEAD 16
 #endif
 constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: leader ordering off)
 

@@ -16,9 +16,9 @@
 // the xy projection, but the segment lies ON the ray's line, so its denominator is the 2-D cross
 // product of two parallel vectors (0 up to rounding) and its point is not finite.
 //
-// Execution shape: one lane per ray, persistent near-first traversal over the same 128-B nodes as K2
-// (AABB part); box tests are fp64 slab tests on the fp32 (outward-padded) boxes with the ray's inverse
-// direction precomputed once per ray and a relative margin.  alongnormal rays are Morton-sorted by
+// Execution shape: one lane per ray, persistent near-first traversal over the same 64-B nodes as K2:
+// box tests are fp64 slab tests of the ray against each child's oriented box (the ray projected once
+// per node onto the node frame), with a relative margin.  alongnormal rays are Morton-sorted by
 // their source and gathered into slot order like K2's queries; visibility rays run vertex-major per
 // camera over a Morton order of the vertices (cached per tree), so neighbouring lanes cast
 // neighbouring, nearly parallel rays.
@@ -89,36 +89,37 @@ __device__ inline bool cgal_plane_line(const D3& p, const D3& d, const D3& a, co
 
 __device__ inline D3 ray_dir(const D3& p, const D3& v) { return vsub(vadd(p, v), p); }
 
-// Line p + t d with precomputed 1/d (inf for d == 0, zero flagged in `flat`).
-struct RayF {
-    D3 p, inv;
-    bool fx, fy, fz;
+// A line o + t d (o relative to the tree origin) projected onto a node frame: o_k = a_k . o, d_k = a_k . d,
+// inv_k = 1 / d_k (flat_k when d_k == 0).  One projection serves both children of a node.
+struct RayProj {
+    double o[3], inv[3];
+    bool flat[3];
 };
-__device__ inline RayF make_rayf(const D3& p, const D3& d) {
-    RayF r;
-    r.p = p;
-    r.fx = d.x == 0.0;
-    r.fy = d.y == 0.0;
-    r.fz = d.z == 0.0;
-    r.inv = D3{r.fx ? 0.0 : 1.0 / d.x, r.fy ? 0.0 : 1.0 / d.y, r.fz ? 0.0 : 1.0 / d.z};
+__device__ inline RayProj ray_proj(const FrameD& f, const D3& o, const D3& d) {
+    RayProj r;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        r.o[k] = vdot(f.a[k], o);
+        const double dk = vdot(f.a[k], d);
+        r.flat[k] = dk == 0.0;
+        r.inv[k] = r.flat[k] ? 0.0 : 1.0 / dk;
+    }
     return r;
 }
 
-// Slab test of the line, t in [tlo, thi], against an fp32 box; tnear = entry parameter.
-__device__ inline bool slab(const RayF& r, float lx, float ly, float lz, float hx, float hy, float hz, double tlo,
-                            double thi, double& tnear) {
-    const double po[3] = {r.p.x, r.p.y, r.p.z}, iv[3] = {r.inv.x, r.inv.y, r.inv.z};
-    const bool fl[3] = {r.fx, r.fy, r.fz};
-    const double lo[3] = {(double)lx, (double)ly, (double)lz}, hi[3] = {(double)hx, (double)hy, (double)hz};
+// Slab test of the line, t in [tlo, thi], against the oriented box {x : lo_k <= a_k . x <= hi_k};
+// tnear = entry parameter.  The slabs are widened by a 2^-40 relative margin for the fp64 projections.
+__device__ inline bool slab(const RayProj& r, const float* ext, double tlo, double thi, double& tnear) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        if (fl[k]) {
-            if (po[k] < lo[k] || po[k] > hi[k]) return false;
+        const double m = 9.094947017729282e-13 * (fabs((double)ext[k]) + fabs((double)ext[3 + k]) + fabs(r.o[k])) + 1e-300;
+        const double lo = (double)ext[k] - m, hi = (double)ext[3 + k] + m;
+        if (r.flat[k]) {
+            if (r.o[k] < lo || r.o[k] > hi) return false;
         } else {
-            double t1 = (lo[k] - po[k]) * iv[k], t2 = (hi[k] - po[k]) * iv[k];
-            const double a = fmin(t1, t2), b = fmax(t1, t2);
-            tlo = fmax(tlo, a);
-            thi = fmin(thi, b);
+            const double t1 = (lo - r.o[k]) * r.inv[k], t2 = (hi - r.o[k]) * r.inv[k];
+            tlo = fmax(tlo, fmin(t1, t2));
+            thi = fmin(thi, fmax(t1, t2));
         }
     }
     tnear = tlo;
@@ -139,11 +140,11 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
         const NodeV nd = load_node(nodes, node);
         if (STATS) ++n_nodes;
         double k0, k1;
-        float l0[3], u0[3], l1[3], u1[3];
-        node_aabb(nd, 0, l0, u0);
-        node_aabb(nd, 1, l1, u1);
-        bool h0 = pol.box(l0[0], l0[1], l0[2], u0[0], u0[1], u0[2], k0);
-        bool h1 = pol.box(l1[0], l1[1], l1[2], u1[0], u1[1], u1[2], k1);
+        float e0[6], e1[6];
+        nd.extents(e0, e1);
+        const RayProj rp = pol.project(frame_d(nd));
+        bool h0 = pol.box(rp, e0, k0);
+        bool h1 = pol.box(rp, e1, k1);
         const int c0 = nd.child(0), c1 = nd.child(1);
         if (h0 && c0 < 0) {
             pol.test(~c0);
@@ -190,17 +191,18 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
 struct AlongPol {
     const TriRec* __restrict__ tris;
     D3 p, dp, dm;
-    RayF rf;      // the line through p (relative to the tree origin: node bounds are origin-relative)
-    D3 pr;
+    D3 pr;        // p relative to the tree origin (node bounds are origin-relative)
     double best;  // distance
     uint32_t best_face;
     D3 best_pt;
     __device__ double lim2() const { return best == INFINITY ? INFINITY : best * best * kSlack; }
-    __device__ bool box(float lx, float ly, float lz, float hx, float hy, float hz, double& key) const {
-        key = box_d2(pr, lx, ly, lz, hx, hy, hz);
+    __device__ RayProj project(const FrameD& f) const { return ray_proj(f, pr, dp); }
+    // the line through p (both directions) meets the box, and the box is within the best distance
+    __device__ bool box(const RayProj& r, const float* ext, double& key) const {
+        key = obb_d2_lo_d(r.o, ext);
         if (key > lim2()) return false;
         double tn;
-        return slab(rf, lx, ly, lz, hx, hy, hz, -INFINITY, INFINITY, tn);
+        return slab(r, ext, -INFINITY, INFINITY, tn);
     }
     __device__ bool keep(double key) const { return key <= lim2(); }
     __device__ bool done() const { return false; }
@@ -230,11 +232,10 @@ struct AlongPol {
 struct AnyPol {
     const TriRec* __restrict__ tris;
     D3 src, d;
-    RayF rf;  // src relative to the tree origin
+    D3 sr;  // src relative to the tree origin
     bool hit;
-    __device__ bool box(float lx, float ly, float lz, float hx, float hy, float hz, double& key) const {
-        return slab(rf, lx, ly, lz, hx, hy, hz, 0.0, INFINITY, key);
-    }
+    __device__ RayProj project(const FrameD& f) const { return ray_proj(f, sr, d); }
+    __device__ bool box(const RayProj& r, const float* ext, double& key) const { return slab(r, ext, 0.0, INFINITY, key); }
     __device__ bool keep(double) const { return !hit; }
     __device__ bool done() const { return hit; }
     __device__ void test(int leaf) {
@@ -313,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
             const D3 p = D3{a.p[3 * i], a.p[3 * i + 1], a.p[3 * i + 2]};
             const D3 n = D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]};
             const D3 dp = ray_dir(p, n), pr = vsub(p, org);
-            AlongPol pol{a.tris, p, dp, ray_dir(p, D3{-n.x, -n.y, -n.z}), make_rayf(pr, dp), pr, INFINITY, MSH_NO_FACE,
+            AlongPol pol{a.tris, p, dp, ray_dir(p, D3{-n.x, -n.y, -n.z}), pr, INFINITY, MSH_NO_FACE,
                          D3{NAN, NAN, NAN}};
             if (finite_d3(p) && finite_d3(dp))
                 traverse_rays<AlongPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(kBlock) void k_rays(RayArgs a) {
             dir = D3{dir.x / len, dir.y / len, dir.z / len};
             const D3 src = vadd(vv, vscale(a.min_dist, dir));
             const D3 d = ray_dir(src, dir);
-            AnyPol pol{a.tris, src, d, make_rayf(vsub(src, org), d), false};
+            AnyPol pol{a.tris, src, d, vsub(src, org), false};
             if (finite_d3(src) && finite_d3(d))
                 traverse_rays<AnyPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
             if (STATS) continue;

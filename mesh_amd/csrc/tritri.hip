@@ -4,8 +4,8 @@
 //   * aabbtree_n_selfintersects (aabb_normals.cpp:192-207, AABB_n_tree.h:107-116): one lane per mesh
 //     triangle, pairs sharing an exactly equal vertex coordinate are skipped.
 // The overlap test is the orientation-predicate test of Guigue & Devillers (2003) evaluated in fp64,
-// with a 2-D edge/containment test for the coplanar case.  Boxes: closed fp64 overlap against the
-// outward-rounded fp32 node boxes.
+// with a 2-D edge/containment test for the coplanar case.  Boxes: closed fp64 separating-axis test of
+// the triangle against each child's outward-rounded oriented box, on the node frame's three axes.
 #include <algorithm>
 
 #include "internal.h"
@@ -124,10 +124,28 @@ __device__ bool tri_tri_overlap(const D3& p1, const D3& q1, const D3& r1, const 
     return coplanar_tri_tri(p1, q1, r1, p2, q2, r2, n1);
 }
 
-__device__ inline bool box_overlap(const double* lo, const double* hi, float lx, float ly, float lz, float hx, float hy,
-                                   float hz) {
-    return lo[0] <= (double)hx && (double)lx <= hi[0] && lo[1] <= (double)hy && (double)ly <= hi[1] &&
-           lo[2] <= (double)hz && (double)lz <= hi[2];
+// Interval of the query triangle (vertices relative to the tree origin) along each frame axis, widened
+// by a 2^-40 relative margin for the fp64 projections.
+struct TriProj {
+    double lo[3], hi[3];
+};
+__device__ inline TriProj tri_proj(const FrameD& f, const D3& a, const D3& b, const D3& c) {
+    TriProj r;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const double pa = vdot(f.a[k], a), pb = vdot(f.a[k], b), pc = vdot(f.a[k], c);
+        const double lo = fmin(fmin(pa, pb), pc), hi = fmax(fmax(pa, pb), pc);
+        const double m = 9.094947017729282e-13 * (fabs(lo) + fabs(hi)) + 1e-300;
+        r.lo[k] = lo - m;
+        r.hi[k] = hi + m;
+    }
+    return r;
+}
+// separating-axis test on the node frame's three axes: false only if the triangle and the child's oriented
+// box are disjoint along one of them
+__device__ inline bool obb_overlap(const TriProj& p, const float* ext) {
+    return p.lo[0] <= (double)ext[3] && (double)ext[0] <= p.hi[0] && p.lo[1] <= (double)ext[4] &&
+           (double)ext[1] <= p.hi[1] && p.lo[2] <= (double)ext[5] && (double)ext[2] <= p.hi[2];
 }
 
 struct TriArgs {
@@ -152,12 +170,10 @@ __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
         D3 qa, qb, qc;
         uint32_t qface;
         load_tri(a.q, (int)i, qa, qb, qc, qface);
-        // query box relative to the tree origin (node bounds are origin-relative and padded >= 1 fp32 ulp,
-        // far above the fp64 rounding of this subtraction)
-        const double lo[3] = {fmin(fmin(qa.x, qb.x), qc.x) - a.org[0], fmin(fmin(qa.y, qb.y), qc.y) - a.org[1],
-                              fmin(fmin(qa.z, qb.z), qc.z) - a.org[2]};
-        const double hi[3] = {fmax(fmax(qa.x, qb.x), qc.x) - a.org[0], fmax(fmax(qa.y, qb.y), qc.y) - a.org[1],
-                              fmax(fmax(qa.z, qb.z), qc.z) - a.org[2]};
+        // query vertices relative to the tree origin (node bounds are origin-relative and padded >= 1 fp32
+        // ulp, far above the fp64 rounding of this subtraction)
+        const D3 org = D3{a.org[0], a.org[1], a.org[2]};
+        const D3 ra = vsub(qa, org), rb = vsub(qb, org), rc = vsub(qc, org);
         bool hit = false;
         auto leaf_test = [&](int leaf) {
             D3 a0, a1, a2;
@@ -176,11 +192,11 @@ __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
             int node = 0, sp = 0;
             for (size_t guard = 0; guard < a.T; ++guard) {
                 const NodeV nd = load_node(a.nodes, node);
-                float l0[3], u0[3], l1[3], u1[3];
-                node_aabb(nd, 0, l0, u0);
-                node_aabb(nd, 1, l1, u1);
-                bool h0 = box_overlap(lo, hi, l0[0], l0[1], l0[2], u0[0], u0[1], u0[2]);
-                bool h1 = box_overlap(lo, hi, l1[0], l1[1], l1[2], u1[0], u1[1], u1[2]);
+                float e0[6], e1[6];
+                nd.extents(e0, e1);
+                const TriProj tp = tri_proj(frame_d(nd), ra, rb, rc);
+                bool h0 = obb_overlap(tp, e0);
+                bool h1 = obb_overlap(tp, e1);
                 const int c0 = nd.child(0), c1 = nd.child(1);
                 if (h0 && c0 < 0) { leaf_test(~c0); h0 = false; if (hit) break; }
                 if (h1 && c1 < 0) { leaf_test(~c1); h1 = false; if (hit) break; }

@@ -1,6 +1,7 @@
 """Diagnostic: download a built LBVH (via the blob API) and check every node's child bounds against the
-primitives below it: AABB containment/tightness and oriented-box (frame n, t, b = n x t) containment,
-child-pointer sanity and depth.  Prints one JSON line."""
+primitives below it: containment and tightness of the quantised oriented boxes (frame n, t, b = n x t;
+bound = base + u * 2^e decoded in fp32 exactly as the kernels do), child-pointer sanity and depth.
+Prints one JSON line."""
 import json
 import os
 import sys
@@ -19,7 +20,7 @@ def parse_blob(b):
     max_depth = int(np.frombuffer(b[8:16].tobytes(), dtype=np.int32)[1])
     off_nodes, off_leaves = int(hdr[11]), int(hdr[12])
     origin = np.frombuffer(b[112:136].tobytes(), dtype=np.float64)
-    nodes = np.frombuffer(b[off_nodes:off_nodes + (T - 1) * 128].tobytes(), dtype=np.float32).reshape(T - 1, 32)
+    nodes = np.frombuffer(b[off_nodes:off_nodes + (T - 1) * 64].tobytes(), dtype=np.uint8).reshape(T - 1, 64)
     leaves = np.frombuffer(b[off_leaves:off_leaves + T * 80].tobytes(), dtype=np.float64).reshape(T, 10)
     return T, max_depth, origin, nodes, leaves
 
@@ -32,7 +33,14 @@ def check_mesh(v, f):
     blob = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     _native.blob_pack(t, blob.data_ptr())
     T, max_depth, origin, nodes, leaves = parse_blob(blob.cpu().numpy())
-    child = nodes[:, 6:8].copy().view(np.int32)
+    fl = nodes.copy().view(np.float32)  # (T-1, 16)
+    child = fl[:, 6:8].copy().view(np.int32)
+    base = fl[:, 8:11]
+    u = nodes[:, 44:56].reshape(T - 1, 2, 6).astype(np.float32)
+    ex = nodes[:, 56:59].copy().view(np.int8).astype(np.int32)
+    scale = np.ldexp(np.float32(1.0), ex).astype(np.float32)  # (T-1, 3)
+    # base + u * 2^e in fp32: the product is exact, the sum rounds once (as fmaf in the kernels)
+    dec = (np.tile(base, 2)[:, None, :] + u * np.tile(scale, 2)[:, None, :]).astype(np.float32)  # (T-1, 2, 6)
     tri = leaves[:, :9].reshape(T, 3, 3) - origin
     llo, lhi = tri.min(1), tri.max(1)
     # leaf ranges by post-order
@@ -51,31 +59,34 @@ def check_mesh(v, f):
             else:
                 lo_.append(~c); hi_.append(~c)
         rng_lo[x], rng_hi[x] = min(lo_), max(hi_)
-    aabb_bad = obb_bad = 0
+    obb_bad = 0
     loose = []
     for x in range(T - 1):
-        nf, tf = nodes[x, 0:3].astype(np.float64), nodes[x, 3:6].astype(np.float64)
-        b = np.array([nodes[x, 1] * nodes[x, 5] - nodes[x, 2] * nodes[x, 4],
-                      nodes[x, 2] * nodes[x, 3] - nodes[x, 0] * nodes[x, 5],
-                      nodes[x, 0] * nodes[x, 4] - nodes[x, 1] * nodes[x, 3]], dtype=np.float32).astype(np.float64)
+        nf, tf = fl[x, 0:3].astype(np.float64), fl[x, 3:6].astype(np.float64)
+        b = np.array([fl[x, 1] * fl[x, 5] - fl[x, 2] * fl[x, 4],
+                      fl[x, 2] * fl[x, 3] - fl[x, 0] * fl[x, 5],
+                      fl[x, 0] * fl[x, 4] - fl[x, 1] * fl[x, 3]], dtype=np.float32).astype(np.float64)
         A = np.stack([nf, tf, b])
+        prs = []
         for s in (0, 1):
             c = child[x, s]
             a, e = (rng_lo[c], rng_hi[c]) if c >= 0 else (~c, ~c)
             pts = tri[a:e + 1].reshape(-1, 3)
-            ab = nodes[x, 8 + 12 * s: 14 + 12 * s].astype(np.float64)
-            ob = nodes[x, 14 + 12 * s: 20 + 12 * s].astype(np.float64)
-            if np.any(pts.min(0) < ab[:3]) or np.any(pts.max(0) > ab[3:]):
-                aabb_bad += 1
-            pr = pts @ A.T
+            prs.append(pts @ A.T)
+        union = np.maximum(np.maximum(prs[0].max(0), prs[1].max(0)) - np.minimum(prs[0].min(0), prs[1].min(0)), 1e-12)
+        for s in (0, 1):
+            ob = dec[x, s].astype(np.float64)
+            pr = prs[s]
             if np.any(pr.min(0) < ob[:3]) or np.any(pr.max(0) > ob[3:]):
                 obb_bad += 1
             if x < 2000:
-                ext = max(float((pts.max(0) - pts.min(0)).max()), 1e-12)
-                loose.append(float(max((pts.min(0) - ab[:3]).max(), (ab[3:] - pts.max(0)).max()) / ext))
-    res = {"T": T, "max_depth": max_depth, "reached_nodes": len(order), "aabb_containment_violations": aabb_bad,
-           "obb_containment_violations": obb_bad, "worst_relative_aabb_looseness_first2000": max(loose),
-           "origin": origin.tolist()}
+                # slack of each bound relative to the node's range along that axis (one code step <= 2/254)
+                # (less the fp32 outward rounding of the unquantised bound: 4 ulps of its magnitude)
+                ulp = 4.0 * np.spacing(np.abs(ob).astype(np.float32)).astype(np.float64)
+                loose.append(float(max(((pr.min(0) - ob[:3] - ulp[:3]) / union).max(),
+                                       ((ob[3:] - pr.max(0) - ulp[3:]) / union).max())))
+    res = {"T": T, "max_depth": max_depth, "reached_nodes": len(order), "obb_containment_violations": obb_bad,
+           "worst_relative_obb_looseness_first2000": max(loose), "origin": origin.tolist()}
     return res
 
 

@@ -140,7 +140,7 @@ def test_blob_and_shards_world2():
     assert infos[0] == infos[1]
     info = infos[0]
     assert info["kind"] == 0 and info["n_points"] == 50002 and info["n_faces"] == 100000
-    assert info["node_bytes"] == 128 and info["leaf_bytes"] == 80
+    assert info["node_bytes"] == 64 and info["leaf_bytes"] == 80
     assert info["off_nodes"] >= info["off_vertices"] + 50002 * 24
     assert info["off_leaves"] >= info["off_nodes"] + (100000 - 1) * info["node_bytes"]
     assert info["total"] >= info["off_leaves"] + 100000 * 80

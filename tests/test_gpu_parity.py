@@ -389,7 +389,7 @@ def test_device_api_matches_host_api():
 
 @pytest.mark.parametrize("name", ["ico", "c2", "offset"])
 def test_tree_bounds_contain_primitives(name):
-    # every child AABB and oriented box (frame n, t, n x t) contains all vertices below it
+    # every child's quantised oriented box (frame n, t, n x t) contains all vertices below it
     from scripts.check_tree import check_mesh
     if name == "ico":
         v, f = W.geodesic_icosphere(20)
@@ -399,9 +399,11 @@ def test_tree_bounds_contain_primitives(name):
         v, f = W.geodesic_icosphere(10)
         v = v * 0.01 + np.array([1e5, -3e4, 2e5])
     r = check_mesh(v, f)
-    assert r["aabb_containment_violations"] == 0 and r["obb_containment_violations"] == 0, r
+    assert r["obb_containment_violations"] == 0, r
     assert r["reached_nodes"] == f.shape[0] - 1
-    assert r["worst_relative_aabb_looseness_first2000"] < 1e-3, r
+    # 8-bit codes: a bound moves outward by at most one code step, 2^e < 2/254 of the node's range along
+    # that axis (plus the fp32 outward rounding)
+    assert r["worst_relative_obb_looseness_first2000"] < 2.2 / 254, r
 
 
 def test_many_tied_candidates(oracle):
