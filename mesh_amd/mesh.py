@@ -1,5 +1,5 @@
 """Minimal ``Mesh`` facade carrying the search / visibility methods of psbody-mesh's ``Mesh``
-(mesh/mesh.py:48-80 for v/f coercion, :208-222, :282-302, :439-455).  Only the hot-path callers are
+(mesh/mesh.py:48-80 for v/f coercion, :208-248, :282-302, :439-455).  Only the hot-path callers are
 mirrored; I/O, topology, texture and viewing are out of scope.
 """
 import numpy as np
@@ -45,6 +45,44 @@ class Mesh(object):
         b2 = np.sum(np.cross(u, wp) * n, axis=1) * oneOver4ASquared
         b1 = np.sum(np.cross(wp, w) * n, axis=1) * oneOver4ASquared
         return vertex_indices, np.array((1 - b1 - b2, b1, b2)).T
+
+    # ---- segmentation transfer (mesh.py:224-248), a caller of the closest-face query ----
+    def parts_by_face(self):
+        """Part name of every face ('' for a face in no part), mesh.py:243-248."""
+        segments_by_face = [''] * len(self.f)
+        for part in self.segm.keys():
+            for face in self.segm[part]:
+                segments_by_face[face] = part
+        return segments_by_face
+
+    def transfer_segm(self, mesh, exclude_empty_parts=True):
+        """Give every face of this mesh the part of the face of `mesh` closest to its centre
+        (mesh.py:224-237).  The centres are computed vectorised with the reference's operation order
+        (a face's mean is (v0 + v1 + v2) / 3, as np.mean over its 3 rows), all centres go to the GPU in
+        one closest-face query, and the faces are grouped per part with a stable sort (each part's
+        list ascending, as the reference's sorted lists).  A face whose closest face of `mesh` is in no
+        part raises KeyError(''), as the reference's segm[''] lookup does."""
+        self.segm = {}
+        if not hasattr(mesh, 'segm'):
+            return
+        v = np.asarray(self.v, dtype=np.float64)
+        f = np.asarray(self.f).astype(np.int64)
+        centres = (v[f[:, 0]] + v[f[:, 1]] + v[f[:, 2]]) / 3.0
+        closest_faces, _ = mesh.closest_faces_and_points(centres)
+        names = list(mesh.segm.keys())
+        part_of = np.full(len(mesh.f), -1, dtype=np.int64)
+        for k, part in enumerate(names):  # later parts win, as in parts_by_face
+            part_of[np.asarray(mesh.segm[part], dtype=np.int64)] = k
+        pid = part_of[np.asarray(closest_faces).ravel().astype(np.int64)]
+        if (pid < 0).any():
+            raise KeyError('')
+        order = np.argsort(pid, kind='stable')
+        bounds = np.searchsorted(pid[order], np.arange(len(names) + 1))
+        self.segm = dict((part, order[bounds[k]:bounds[k + 1]].tolist()) for k, part in enumerate(names))
+        if exclude_empty_parts:
+            for part in list(self.segm.keys()):
+                if not self.segm[part]:
+                    del self.segm[part]
 
     # ---- visibility (mesh.py:282-302) ----
     def vertex_visibility(self, camera, normal_threshold=None, omni_directional_camera=False, binary_visiblity=True):

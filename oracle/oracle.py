@@ -281,3 +281,27 @@ def barycentric_coordinates_for_points(v, f, points, face_indices):
     vi = np.asarray(f)[np.asarray(face_indices).flatten(), :]
     a, b, c = v[vi[:, 0]], v[vi[:, 1]], v[vi[:, 2]]
     return vi, barycentric_coordinates_of_projection(points, a, b - a, c - a)
+
+
+def transfer_segm(v, f, mesh_segm, closest_faces, exclude_empty_parts=True):
+    """Mesh.transfer_segm (mesh.py:224-237) as the reference writes it, with the closest faces supplied
+    (the reference gets them from mesh.closest_faces_and_points(face_centres))."""
+    n_mesh_faces = 1 + max((max(x) for x in mesh_segm.values() if len(x)), default=0)
+    segments_by_face = [''] * max(n_mesh_faces, int(np.max(closest_faces)) + 1)
+    for part in mesh_segm.keys():
+        for face in mesh_segm[part]:
+            segments_by_face[face] = part
+    parts_by_face = [segments_by_face[face] for face in np.asarray(closest_faces).flatten()]
+    segm = dict([(part, []) for part in mesh_segm.keys()])
+    for face, part in enumerate(parts_by_face):
+        segm[part].append(face)
+    for part in list(segm.keys()):
+        segm[part].sort()
+        if exclude_empty_parts and not segm[part]:
+            del segm[part]
+    return segm
+
+
+def face_centres(v, f):
+    """np.array([v[face, :].mean(axis=0) for face in f]) (mesh.py:227)."""
+    return np.array([np.asarray(v)[face, :].mean(axis=0) for face in np.asarray(f)])

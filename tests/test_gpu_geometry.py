@@ -1,4 +1,4 @@
-"""GPU parity of the geometry that feeds and consumes the search path (SURVEY.md §8f rows 1-2).
+"""GPU parity of the geometry that feeds and consumes the search path (SURVEY.md §8f rows 1, 2 and 4).
 
 * fused barycentrics: ``aabbtree_nearest_barycentric`` / ``AabbTreeBatch.nearest_barycentric`` return the
   closest face and point (bit-exact vs the exhaustive oracle) plus Heidrich weights that must equal the
@@ -7,6 +7,8 @@
   The restatement itself is pinned by tests/test_geometry.py:70-104's known answers (test_oracle.py).
 * vertex normals: ``Mesh.estimate_vertex_normals`` (GPU) must equal the scipy-sparse restatement of
   mesh.py:208-216 bit for bit, and meet tests/test_mesh.py:111-118 / test_geometry.py:61-68.
+* transfer_segm: ``Mesh.transfer_segm`` (GPU closest faces of the face centres) must give the same part
+  lists as the reference's loop (mesh.py:224-237, restated in the oracle) on exhaustive closest faces.
 """
 import numpy as np
 import pytest
@@ -142,3 +144,29 @@ def test_vertex_normals_c5_size(oracle):
     vn = Mesh(v=v, f=f).estimate_vertex_normals()
     ref = oracle.estimate_vertex_normals(v, f)
     assert np.array_equal(vn, ref)
+
+
+# ---------------------------------------------------------------- transfer_segm
+@pytest.mark.parametrize("exclude", [True, False])
+def test_transfer_segm(oracle, exclude):
+    from mesh_amd.mesh import Mesh
+    # source mesh: C2 stand-in with a segmentation by height band (one empty part); target: a finer
+    # noisy sphere around it
+    v, f = W.c2_mesh()
+    src = Mesh(v=v, f=f)
+    zc = (v[f[:, 0], 2] + v[f[:, 1], 2] + v[f[:, 2], 2]) / 3.0
+    bands = np.digitize(zc, np.quantile(zc, [0.2, 0.5, 0.8]))
+    src.segm = {"feet": np.nonzero(bands == 0)[0].tolist(), "legs": np.nonzero(bands == 1)[0].tolist(),
+                "torso": np.nonzero(bands == 2)[0].tolist(), "head": np.nonzero(bands == 3)[0].tolist(),
+                "nothing": []}
+    tv, tf = W.geodesic_icosphere(30)
+    tv = tv * np.array([0.6, 1.7, 0.3]) * 1.01
+    tgt = Mesh(v=tv, f=tf)
+    tgt.transfer_segm(src, exclude_empty_parts=exclude)
+    centres = oracle.face_centres(tv, tf)
+    bf, _, _, _ = oracle.brute_nearest(v, f, centres)
+    want = oracle.transfer_segm(tv, tf, src.segm, bf, exclude_empty_parts=exclude)
+    assert list(tgt.segm.keys()) == list(want.keys())
+    for k in want:
+        assert tgt.segm[k] == want[k], k
+    assert ("nothing" in tgt.segm) == (not exclude)
