@@ -198,6 +198,29 @@ int msh_blob_header_write(int kind, uint64_t P, uint64_t T, uint64_t T_main, voi
                           msh_blob_info* info);
 int msh_blob_header_parse(const void* src, size_t bytes, msh_blob_info* info);
 
+/* ---- mesh files feeding the path (host parsing) ----
+ * OBJ: replaces psbody.mesh.serialization.loadobj (mesh/src/py_loadobj.cpp:62-243).  sizes[9] = v rows,
+ * vt rows, vt columns, vn rows, f rows, ft rows, fn rows, groups, landmarks.  Arrays are row-major
+ * (rows x 3, vt rows x vt columns); groups and landmarks are enumerated in name order (std::map, as the
+ * reference).  Errors: "Could not load file". */
+typedef struct msh_obj msh_obj;
+int msh_obj_load(const char* path, msh_obj** out);
+int msh_obj_sizes(const msh_obj* obj, uint64_t* sizes);
+int msh_obj_arrays(const msh_obj* obj, double* v, double* vt, double* vn, uint32_t* f, uint32_t* ft, uint32_t* fn);
+const char* msh_obj_mtl_path(const msh_obj* obj);
+int msh_obj_group(const msh_obj* obj, size_t k, const char** name, uint64_t* n_faces, const uint32_t** faces);
+int msh_obj_landmark(const msh_obj* obj, size_t k, const char** name, uint32_t* vertex);
+void msh_obj_free(msh_obj* obj);
+/* PLY: replaces psbody.mesh.serialization.plyutils.read (mesh/src/plyutils.c:64-139 over rply.c).
+ * sizes[4] = vertices, faces, has colour, has normals; v / colour / normals (P,3), tri (F,3) as double
+ * (items 0..2 of each face list).  Errors: "Failed to open PLY file.", "plyread_mex: Bad raw header.",
+ * "Read failed. <path>". */
+typedef struct msh_ply msh_ply;
+int msh_ply_load(const char* path, msh_ply** out);
+int msh_ply_sizes(const msh_ply* ply, uint64_t* sizes);
+int msh_ply_arrays(const msh_ply* ply, double* v, double* tri, double* color, double* normals);
+void msh_ply_free(msh_ply* ply);
+
 /* ---- kernel timing (HIP events on the launch stream; used by bench.py's roofline) ---- */
 int msh_timing_enable(int on);
 /* Total milliseconds and launch count of kernel `name` ("nearest", "sort", "morton") since reset. */

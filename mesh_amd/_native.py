@@ -65,6 +65,17 @@ SIGNATURES = [
     ("msh_batch_nearest_bary_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     ("msh_blob_header_write", _i, [_i, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp, _sz, _vp]),
     ("msh_blob_header_parse", _i, [_vp, _sz, _vp]),
+    ("msh_obj_load", _i, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    ("msh_obj_sizes", _i, [_vp, _c_u64_p]),
+    ("msh_obj_arrays", _i, [_vp, _c_double_p, _c_double_p, _c_double_p, _c_u32_p, _c_u32_p, _c_u32_p]),
+    ("msh_obj_mtl_path", ctypes.c_char_p, [_vp]),
+    ("msh_obj_group", _i, [_vp, _sz, ctypes.POINTER(ctypes.c_char_p), _c_u64_p, ctypes.POINTER(_c_u32_p)]),
+    ("msh_obj_landmark", _i, [_vp, _sz, ctypes.POINTER(ctypes.c_char_p), _c_u32_p]),
+    ("msh_obj_free", None, [_vp]),
+    ("msh_ply_load", _i, [ctypes.c_char_p, ctypes.POINTER(_vp)]),
+    ("msh_ply_sizes", _i, [_vp, _c_u64_p]),
+    ("msh_ply_arrays", _i, [_vp, _c_double_p, _c_double_p, _c_double_p, _c_double_p]),
+    ("msh_ply_free", None, [_vp]),
     ("msh_timing_enable", _i, [_i]),
     ("msh_timing_get", _i, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_double), _c_i64_p]),
     ("msh_timing_reset", _i, []),

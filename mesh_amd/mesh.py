@@ -9,13 +9,50 @@ from . import search
 
 
 class Mesh(object):
-    def __init__(self, v=None, f=None, vn=None):
+    def __init__(self, v=None, f=None, vn=None, filename=None):
+        if filename is not None:
+            self.load_from_file(filename)
         if v is not None:
             self.v = np.array(v, dtype=np.float64)
         if f is not None:
             self.f = np.require(f, dtype=np.uint32)
         if vn is not None:
             self.vn = np.array(vn, dtype=np.float64)
+
+    # ---- mesh files (serialization.py:97-131, 410-445) through the native readers ----
+    def load_from_file(self, filename):
+        if filename.endswith(".ply"):
+            self.load_from_ply(filename)
+        elif filename.endswith(".obj"):
+            self.load_from_obj(filename)
+        else:
+            raise NotImplementedError("Unknown mesh file format.")
+
+    def load_from_obj(self, filename):
+        """Geometry, groups and landmarks of load_from_obj_cpp (serialization.py:97-131); materials and
+        textures are out of scope."""
+        from collections import OrderedDict
+        from .serialization.loadobj import loadobj
+        v, vt, vn, f, ft, fn, mtl_path, landm, segm = loadobj(filename)
+        for name, a in (("v", v), ("f", f), ("vn", vn), ("vt", vt), ("fn", fn), ("ft", ft)):
+            if a.size != 0:
+                setattr(self, name, a)
+        if segm:
+            self.segm = OrderedDict((k, x.tolist()) for k, x in segm.items())
+        if landm:
+            self.landm = landm
+            self.landm_xyz = dict((k, self.v[i]) for k, i in landm.items())
+
+    def load_from_ply(self, filename):
+        """serialization.py:426-445: v, f, vertex colours / 255, normals."""
+        from .serialization import plyutils
+        v, tri, color, normals = plyutils.read_arrays(filename)
+        self.v = v
+        self.f = tri.copy()
+        if color is not None:
+            self.vc = color / 255
+        if normals is not None:
+            self.vn = normals
 
     # ---- geometry helpers used by the callers (mesh.py:208-222) ----
     def estimate_vertex_normals(self):

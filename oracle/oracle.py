@@ -305,3 +305,179 @@ def transfer_segm(v, f, mesh_segm, closest_faces, exclude_empty_parts=True):
 def face_centres(v, f):
     """np.array([v[face, :].mean(axis=0) for face in f]) (mesh.py:227)."""
     return np.array([np.asarray(v)[face, :].mean(axis=0) for face in np.asarray(f)])
+
+
+# ---- mesh files (pure-Python restatements of the reference readers; small files only) -------------
+def loadobj(path):
+    """mesh/src/py_loadobj.cpp:62-243, line for line: returns (v, vt, vn, f, ft, fn, mtl_path, landm, segm)."""
+    import re
+    num = re.compile(r"[+-]?(\d+\.?\d*|\.\d+)([eE][+-]?\d+)?")
+
+    def doubles(s):
+        out = []
+        for tok in s.split():
+            m = num.match(tok)
+            if not m:
+                break
+            if m.group(0) in ("+", "-"):
+                break
+            out.append(float(m.group(0)))
+            if m.end() != len(tok):
+                break
+        return out
+
+    def atoi(s):
+        m = re.match(r"\s*([+-]?\d+)", s)
+        return int(m.group(1)) if m else 0
+
+    v, vt, vn, f, ft, fn = [], [], [], [], [], []
+    segm, landm = {}, {}
+    next_v_is_land, land_name, curr, mtl, len_vt = False, "", "", "", 3
+    with open(path, "rb") as fh:
+        data = fh.read().decode("latin-1")
+    lines = data.split("\n")
+    if lines and lines[-1] == "":
+        lines.pop()
+    for line in lines:
+        if line[:6] == "mtllib":
+            mtl = line[6:]
+        if line[:1] == "g":
+            curr = line[2:]
+            segm.setdefault(curr, [])
+        if line[:2] == "vt":
+            x = doubles(line[2:])
+            vt += x
+            len_vt = len(x)
+        elif line[:2] == "vn":
+            vn += doubles(line[2:])
+        elif line[:1] == "f":
+            lf, lt, ln = [], [], []
+            for tok in line[1:].split():
+                parts = tok.split("/")
+                if parts and parts[-1] == "" and len(parts) > 1:
+                    parts = parts[:-1]  # getline yields no empty tail after a trailing '/'
+                for counter, el in enumerate(parts):
+                    if el and counter < 3:
+                        (lf, lt, ln)[counter].append(atoi(el))
+            for (loc, dst) in ((lf, f), (lt, ft), (ln, fn)):
+                for i in range(1, len(loc) - 1):
+                    dst += [(loc[0] - 1) & 0xFFFFFFFF, (loc[i] - 1) & 0xFFFFFFFF, (loc[i + 1] - 1) & 0xFFFFFFFF]
+                    if dst is f and curr != "":
+                        segm[curr].append(len(f) // 3 - 1)
+        elif line[:1] == "v":
+            v += doubles(line[1:])
+            if next_v_is_land:
+                next_v_is_land = False
+                landm[land_name] = len(v) // 3 - 1
+        elif line[:9] == "#landmark":
+            next_v_is_land = True
+            land_name = line[10:]
+    nv, nvn = len(v) // 3, len(vn) // 3
+    nvt = len(vt) // len_vt if len_vt else 0
+    return (np.array(v[:3 * nv], dtype=np.float64).reshape(nv, 3),
+            np.array(vt[:nvt * len_vt], dtype=np.float64).reshape(nvt, len_vt),
+            np.array(vn[:3 * nvn], dtype=np.float64).reshape(nvn, 3),
+            np.array(f, dtype=np.uint32).reshape(-1, 3), np.array(ft, dtype=np.uint32).reshape(-1, 3),
+            np.array(fn, dtype=np.uint32).reshape(-1, 3), mtl, dict(sorted(landm.items())),
+            dict((k, np.array(x, dtype=np.uint32)) for k, x in sorted(segm.items())))
+
+
+def ply_read(path):
+    """plyutils.read (mesh/src/plyutils.c:64-139) over rply's reader: dict of lists of floats, or raises
+    ValueError with the reference's message."""
+    import struct
+    with open(path, "rb") as fh:
+        data = fh.read()
+    if data[:4] != b"ply\n":
+        raise ValueError("Failed to open PLY file.")
+    pos = 4
+    mode, elems = None, []
+    types = {"int8": "b", "char": "b", "uint8": "B", "uchar": "B", "int16": "h", "short": "h", "uint16": "H",
+             "ushort": "H", "int32": "i", "int": "i", "uint32": "I", "uint": "I", "float32": "f", "float": "f",
+             "float64": "d", "double": "d"}
+    ok = False
+    while True:
+        nl = data.find(b"\n", pos)
+        if nl < 0:
+            break
+        w = data[pos:nl].decode("latin-1").replace("\r", " ").split()
+        pos = nl + 1
+        if not w:
+            continue
+        if w[0] == "end_header":
+            ok = True
+            break
+        if w[0] in ("comment", "obj_info"):
+            continue
+        if w[0] == "format" and len(w) >= 3 and w[2] == "1.0" and w[1] in ("ascii", "binary_little_endian",
+                                                                          "binary_big_endian"):
+            mode = w[1]
+        elif w[0] == "element" and len(w) == 3:
+            elems.append([w[1], int(w[2]), []])
+        elif w[0] == "property" and elems and len(w) == 5 and w[1] == "list" and w[2] in types and w[3] in types:
+            elems[-1][2].append((w[4], types[w[2]], types[w[3]]))
+        elif w[0] == "property" and elems and len(w) == 3 and w[1] in types:
+            elems[-1][2].append((w[2], None, types[w[1]]))
+        else:
+            break
+    if not ok or mode is None:
+        raise ValueError("plyread_mex: Bad raw header.")
+    body = data[pos:]
+    ascii_words = body.decode("latin-1").split() if mode == "ascii" else None
+    wi = [0]
+    bo = [0]
+    end = "<" if mode == "binary_little_endian" else ">"
+    lims = {"b": (-128, 127), "B": (0, 255), "h": (-32768, 32767), "H": (0, 65535),
+            "i": (-2 ** 31, 2 ** 31 - 1), "I": (0, 2 ** 32 - 1), "f": (-3.4028234663852886e38, 3.4028234663852886e38),
+            "d": (-np.inf, np.inf)}
+
+    def val(t):
+        if ascii_words is not None:
+            if wi[0] >= len(ascii_words):
+                raise ValueError("Read failed. " + path)
+            s = ascii_words[wi[0]]
+            wi[0] += 1
+            try:
+                x = float(s) if t in "fd" else float(int(s, 10))
+            except ValueError:
+                raise ValueError("Read failed. " + path)
+            if not (lims[t][0] <= x <= lims[t][1]):
+                raise ValueError("Read failed. " + path)
+            return x
+        n = struct.calcsize(t)
+        if bo[0] + n > len(body):
+            raise ValueError("Read failed. " + path)
+        x = struct.unpack(end + t, body[bo[0]:bo[0] + n])[0]
+        bo[0] += n
+        return float(x)
+
+    vert = next((e for e in elems if e[0] == "vertex"), None)
+    face = next((e for e in elems if e[0] == "face"), None)
+    names = [p[0] for p in vert[2]] if vert else []
+    has_color = any(n in names for n in ("red", "green", "blue"))
+    has_normals = any(n in names for n in ("nx", "ny", "nz"))
+    fnames = [p[0] for p in face[2]] if face else []
+    fprop = "vertex_indices" if ("vertex_indices" in fnames and face[1] > 0) else "vertex_index"
+    nv = vert[1] if vert else 0
+    nf = face[1] if (face and fprop in fnames) else 0
+    cols = {k: [float("nan")] * nv for k in ("x", "y", "z", "red", "green", "blue", "nx", "ny", "nz")}
+    tri = [[float("nan")] * nf for _ in range(3)]
+    for e in elems:
+        for i in range(e[1]):
+            for (name, ct, it) in e[2]:
+                if ct is None:
+                    x = val(it)
+                    if e is vert and name in cols:
+                        cols[name][i] = x
+                else:
+                    c = int(val(ct))
+                    for k in range(c):
+                        x = val(it)
+                        if e is face and name == fprop and k < 3:
+                            tri[k][i] = x
+    res = {"pts": [cols["x"], cols["y"], cols["z"]], "tri": tri}
+    if has_color:
+        res["color"] = [cols["red"], cols["green"], cols["blue"]]
+    if has_normals:
+        res["normals"] = [cols["nx"], cols["ny"], cols["nz"]]
+    return res

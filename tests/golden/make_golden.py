@@ -13,6 +13,7 @@ Outputs (data only — inputs and expected outputs, no reference source):
                    tests/test_visibility.py:13-53, tests/test_intersections.py:27,
                    tests/test_geometry.py:61-104 and tests/test_mesh.py:111-118 (normals, barycentrics)
                    (the icosphere of mesh/sphere.py:19-57 is stored as data too)
+  data/*.obj|ply   the reference's own mesh fixture files (native OBJ / PLY reader tests)
   kdtree.npz       scipy.spatial.KDTree answers for ClosestPointTree (search.py:52-65) on the
                    sphere fixture (scipy is the third-party arithmetic that path uses)
 """
@@ -115,6 +116,15 @@ REF_TESTS = {
     "test_estimate_vertex_normals": {"mesh": "sphere", "mse_max": 0.05},
     # tests/test_geometry.py:61-68: estimate_vertex_normals == VertNormals within 1e-15 (sphere fixture)
     "test_vert_normals": {"mesh": "sphere", "tol": 1e-15},
+    # tests/test_mesh.py:17-26,35-47: test_box.obj / test_box.ply loaded by the native readers
+    "test_load_box": {
+        "v": [[0.5, 0.5, 0.5], [-0.5, 0.5, 0.5], [0.5, -0.5, 0.5], [-0.5, -0.5, 0.5], [0.5, 0.5, -0.5],
+              [-0.5, 0.5, -0.5], [0.5, -0.5, -0.5], [-0.5, -0.5, -0.5]],
+        "f": [[0, 1, 2], [3, 2, 1], [0, 2, 4], [6, 4, 2], [0, 4, 1], [5, 1, 4], [7, 5, 6], [4, 6, 5], [7, 6, 3],
+              [2, 3, 6], [7, 3, 5], [1, 5, 3]],
+        "segm": {"a": [0, 1, 2, 3, 4, 5], "b": [6, 10, 11], "c": [7, 8, 9]},
+        "landm": {"pospospos": 0, "negnegneg": 7},
+    },
     # tests/test_intersections.py:27 (disabled in the reference; verified by brute force in SURVEY §4)
     "test_intersections": {"q_center": [-1, 0, 0], "m_center": [1, 0, 0], "radius": 2,
                            "expected": [2, 4, 5, 6, 16, 25, 26, 27, 36, 37, 38, 40, 58, 60, 61, 63, 76, 77, 79]},
@@ -132,6 +142,12 @@ def main():
     arrays["icosphere_v"] = np.array(ICO_V, dtype=np.float64)
     arrays["icosphere_f"] = np.array(ICO_F, dtype=np.uint32) - 1
     np.savez_compressed(os.path.join(HERE, "meshes.npz"), **arrays)
+    # the reference's mesh files themselves (inputs of the native-reader tests)
+    os.makedirs(os.path.join(HERE, "data"), exist_ok=True)
+    for name in sorted(os.listdir(REF_DATA)):
+        if name.endswith((".obj", ".ply")):
+            with open(os.path.join(REF_DATA, name), "rb") as src, open(os.path.join(HERE, "data", name), "wb") as dst:
+                dst.write(src.read())
     with open(os.path.join(HERE, "ref_tests.json"), "w") as fh:
         json.dump(REF_TESTS, fh, indent=1)
 
