@@ -15,12 +15,12 @@
 //   Pass 1 (k_knn): persistent grid; each WAVE dequeues 64-query tiles from one of 8 XCD-group
 //     counters (group = blockIdx % 8 labels the blocks sharing an XCD; each counter owns a contiguous
 //     eighth of the Morton-sorted queries, so an XCD's L2 serves one region of the BVH; exhausted
-//     groups steal).  One lane per query, near-child-first depth-first traversal: one 128-B node read
-//     (one L2 line) bounds both children by max(fp32 AABB bound, fp32 oriented-box bound); the far
-//     child is pushed (16-entry LDS stack per lane, [depth][lane] layout, deeper entries spill to a
-//     per-lane global area sized from the tree depth).  Leaf children are parked and tested in
-//     wave-wide leaf phases (Aila & Laine's postponed leaves): an fp32 lower bound of the leaf's
-//     distance first (tri_d2_lo), CGAL's exact fp64 construction only if that cannot reject it.
+//     groups steal).  One lane per query, near-child-first depth-first traversal: one 64-B node read
+//     bounds both children by their fp32 oriented boxes; the far child is pushed (16-entry LDS stack
+//     per lane, [depth][lane] layout, deeper entries spill to a lane-interleaved global area sized
+//     from the tree depth).  Leaf children are parked and tested in wave-wide leaf phases (Aila &
+//     Laine's postponed leaves) with CGAL's exact fp64 construction.  Pass 1 runs over the leader
+//     slots first and then over the followers, which start from their leaders' bound.
 //     The fp32 pruning radius is cached per lane and refreshed only when the best distance changes.
 //     A lane that exceeds `budget` node steps stops and appends its query (with its exact best so far)
 //     to a deferred list: queries near the centre of a closed surface are equidistant from most of it
@@ -130,12 +130,6 @@ __device__ inline bool finite3(const D3& q) { return isfinite(q.x) && isfinite(q
 // >= the final best, so pruning with min(best, shared) keeps the result exact.  limf caches
 // limit() rounded up to fp32 (the unit of the node bounds); relim() refreshes it whenever best or
 // shared changes, so a traversal step compares against a register instead of re-deriving it.
-__device__ inline void rel_f32(const D3& a, const D3& q, float& x, float& y, float& z) {
-    x = (float)(a.x - q.x);
-    y = (float)(a.y - q.y);
-    z = (float)(a.z - q.z);
-}
-
 struct TriPol {
     const TriRec* __restrict__ tris;
     D3 q;
@@ -145,16 +139,13 @@ struct TriPol {
     float limf;
     __device__ double limit() const { return fmin(best, shared) * kSlack; }
     __device__ void relim() { limf = __double2float_ru(limit()); }
+    // CGAL's exact fp64 construction for every leaf that passed its node's oriented-box bound.  (An fp32
+    // Ericson pretest before it, tri_d2_lo, rejected some leaves early but cost more than it saved: C3
+    // pass 1 137 -> 117 ms without it.)
     __device__ void test(int leaf) {
         D3 a, b, c;
         uint32_t face;
         load_tri(tris, leaf, a, b, c, face);
-        float ax, ay, az, bx, by, bz, cx, cy, cz;
-        rel_f32(a, q, ax, ay, az);
-        rel_f32(b, q, bx, by, bz);
-        rel_f32(c, q, cx, cy, cz);
-        const float lo = tri_d2_lo(ax, ay, az, bx, by, bz, cx, cy, cz);
-        if (lo > limf) return;  // NaN never rejects
         D3 o;
         int part;
         const double d2 = closest_on_triangle(q, a, b, c, o, part);
@@ -190,12 +181,6 @@ struct NrmPol {
         D3 a, b, c;
         uint32_t face;
         load_tri(tris, leaf, a, b, c, face);
-        float ax, ay, az, bx, by, bz, cx, cy, cz;
-        rel_f32(a, q, ax, ay, az);
-        rel_f32(b, q, bx, by, bz);
-        rel_f32(c, q, cx, cy, cz);
-        const float lo = tri_d2_lo(ax, ay, az, bx, by, bz, cx, cy, cz);
-        if (lo > limf) return;
         D3 o;
         int part;
         const double d2 = closest_on_triangle(q, a, b, c, o, part);
@@ -432,6 +417,10 @@ __device__ inline D3 load_q(const KnnArgs& a, size_t i) { return D3{a.q[3 * i], 
 #define MSH_LEAD 16
 #endif
 constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: leader ordering off)
+#ifndef MSH_LEAF_K
+#define MSH_LEAF_K 2
+#endif
+constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when parked lanes >= traversing lanes / kLeafK
 
 // slot of work unit k in the launch's phase
 __device__ inline size_t slot_of(const KnnArgs& a, size_t k) {
@@ -531,7 +520,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 const unsigned long long bt = __ballot(active && !parked);
                 if ((bp | bt) == 0ull) break;
                 const int np = __popcll(bp), nt = __popcll(bt);
-                if (np > 0 && (nt == 0 || 2 * np >= nt)) {
+                if (np > 0 && (nt == 0 || kLeafK * np >= nt)) {
                     if (STATS && lane == 0) {
                         ++u_leaf_it;
                         u_leaf_lanes += np;

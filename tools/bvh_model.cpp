@@ -435,8 +435,17 @@ extern "C" void model_counts_obb_first(const double* v, const uint32_t* f, int T
 // ---- packet (wave-uniform) traversal experiment: 64 queries share one node stack; a child is entered
 // when any lane's bound passes.  Outputs per packet: uniform node visits, uniform leaf visits and the
 // per-lane leaf tests summed over the packet.  mode as model_counts_obb (1 = max(AABB, OBB)).
+extern "C" void model_packets_init(const double* v, const uint32_t* f, int T, const double* q, long npk, int mode,
+                                   uint32_t* steps_out, uint32_t* leafv_out, uint32_t* leaft_out,
+                                   const double* init_best);
 extern "C" void model_packets(const double* v, const uint32_t* f, int T, const double* q, long npk, int mode,
                               uint32_t* steps_out, uint32_t* leafv_out, uint32_t* leaft_out) {
+    model_packets_init(v, f, T, q, npk, mode, steps_out, leafv_out, leaft_out, nullptr);
+}
+// init_best (nullable): per-query initial squared bound
+extern "C" void model_packets_init(const double* v, const uint32_t* f, int T, const double* q, long npk, int mode,
+                                   uint32_t* steps_out, uint32_t* leafv_out, uint32_t* leaft_out,
+                                   const double* init_best) {
     Tree tr = build_lbvh(v, f, T);
     std::vector<OBB> ob(2 * (T - 1));
 #pragma omp parallel for schedule(dynamic, 256)
@@ -451,7 +460,8 @@ extern "C" void model_packets(const double* v, const uint32_t* f, int T, const d
     for (long p = 0; p < npk; ++p) {
         const double* qq = q + 3 * 64 * p;
         double best[64];
-        for (int l = 0; l < 64; ++l) best[l] = std::numeric_limits<double>::infinity();
+        for (int l = 0; l < 64; ++l)
+            best[l] = init_best ? init_best[64 * p + l] : std::numeric_limits<double>::infinity();
         uint32_t ns = 0, nlv = 0, nlt = 0;
         struct E { int node; double d[64]; };
         std::vector<E> st;
