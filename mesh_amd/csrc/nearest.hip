@@ -403,13 +403,6 @@ __device__ inline typename PolOf<MODE>::T make_pol(const KnnArgs& a, size_t i, c
     return pol;
 }
 
-// Test the parked leaves p0, p1 (-1 = empty).
-template <class Pol>
-__device__ inline void test_pending(Pol& pol, int& p0, int& p1) {
-    if (p0 >= 0) pol.test(p0);
-    if (p1 >= 0) pol.test(p1);
-    p0 = p1 = -1;
-}
 
 __device__ inline D3 load_q(const KnnArgs& a, size_t i) { return D3{a.q[3 * i], a.q[3 * i + 1], a.q[3 * i + 2]}; }
 
@@ -420,7 +413,12 @@ constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: lea
 #ifndef MSH_LEAF_K
 #define MSH_LEAF_K 2
 #endif
-constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when parked lanes >= traversing lanes / kLeafK
+constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= traversing lanes / kLeafK
+#ifndef MSH_LEAF_Q
+#define MSH_LEAF_Q 3
+#endif
+constexpr int kLeafQ = MSH_LEAF_Q;  // leaves a lane may hold before it stops traversing (2..4)
+static_assert(kLeafQ >= 2 && kLeafQ <= 4, "kLeafQ must be 2, 3 or 4");
 
 // slot of work unit k in the launch's phase
 __device__ inline size_t slot_of(const KnnArgs& a, size_t k) {
@@ -499,15 +497,32 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             const int root = query_root(a, i, q, qf);
             Walker w{root, 0};
             bool active = true, deferred = false;
-            int p0 = -1, p1 = -1;  // leaf children waiting for a wave-wide leaf phase
+            // leaf children waiting for a wave-wide leaf phase: a per-lane queue of up to kLeafQ leaves
+            int q0 = -1, q1 = -1, q2 = -1, q3 = -1, nq = 0;
+            auto enqueue = [&](int x) {
+                if (x < 0) return;
+                if (nq == 0) q0 = x;
+                else if (nq == 1) q1 = x;
+                else if (nq == 2) q2 = x;
+                else q3 = x;
+                ++nq;
+            };
+            auto test_queue = [&]() {
+                if (nq > 0) pol.test(q0);
+                if (nq > 1) pol.test(q1);
+                if (kLeafQ > 2 && nq > 2) pol.test(q2);
+                if (kLeafQ > 3 && nq > 3) pol.test(q3);
+                nq = 0;
+            };
             size_t steps = 0;
-            // Wave-synchronous loop.  Lanes that reach leaves park them; leaf tests run when the
-            // parked lanes are at least a third of the busy ones (or nobody can traverse), so the
-            // expensive fp64 leaf path executes for many lanes at once instead of stalling the wave
-            // on one lane every iteration (Aila & Laine 2009, "postponed leaf" while-while).
+            // Wave-synchronous loop.  Lanes that reach leaves queue them; a lane keeps traversing while
+            // its queue has room for a node's two children.  Leaf tests run when the blocked lanes are
+            // at least 1/kLeafK of the traversing ones (or nobody can traverse), so the expensive fp64
+            // leaf path executes for many lanes at once instead of stalling the wave on one lane every
+            // iteration (Aila & Laine 2009, "postponed leaf" while-while).
             for (;;) {
                 // a hinted lane whose result is not below its hint re-runs unhinted (hint_from_leaders)
-                if (!active && !deferred && p0 < 0 && hint != INFINITY && !(pol.best <= hint)) {
+                if (!active && !deferred && nq == 0 && hint != INFINITY && !(pol.best <= hint)) {
                     hint = INFINITY;
                     pol.shared = INFINITY;
                     pol.relim();
@@ -515,19 +530,20 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     steps = 0;
                     active = true;
                 }
-                const bool parked = p0 >= 0;
-                const unsigned long long bp = __ballot(parked);
-                const unsigned long long bt = __ballot(active && !parked);
-                if ((bp | bt) == 0ull) break;
-                const int np = __popcll(bp), nt = __popcll(bt);
-                if (np > 0 && (nt == 0 || kLeafK * np >= nt)) {
+                const bool can = active && nq <= kLeafQ - 2;
+                const bool has = nq > 0;
+                const unsigned long long bl = __ballot(has);
+                const unsigned long long bt = __ballot(can);
+                if ((bl | bt) == 0ull) break;
+                const int nb = __popcll(__ballot(has && !can)), nt = __popcll(bt);
+                if (bl != 0ull && (nt == 0 || kLeafK * nb >= nt)) {
                     if (STATS && lane == 0) {
                         ++u_leaf_it;
-                        u_leaf_lanes += np;
+                        u_leaf_lanes += __popcll(bl);
                     }
-                    if (parked) {
-                        if (STATS) n_leaves += 1 + (p1 >= 0);
-                        test_pending(pol, p0, p1);
+                    if (has) {
+                        if (STATS) n_leaves += nq;
+                        test_queue();
                     }
                     continue;
                 }
@@ -535,17 +551,21 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     ++u_trav_it;
                     u_trav_lanes += nt;
                 }
-                if (active && !parked) {
-                    active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, p0, p1);
+                if (can) {
+                    int l0 = -1, l1 = -1;
+                    active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, l0, l1);
+                    enqueue(l0);
+                    enqueue(l1);
                     ++steps;
                     if (active && steps >= a.T) active = false;  // each node is entered once: corrupt tree
                     if (active && steps == a.budget) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
                         if (slot < a.max_deferred) {
-                            test_pending(pol, p0, p1);
+                            if (STATS) n_leaves += nq;
+                            test_queue();
                             if (a.phase == 1) {  // followers must not take a hint from this leader yet
-                                D3 nq = D3{NAN, NAN, NAN};
-                                if (a.res) store_qres(a.res + i, MSH_NO_FACE, 0u, nq.x, nq.y, nq.z);
+                                D3 nq3 = D3{NAN, NAN, NAN};
+                                if (a.res) store_qres(a.res + i, MSH_NO_FACE, 0u, nq3.x, nq3.y, nq3.z);
                             }
                             DeferRec r;
                             r.slot = (uint32_t)i;

@@ -8,7 +8,8 @@
 //   scan       exclusive scan of hist  ->  global output offset of (digit, tile)
 //   k_scatter  the tile is re-read wave by wave in index order; each key's rank among equal digits is
 //              found with eight 64-lane ballots (no LDS atomics, deterministic, stable), per-wave digit
-//              counters live in LDS, and a cross-wave prefix gives the final destination.
+//              counters live in LDS; the tile is staged in LDS in its locally sorted order and written
+//              out linearly, so each digit's run of the tile is one contiguous, coalesced store.
 // HBM traffic per pass: read keys+values twice (8 B + 4 B), write keys+values once (8 B).
 #include "internal.h"
 
@@ -35,16 +36,22 @@ __global__ __launch_bounds__(kBlock) void k_hist(const uint32_t* __restrict__ ke
     hist[(size_t)tid * nb + blockIdx.x] = c;
 }
 
+__device__ inline uint32_t block_exclusive_scan(uint32_t x, uint32_t* sh, uint32_t& total);
+
 __global__ __launch_bounds__(kBlock) void k_scatter(const uint32_t* __restrict__ keys, const uint32_t* __restrict__ vals,
                                                     uint32_t* __restrict__ okeys, uint32_t* __restrict__ ovals, size_t n,
                                                     int shift, const uint32_t* __restrict__ offs, unsigned nb) {
     __shared__ uint32_t wcnt[4][256];
-    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t gbase[256];   // global start of (digit, this tile) minus the digit's local start
+    __shared__ uint32_t lstart[256];  // local (in-tile) start of each digit
+    __shared__ uint32_t scan_sh[4];
+    __shared__ uint32_t lk[kSortTile], lv[kSortTile];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     wcnt[0][tid] = 0; wcnt[1][tid] = 0; wcnt[2][tid] = 0; wcnt[3][tid] = 0;
-    gbase[tid] = offs[(size_t)tid * nb + blockIdx.x];
+    const uint32_t g_off = offs[(size_t)tid * nb + blockIdx.x];
     __syncthreads();
-    const size_t base = (size_t)blockIdx.x * kSortTile + (size_t)w * kWaveItems;
+    const size_t tile0 = (size_t)blockIdx.x * kSortTile;
+    const size_t base = tile0 + (size_t)w * kWaveItems;
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t kk[kSortItems], vv[kSortItems], rr[kSortItems];
 #pragma unroll
@@ -72,23 +79,37 @@ __global__ __launch_bounds__(kBlock) void k_scatter(const uint32_t* __restrict__
     }
     __syncthreads();
     {
-        const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid];
-        const uint32_t g = gbase[tid];
-        wcnt[0][tid] = g;
-        wcnt[1][tid] = g + c0;
-        wcnt[2][tid] = g + c0 + c1;
-        wcnt[3][tid] = g + c0 + c1 + c2;
+        // digit tid: local start = exclusive scan of the tile's digit counts; per-wave starts inside it
+        const uint32_t c0 = wcnt[0][tid], c1 = wcnt[1][tid], c2 = wcnt[2][tid], c3 = wcnt[3][tid];
+        uint32_t total;
+        const uint32_t ls = block_exclusive_scan(c0 + c1 + c2 + c3, scan_sh, total);
+        lstart[tid] = ls;
+        gbase[tid] = g_off - ls;
+        wcnt[0][tid] = ls;
+        wcnt[1][tid] = ls + c0;
+        wcnt[2][tid] = ls + c0 + c1;
+        wcnt[3][tid] = ls + c0 + c1 + c2;
     }
     __syncthreads();
+    // stage the tile in LDS in its locally sorted (stable) order ...
 #pragma unroll
     for (int it = 0; it < kSortItems; ++it) {
         const size_t i = base + (size_t)it * 64 + lane;
         if (i < n) {
             const uint32_t d = (kk[it] >> shift) & 255u;
-            const uint32_t dst = wcnt[w][d] + rr[it];
-            okeys[dst] = kk[it];
-            ovals[dst] = vv[it];
+            const uint32_t p = wcnt[w][d] + rr[it];
+            lk[p] = kk[it];
+            lv[p] = vv[it];
         }
+    }
+    __syncthreads();
+    // ... and write it out linearly: consecutive lanes write consecutive addresses of one digit's run
+    const uint32_t tn = (uint32_t)(n - tile0 < (size_t)kSortTile ? n - tile0 : (size_t)kSortTile);
+    for (uint32_t p = tid; p < tn; p += kBlock) {
+        const uint32_t key = lk[p];
+        const uint32_t dst = gbase[(key >> shift) & 255u] + p;
+        okeys[dst] = key;
+        ovals[dst] = lv[p];
     }
 }
 
