@@ -254,8 +254,11 @@ static const size_t kSortMin = 4096;  // below this the query Morton sort costs 
 // Query order for S point rows (device): below kSortMin the caller's arrays are used as they are;
 // otherwise Morton codes + radix sort give the permutation (ws.vals), and the rows (and normals, when
 // given) are gathered once into slot order (ws.qs / ws.ns) with the inverse permutation (ws.inv).
+#ifndef MSH_SLOT_GATHER
+#define MSH_SLOT_GATHER 0
+#endif
 static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_t S, hipStream_t s,
-                        QueryOrder* ord) {
+                        QueryOrder* ord, bool allow_lazy = false) {
     *ord = QueryOrder{d_q, d_n, nullptr, nullptr};
     if (S < kSortMin) return MSH_OK;
     Workspace& ws = t->ws;
@@ -269,6 +272,10 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
     MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
     MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
                              ws.vals_alt.as<uint32_t>(), S, 30, ws, s));
+    if (allow_lazy && !MSH_SLOT_GATHER && !d_n) {
+        *ord = QueryOrder{d_q, nullptr, ws.vals.as<uint32_t>(), ws.inv.as<uint32_t>(), false};
+        return MSH_OK;
+    }
     MSH_TRY(gather_rows(d_q, d_n, ws.vals.as<uint32_t>(), S, ws.qs.as<double>(), d_n ? ws.ns.as<double>() : nullptr,
                         ws.inv.as<uint32_t>(), s));
     *ord = QueryOrder{ws.qs.as<double>(), d_n ? ws.ns.as<double>() : nullptr, ws.vals.as<uint32_t>(),
@@ -680,7 +687,7 @@ int msh_tree_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* 
     hipStream_t s = pick(t, stream);
     WsOrder order(t, s);
     QueryOrder ord;
-    MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord));
+    MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord, true));
     return launch_nearest(t, ord, S, SlotOut{d_face, d_part, d_pt, nullptr, nullptr}, s);
 }
 
@@ -693,7 +700,7 @@ int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint3
     hipStream_t s = pick(t, stream);
     WsOrder order(t, s);
     QueryOrder ord;
-    MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord));
+    MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord, true));
     return launch_nearest(t, ord, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_w}, s);
 }
 
@@ -734,7 +741,7 @@ int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* n
     {
         WsOrder order(t, s);
         QueryOrder ord;
-        MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord));
+        MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord, true));
         MSH_TRY(t->ws.stats.reserve(8 * sizeof(unsigned long long)));
         MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, 8 * sizeof(unsigned long long), s));
         MSH_TRY(launch_nearest_stats(t, ord, S, t->ws.stats.as<unsigned long long>(), s));

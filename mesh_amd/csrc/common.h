@@ -319,121 +319,6 @@ __device__ inline double obb_d2_lo_d(const double* pp, const float* ext) {
     return s * 0.999996185302734375;  // 1 - 2^-18
 }
 
-// Leaf pretest of the exact policies.  Lower bound of the squared distance from the origin to
-// triangle (A, B, C) given in fp32 coordinates
-// relative to the query (Ericson's Voronoi-region closest point, evaluated in fp32).  For a triangle
-// whose smallest angle is not tiny the rounding error of the result is O(ulp * M / sin^2(angle)),
-// M = largest |coordinate|: triangles with sin^2 < 1e-2 return 0 (no rejection), a face-region
-// result outside the triangle returns 0, and the bound subtracts 2^-12 * M (>= 40x the error bound).
-// NaN (degenerate input) also propagates, which callers treat as "cannot reject".
-__host__ __device__ inline float tri_d2_lo(float ax, float ay, float az, float bx, float by, float bz, float cx, float cy,
-                                           float cz) {
-    const float abx = bx - ax, aby = by - ay, abz = bz - az;
-    const float acx = cx - ax, acy = cy - ay, acz = cz - az;
-    {
-        const float nx = aby * acz - abz * acy, ny = abz * acx - abx * acz, nz = abx * acy - aby * acx;
-        const float n2 = nx * nx + ny * ny + nz * nz;
-        const float l2 = (abx * abx + aby * aby + abz * abz) * (acx * acx + acy * acy + acz * acz);
-        if (!(n2 >= 1e-2f * l2)) return 0.f;  // sliver or degenerate (also catches NaN / 0)
-    }
-    float px, py, pz;
-    const float d1 = -(abx * ax + aby * ay + abz * az), d2 = -(acx * ax + acy * ay + acz * az);
-    const float d3 = -(abx * bx + aby * by + abz * bz), d4 = -(acx * bx + acy * by + acz * bz);
-    const float d5 = -(abx * cx + aby * cy + abz * cz), d6 = -(acx * cx + acy * cy + acz * cz);
-    const float vc = d1 * d4 - d3 * d2, vb = d5 * d2 - d1 * d6, va = d3 * d6 - d5 * d4;
-    if (d1 <= 0.f && d2 <= 0.f) {
-        px = ax; py = ay; pz = az;
-    } else if (d3 >= 0.f && d4 <= d3) {
-        px = bx; py = by; pz = bz;
-    } else if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
-        const float t = d1 / (d1 - d3);
-        px = ax + t * abx; py = ay + t * aby; pz = az + t * abz;
-    } else if (d6 >= 0.f && d5 <= d6) {
-        px = cx; py = cy; pz = cz;
-    } else if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
-        const float t = d2 / (d2 - d6);
-        px = ax + t * acx; py = ay + t * acy; pz = az + t * acz;
-    } else if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
-        const float t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-        px = bx + t * (cx - bx); py = by + t * (cy - by); pz = bz + t * (cz - bz);
-    } else {
-        const float den = 1.f / (va + vb + vc);
-        const float v = vb * den, w = vc * den;
-        if (!(v >= -1e-3f && w >= -1e-3f && v + w <= 1.001f)) return 0.f;
-        px = ax + abx * v + acx * w; py = ay + aby * v + acy * w; pz = az + abz * v + acz * w;
-    }
-    const float M = fmaxf(fmaxf(fmaxf(fabsf(ax), fabsf(ay)), fmaxf(fabsf(az), fabsf(bx))),
-                          fmaxf(fmaxf(fabsf(by), fabsf(bz)), fmaxf(fmaxf(fabsf(cx), fabsf(cy)), fabsf(cz))));
-    const float d = sqrtf(px * px + py * py + pz * pz) - M * 2.44140625e-4f;  // 2^-12
-    return d > 0.f ? d * d * 0.999999523162841796875f : (d <= 0.f ? 0.f : d);  // NaN propagates
-}
-
-// Two-sided bounds for the candidate-deferring policy (TriCandPol, MSH_CAND=1).  Bounds of the
-// squared distance from the origin to triangle (A, B, C) given in fp32 coordinates
-// relative to the query (Ericson's Voronoi regions evaluated in fp32; the face region uses the
-// supporting-plane distance).  lo <= d2 <= hi for the exact (and the fp64 CGAL) squared distance d2.
-// The rounding error of the fp32 distance is O(ulp * M / sin^2(angle)), M = largest |coordinate|:
-// triangles with sin^2 < 1e-2, and face-region results outside the triangle, return lo = 0 and
-// hi = +inf (no information); otherwise the distance is widened by 2^-15 * M both ways (see the
-// margin note).  NaN (degenerate input) propagates into lo and hi; callers treat NaN as "unknown".
-__host__ __device__ inline void tri_d2_bounds(float ax, float ay, float az, float bx, float by, float bz, float cx,
-                                              float cy, float cz, float& lo, float& hi) {
-    lo = 0.f;
-    hi = INFINITY;
-    const float abx = bx - ax, aby = by - ay, abz = bz - az;
-    const float acx = cx - ax, acy = cy - ay, acz = cz - az;
-    const float nx = aby * acz - abz * acy, ny = abz * acx - abx * acz, nz = abx * acy - aby * acx;
-    const float n2 = nx * nx + ny * ny + nz * nz;
-    {
-        const float l2 = (abx * abx + aby * aby + abz * abz) * (acx * acx + acy * acy + acz * acz);
-        if (!(n2 >= 1e-2f * l2)) return;  // sliver or degenerate (also catches NaN / 0)
-    }
-    float px, py, pz;
-    const float d1 = -(abx * ax + aby * ay + abz * az), d2 = -(acx * ax + acy * ay + acz * az);
-    const float d3 = -(abx * bx + aby * by + abz * bz), d4 = -(acx * bx + acy * by + acz * bz);
-    const float d5 = -(abx * cx + aby * cy + abz * cz), d6 = -(acx * cx + acy * cy + acz * cz);
-    const float vc = d1 * d4 - d3 * d2, vb = d5 * d2 - d1 * d6, va = d3 * d6 - d5 * d4;
-    if (d1 <= 0.f && d2 <= 0.f) {
-        px = ax; py = ay; pz = az;
-    } else if (d3 >= 0.f && d4 <= d3) {
-        px = bx; py = by; pz = bz;
-    } else if (vc <= 0.f && d1 >= 0.f && d3 <= 0.f) {
-        const float t = d1 / (d1 - d3);
-        px = ax + t * abx; py = ay + t * aby; pz = az + t * abz;
-    } else if (d6 >= 0.f && d5 <= d6) {
-        px = cx; py = cy; pz = cz;
-    } else if (vb <= 0.f && d2 >= 0.f && d6 <= 0.f) {
-        const float t = d2 / (d2 - d6);
-        px = ax + t * acx; py = ay + t * acy; pz = az + t * acz;
-    } else if (va <= 0.f && (d4 - d3) >= 0.f && (d5 - d6) >= 0.f) {
-        const float t = (d4 - d3) / ((d4 - d3) + (d5 - d6));
-        px = bx + t * (cx - bx); py = by + t * (cy - by); pz = bz + t * (cz - bz);
-    } else {
-        // face region: the distance to the supporting plane, |n . a| / |n|, is a lower bound of the
-        // distance to the triangle whatever the true region, and it avoids the cancellation of the
-        // barycentric reconstruction (2^-15 M observed there vs 2^-22 M for the plane distance)
-        const float den = va + vb + vc;
-        const float v = vb / den, w = vc / den;
-        if (!(v >= -1e-3f && w >= -1e-3f && v + w <= 1.001f)) return;
-        const float h = fabsf(nx * ax + ny * ay + nz * az) / sqrtf(n2);
-        px = h; py = 0.f; pz = 0.f;
-    }
-    const float M = fmaxf(fmaxf(fmaxf(fabsf(ax), fabsf(ay)), fmaxf(fabsf(az), fabsf(bx))),
-                          fmaxf(fmaxf(fabsf(by), fabsf(bz)), fmaxf(fmaxf(fabsf(cx), fabsf(cy)), fabsf(cz))));
-    // Margin: region classification and the vertex/edge constructions err by <= ~2^-24 M times the
-    // conditioning 1/sin^2 <= 100 (sliver guard above), i.e. ~2^-17.4 M; 2^-15 M leaves a 5x cushion.
-    // Measured: over 10^7 random/adversarial cases (tests/csrc/pretest_check.cpp) violations first
-    // appear with a 2^-21 M margin, 64x below the one used.
-#ifndef MSH_PRETEST_MARGIN
-#define MSH_PRETEST_MARGIN 3.0517578125e-5f  // 2^-15
-#endif
-    const float dist = sqrtf(px * px + py * py + pz * pz), mg = M * MSH_PRETEST_MARGIN;
-    const float dl = dist - mg, dh = dist + mg;
-    lo = dl > 0.f ? dl * dl * 0.999999523162841796875f : (dl <= 0.f ? 0.f : dl);  // 1 - 2^-21; NaN propagates
-    hi = dh * dh * 1.00000095367431640625f;  // 1 + 2^-20 (NaN propagates: never prunes)
-}
-
-
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // blocks b and b+8 share an XCD, so give each XCD a contiguous range of logical tiles — adjacent
 // Morton-sorted query tiles then share that XCD's L2.

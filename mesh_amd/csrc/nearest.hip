@@ -37,12 +37,6 @@
 
 #include "internal.h"
 
-// MSH_WAVES (tuning): force the pass-1 kernel's occupancy (waves per SIMD) through its register budget.
-#ifdef MSH_WAVES
-#define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MSH_WAVES, MSH_WAVES)))
-#else
-#define MSH_KNN_ATTR
-#endif
 
 namespace msh {
 
@@ -65,6 +59,8 @@ struct KnnArgs {
     const double* q;       // query rows in slot order (Morton-sorted copy, or the caller's array)
     const double* n;       // MODE 1: query normals in slot order
     const uint32_t* perm;  // slot -> caller's query index (nullptr: identity)
+    const uint32_t* qperm; // non-null: q holds the caller's rows and slot i reads row qperm[i]
+    uint32_t* inv_w;       // with qperm: pass 1 records inv_w[qperm[i]] = i
     size_t S;
     QRes* res;             // slot-order records (sorted path); nullptr: write the caller's arrays below
     double* res_w;         // MODE 3 slot-order barycentric weights (3 per slot)
@@ -404,7 +400,10 @@ __device__ inline typename PolOf<MODE>::T make_pol(const KnnArgs& a, size_t i, c
 }
 
 
-__device__ inline D3 load_q(const KnnArgs& a, size_t i) { return D3{a.q[3 * i], a.q[3 * i + 1], a.q[3 * i + 2]}; }
+__device__ inline D3 load_q(const KnnArgs& a, size_t i) {
+    const size_t r = a.qperm ? (size_t)a.qperm[i] : i;
+    return D3{a.q[3 * r], a.q[3 * r + 1], a.q[3 * r + 2]};
+}
 
 #ifndef MSH_LEAD
 #define MSH_LEAD 16
@@ -420,9 +419,23 @@ constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= t
 constexpr int kLeafQ = MSH_LEAF_Q;  // leaves a lane may hold before it stops traversing (2..4)
 static_assert(kLeafQ >= 2 && kLeafQ <= 4, "kLeafQ must be 2, 3 or 4");
 
-// slot of work unit k in the launch's phase
+#ifndef MSH_LEAD2
+#define MSH_LEAD2 256
+#endif
+// second level: one super-leader per kLead2 slots (0: off), run first and unhinted; the other leaders
+// then start from the bound of the 4 super-leaders of their 4 * kLead2-slot window
+constexpr unsigned kLead2 = MSH_LEAD2;
+static_assert(kLead2 == 0 || (kLead > 1 && kLead2 % kLead == 0 && kLead2 / kLead >= 2), "kLead2: a multiple of kLead");
+
+// slot of work unit k in the launch's phase: 3 super-leaders, 1 leaders (without the super-leaders
+// when kLead2 > 0), 2 followers, 0 every slot
 __device__ inline size_t slot_of(const KnnArgs& a, size_t k) {
-    if (a.phase == 1) return k * kLead;
+    if (a.phase == 3) return k * kLead2;
+    if (a.phase == 1) {
+        if (kLead2 == 0) return k * kLead;
+        constexpr size_t r = kLead2 / (kLead ? kLead : 1);
+        return kLead * (k + k / (r - 1) + 1);
+    }
     if (a.phase == 2) {
         const size_t g = k / (kLead - 1);
         return g * kLead + (k - g * (kLead - 1)) + 1;
@@ -430,17 +443,18 @@ __device__ inline size_t slot_of(const KnnArgs& a, size_t k) {
     return k;
 }
 
-// Upper bound of slot i's squared distance from the closest points its tile's leaders found: a leader's
-// point p_L lies on a mesh triangle, so d*(q) <= |q - p_L|.  The bound is widened by 2^-30 relative and
-// (2^-40 M)^2 absolute (M = largest |coordinate|) against the rounding of the fp64 constructions; the
-// caller still re-runs the query unhinted whenever its final best exceeds the bound, so a bound that is
-// too tight costs time, never correctness.  Leaders of another mesh (batched trees), deferred leaders
-// (NO_FACE until pass 2 runs) and non-finite ones are skipped.
-__device__ inline double hint_from_leaders(const KnnArgs& a, size_t i, const D3& q) {
-    const size_t base = i & ~(size_t)63;
+// Upper bound of slot i's squared distance from the closest points found by the leaders at slots
+// base, base + stride, ... < base + window (base = the window containing i): a leader's point p_L lies on
+// a mesh triangle, so d*(q) <= |q - p_L|.  The bound is widened by 2^-30 relative and (2^-40 M)^2
+// absolute (M = largest |coordinate|) against the rounding of the fp64 constructions; the caller still
+// re-runs the query unhinted whenever its final best exceeds the bound, so a bound that is too tight
+// costs time, never correctness.  Leaders of another mesh (batched trees), deferred leaders (NO_FACE
+// until pass 2 runs) and non-finite ones are skipped.
+__device__ inline double hint_from_leaders(const KnnArgs& a, size_t i, const D3& q, size_t window, size_t stride) {
+    const size_t base = (i / window) * window;
     const size_t mesh = a.orgs ? i / a.qper : 0;
     double h = INFINITY;
-    for (unsigned L = 0; L < 64; L += kLead) {
+    for (size_t L = 0; L < window; L += stride) {
         const size_t li = base + L;
         if (li >= a.S) break;
         if (a.orgs && li / a.qper != mesh) continue;
@@ -458,7 +472,7 @@ __device__ inline double hint_from_leaders(const KnnArgs& a, size_t i, const D3&
 }
 
 template <int MODE, bool STATS>
-__global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
+__global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
     const int tid = threadIdx.x, lane = tid & 63;
     uint2* lds = stk + tid;
@@ -476,6 +490,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         const size_t i = slot_of(a, k);
         if (i >= a.S) continue;
         const D3 q = load_q(a, i);
+        if (a.inv_w) a.inv_w[a.qperm[i]] = (uint32_t)i;
         auto pol = make_pol<MODE>(a, i, q);
         if (!finite3(q)) {  // no distance is defined: NO_FACE / NaN, no traversal
             if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
@@ -483,8 +498,8 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         }
         double hint = INFINITY;
         if constexpr (MODE == 0 || MODE == 3) {
-            if (a.phase == 2) {
-                hint = hint_from_leaders(a, i, q);
+            if (a.phase == 2 || (a.phase == 1 && kLead2 > 0)) {
+                hint = a.phase == 2 ? hint_from_leaders(a, i, q, 64, kLead) : hint_from_leaders(a, i, q, 4 * kLead2, kLead2);
                 pol.shared = hint;
                 pol.relim();
             }
@@ -563,7 +578,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         if (slot < a.max_deferred) {
                             if (STATS) n_leaves += nq;
                             test_queue();
-                            if (a.phase == 1) {  // followers must not take a hint from this leader yet
+                            if (a.phase == 1 || a.phase == 3) {  // nobody may take a hint from it yet
                                 D3 nq3 = D3{NAN, NAN, NAN};
                                 if (a.res) store_qres(a.res + i, MSH_NO_FACE, 0u, nq3.x, nq3.y, nq3.z);
                             }
@@ -820,7 +835,10 @@ static int device_cus(int dev) {
     return cache[dev];
 }
 
-constexpr unsigned kBudget = 2048;  // pass-1 node steps per lane before a query is deferred
+#ifndef MSH_BUDGET
+#define MSH_BUDGET 1024
+#endif
+constexpr unsigned kBudget = MSH_BUDGET;  // pass-1 node steps per lane before a query is deferred
 #ifndef MSH_KNN_BPC
 #define MSH_KNN_BPC 4
 #endif
@@ -875,7 +893,15 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         {
             TimedLaunch t1(STATS ? "knn_pass1_stats" : "knn_pass1", s);
             if (lead) {
-                MSH_TRY(pass1(1, n_lead, STATS ? "knn_lead_stats" : "knn_lead"));
+                if (kLead2 > 0) {
+                    constexpr size_t l2 = kLead2 ? kLead2 : 1;
+                    const size_t n_super = (a.S + l2 - 1) / l2;
+                    MSH_TRY(pass1(3, n_super, STATS ? "knn_lead2_stats" : "knn_lead2"));
+                    MSH_HIP(hipMemsetAsync(a.counters, 0, 8 * 32 * sizeof(unsigned), s));
+                    MSH_TRY(pass1(1, n_lead - n_super, STATS ? "knn_lead_stats" : "knn_lead"));
+                } else {
+                    MSH_TRY(pass1(1, n_lead, STATS ? "knn_lead_stats" : "knn_lead"));
+                }
                 MSH_HIP(hipMemsetAsync(a.counters, 0, 8 * 32 * sizeof(unsigned), s));  // group counters only
                 MSH_TRY(pass1(2, a.S - n_lead, STATS ? "knn_follow_stats" : "knn_follow"));
             } else {
@@ -899,6 +925,10 @@ static int run_knn(msh_tree* tree, KnnArgs a, const QueryOrder& ord, const SlotO
     if (a.S == 0) return MSH_OK;
     a.q = ord.q;
     a.perm = ord.perm;
+    if (!ord.gathered) {
+        a.qperm = ord.perm;
+        a.inv_w = const_cast<uint32_t*>(ord.inv);
+    }
     Workspace& ws = tree->ws;
     if (ord.perm) {  // STATS launches keep the records too: followers take their hints from them
         MSH_TRY(ws.res.reserve(a.S * sizeof(QRes)));
