@@ -319,6 +319,26 @@ __device__ inline double obb_d2_lo_d(const double* pp, const float* ext) {
     return s * 0.999996185302734375;  // 1 - 2^-18
 }
 
+// Per-lane traversal stack: entry sp lives in LDS (lds[sp * kBlock], lane-interleaved) for
+// sp < kStack and in the block's global spill area beyond.  The spill side uses the nontemporal
+// builtins so the compiler cannot fold the two cases into one generic (flat) access through a
+// pointer select: flat accesses to LDS go through the vector memory pipe and make every stack
+// push/pop wait for the outstanding node loads.
+__device__ inline void stack_put(uint2* __restrict__ lds, uint2* __restrict__ spill, int sp, uint2 e) {
+    if (sp < kStack) {
+        lds[sp * kBlock] = e;
+    } else {
+        unsigned long long* p = reinterpret_cast<unsigned long long*>(spill + (size_t)(sp - kStack) * kBlock);
+        __builtin_nontemporal_store(((unsigned long long)e.y << 32) | e.x, p);
+    }
+}
+__device__ inline uint2 stack_get(const uint2* __restrict__ lds, const uint2* __restrict__ spill, int sp) {
+    if (sp < kStack) return lds[sp * kBlock];
+    const unsigned long long* p = reinterpret_cast<const unsigned long long*>(spill + (size_t)(sp - kStack) * kBlock);
+    const unsigned long long v = __builtin_nontemporal_load(p);
+    return make_uint2((unsigned)v, (unsigned)(v >> 32));
+}
+
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // blocks b and b+8 share an XCD, so give each XCD a contiguous range of logical tiles — adjacent
 // Morton-sorted query tiles then share that XCD's L2.

@@ -222,8 +222,7 @@ struct Walker {
     int node;
     int sp;
     __device__ inline void push(uint2 e, uint2* __restrict__ lds, uint2* __restrict__ spill) {
-        if (sp < kStack) lds[sp * kBlock] = e;
-        else spill[(sp - kStack) * kBlock] = e;
+        stack_put(lds, spill, sp, e);
         ++sp;
     }
     // pop until an entry survives the current limit; false when the stack is exhausted
@@ -231,7 +230,7 @@ struct Walker {
     __device__ inline bool pop(const Pol& pol, uint2* __restrict__ lds, uint2* __restrict__ spill) {
         while (sp > 0) {
             --sp;
-            const uint2 e = sp < kStack ? lds[sp * kBlock] : spill[(sp - kStack) * kBlock];
+            const uint2 e = stack_get(lds, spill, sp);
             if (__uint_as_float(e.y) <= pol.limf) {
                 node = (int)e.x;
                 return true;
@@ -419,6 +418,9 @@ constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= t
 constexpr int kLeafQ = MSH_LEAF_Q;  // leaves a lane may hold before it stops traversing (2..4)
 static_assert(kLeafQ >= 2 && kLeafQ <= 4, "kLeafQ must be 2, 3 or 4");
 
+#ifndef MSH_TEST_LOOP
+#define MSH_TEST_LOOP 1
+#endif
 #ifndef MSH_LEAD2
 #define MSH_LEAD2 256
 #endif
@@ -513,20 +515,30 @@ __global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
             Walker w{root, 0};
             bool active = true, deferred = false;
             // leaf children waiting for a wave-wide leaf phase: a per-lane queue of up to kLeafQ leaves
-            int q0 = -1, q1 = -1, q2 = -1, q3 = -1, nq = 0;
+            int q0 = -1, q1 = -1, q2 = -1, nq = 0;
+            static_assert(kLeafQ >= 2 && kLeafQ <= 3, "leaf queue: 2 or 3 entries");
+            // a shift register (no dynamic index, so the queue stays in VGPRs, not in scratch)
             auto enqueue = [&](int x) {
                 if (x < 0) return;
-                if (nq == 0) q0 = x;
-                else if (nq == 1) q1 = x;
-                else if (nq == 2) q2 = x;
-                else q3 = x;
+                q2 = q1;
+                q1 = q0;
+                q0 = x;
                 ++nq;
             };
             auto test_queue = [&]() {
+#if MSH_TEST_LOOP
+                // one copy of the fp64 construction in the code (a loop over the queue), not one per entry
+#pragma nounroll
+                for (int k = 0; k < nq; ++k) {
+                    pol.test(q0);
+                    q0 = q1;
+                    q1 = q2;
+                }
+#else
                 if (nq > 0) pol.test(q0);
                 if (nq > 1) pol.test(q1);
                 if (kLeafQ > 2 && nq > 2) pol.test(q2);
-                if (kLeafQ > 3 && nq > 3) pol.test(q3);
+#endif
                 nq = 0;
             };
             size_t steps = 0;

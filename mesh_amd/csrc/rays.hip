@@ -165,8 +165,7 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
             double kf = k1;
             if (k1 < k0) { nearc = c1; farc = c0; kf = k0; }
             const uint2 e = make_uint2((unsigned)farc, __float_as_uint(__double2float_rd(kf)));
-            if (sp < kStack) lds[sp * kBlock] = e;
-            else spill[(sp - kStack) * kBlock] = e;
+            stack_put(lds, spill, sp, e);
             ++sp;
             node = nearc;
             continue;
@@ -176,7 +175,7 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
         bool found = false;
         while (sp > 0) {
             --sp;
-            const uint2 e = sp < kStack ? lds[sp * kBlock] : spill[(sp - kStack) * kBlock];
+            const uint2 e = stack_get(lds, spill, sp);
             if (pol.keep((double)__uint_as_float(e.y))) {
                 node = (int)e.x;
                 found = true;

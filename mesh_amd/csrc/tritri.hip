@@ -202,8 +202,7 @@ __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
                 if (h1 && c1 < 0) { leaf_test(~c1); h1 = false; if (hit) break; }
                 if (h0 && h1) {
                     const uint2 e = make_uint2((unsigned)c1, 0u);
-                    if (sp < kStack) lds[sp * kBlock] = e;
-                    else spill[(sp - kStack) * kBlock] = e;
+                    stack_put(lds, spill, sp, e);
                     ++sp;
                     node = c0;
                     continue;
@@ -212,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_tritri(TriArgs a) {
                 if (h1) { node = c1; continue; }
                 if (sp == 0) break;
                 --sp;
-                node = (int)(sp < kStack ? lds[sp * kBlock] : spill[(sp - kStack) * kBlock]).x;
+                node = (int)stack_get(lds, spill, sp).x;
             }
         }
         a.flags[i] = hit ? 1u : 0u;
