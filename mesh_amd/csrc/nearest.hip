@@ -142,9 +142,13 @@ struct TriPol {
         D3 a, b, c;
         uint32_t face;
         load_tri(tris, leaf, a, b, c, face);
+#ifdef MSH_EXP_CHEAPLEAF
+        const double d2 = fmin(fmin(sqdist(q, a), sqdist(q, b)), sqdist(q, c));  // timing experiment only
+#else
         D3 o;
         int part;
         const double d2 = closest_on_triangle(q, a, b, c, o, part);
+#endif
         if (d2 < best || (d2 == best && face < best_face)) {
             best = d2;
             best_face = face;
@@ -456,8 +460,13 @@ __device__ inline double hint_from_leaders(const KnnArgs& a, size_t i, const D3&
     const size_t base = (i / window) * window;
     const size_t mesh = a.orgs ? i / a.qper : 0;
     double h = INFINITY;
+#ifdef MSH_EXP_SELFHINT
+    for (size_t L = 0; L < window + 1; L += stride) {  // experiment: the slot's own stale result last
+        const size_t li = L < window ? base + L : i;
+#else
     for (size_t L = 0; L < window; L += stride) {
         const size_t li = base + L;
+#endif
         if (li >= a.S) break;
         if (a.orgs && li / a.qper != mesh) continue;
         const uint4 r0 = reinterpret_cast<const uint4*>(a.res + li)[0];
@@ -473,8 +482,15 @@ __device__ inline double hint_from_leaders(const KnnArgs& a, size_t i, const D3&
     return h * (1.0 + 9.313225746154785e-10) + e * e;  // 1 + 2^-30
 }
 
+// Pass 1 runs 4 waves per SIMD: the register budget drops from 139 to 128 VGPRs at the cost of a few
+// spills of loop-invariant values outside the node step (C3: +10 % over the compiler's 3 waves).
+#ifndef MSH_WAVES
+#define MSH_WAVES 4
+#endif
+// (not for the normals metric, MODE 1, whose larger live set would spill in the node step)
+#define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 1 : MSH_WAVES)))
 template <int MODE, bool STATS>
-__global__ __launch_bounds__(kBlock) void k_knn(KnnArgs a) {
+__global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
     const int tid = threadIdx.x, lane = tid & 63;
     uint2* lds = stk + tid;

@@ -22,6 +22,11 @@ for s in $STAGES; do
         n=$(basename $so .so)
         MESH_AMD_LIB=$PWD/$so timeout -k 10 300 python bench.py --queries ${VQ:-10000000} --steps ${VSTEPS:-5} --warmup 2 --no-cpu > gpurun_out/var_$n.log 2>&1; ok var_$n $?
       done ;;
+    variants_c5)  # the same sweep through the C5 ray workloads
+      for so in build/variants/*.so; do
+        n=$(basename $so .so)
+        MESH_AMD_LIB=$PWD/$so timeout -k 10 600 python scripts/bench_configs.py --configs c5 --reps 3 > gpurun_out/varc5_$n.log 2>&1; ok varc5_$n $?
+      done ;;
     bench_wide) MESH_AMD_TRAVERSAL=wide timeout -k 10 600 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_wide.log 2>&1; ok bench_wide $? ;;
     split)  MESH_AMD_STATS_DUMP=1 timeout -k 10 600 python scripts/c3_split.py > gpurun_out/split.log 2>&1; ok split $? ;;
     pytest_quick) timeout -k 10 600 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread -k "spill or cooperative or c1 or c2 or c3 or rays or alongnormal or visibility" > gpurun_out/pytest_quick.log 2>&1; ok pytest_quick $? ;;
