@@ -409,7 +409,7 @@ __device__ inline D3 load_q(const KnnArgs& a, size_t i) {
 }
 
 #ifndef MSH_LEAD
-#define MSH_LEAD 16
+#define MSH_LEAD 8
 #endif
 constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: leader ordering off)
 #ifndef MSH_LEAF_K
