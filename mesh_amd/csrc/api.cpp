@@ -1220,6 +1220,11 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
         t->scene_hi[k] = h.scene_hi[k];
         t->origin[k] = h.origin[k];
     }
+    {
+        // from the fp32-rounded scene box: widened by far more than its rounding (2^-24 relative)
+        const double box[6] = {h.scene_lo[0], h.scene_lo[1], h.scene_lo[2], h.scene_hi[0], h.scene_hi[1], h.scene_hi[2]};
+        t->half_diag = half_diagonal(box, t->origin) * (1.0 + 1e-6);
+    }
     const char* src = static_cast<const char*>(d_src);
     const size_t leaf = h.leaf_bytes;
     hipStream_t s = us ? us : t->stream;

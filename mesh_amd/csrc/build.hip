@@ -25,6 +25,18 @@
 
 namespace msh {
 
+// largest distance from `origin` to a corner of box (lo[3], hi[3]); a non-finite box gives +inf (the
+// query margin then disables culling rather than under-bounding it)
+double half_diagonal(const double* box, const double* origin) {
+    double s = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        const double d = std::max(fabs(box[k] - origin[k]), fabs(box[3 + k] - origin[k]));
+        s += d * d;
+    }
+    const double r = sqrt(s) * (1.0 + 1e-12);
+    return r == r ? r : INFINITY;
+}
+
 // Batched kernels: B meshes of P vertices / T primitives each, stored back to back (primitive
 // g = b*T + t of mesh b = g / T); the single-mesh build is B = 1.
 __global__ __launch_bounds__(kBlock) void k_tri_bounds(const double* __restrict__ v, size_t P, const uint32_t* __restrict__ f,
@@ -343,8 +355,8 @@ __global__ __launch_bounds__(kBlock) void k_obb(const void* __restrict__ leaves,
             uint32_t w[4];
 #pragma unroll
             for (int j = 0; j < 3; ++j) w[j] = u[4 * j] | (u[4 * j + 1] << 8) | (u[4 * j + 2] << 16) | (u[4 * j + 3] << 24);
-            w[3] = ((uint32_t)(uint8_t)(int8_t)ex[0]) | ((uint32_t)(uint8_t)(int8_t)ex[1] << 8) |
-                   ((uint32_t)(uint8_t)(int8_t)ex[2] << 16);
+            // biased exponents (e + 127 in [1, 254]): the decoder shifts them into an fp32 exponent field
+            w[3] = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
             *reinterpret_cast<float4*>(f + 11) = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]),
                                                              __uint_as_float(w[2]), __uint_as_float(w[3]));
             f[15] = 0.0f;
@@ -474,6 +486,7 @@ int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T,
         const double c = 0.5 * (box_h[k] + box_h[3 + k]);
         tree->origin[k] = (c == c && fabs(c) < INFINITY) ? c : 0.0;
     }
+    tree->half_diag = half_diagonal(box_h, tree->origin);
     MSH_TRY(upload_origin(tree, s));
     // Morton codes + sort
     MSH_TRY(ws.keys.reserve(T * sizeof(uint32_t)));
@@ -583,6 +596,12 @@ int build_lbvh_batch(msh_tree* tree, const double* d_lo, const double* d_hi, siz
         }
         tree->scene_lo[k] = (float)lo;
         tree->scene_hi[k] = (float)hi;
+    }
+    tree->half_diag = 0.0;
+    for (size_t b = 0; b < B; ++b) {
+        const double c[3] = {0.5 * (hb[6 * b] + hb[6 * b + 3]), 0.5 * (hb[6 * b + 1] + hb[6 * b + 4]),
+                             0.5 * (hb[6 * b + 2] + hb[6 * b + 5])};
+        tree->half_diag = std::max(tree->half_diag, half_diagonal(&hb[6 * b], c));
     }
     tree->max_depth = (int)depth;
     return MSH_OK;

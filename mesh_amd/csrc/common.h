@@ -31,14 +31,15 @@ constexpr double kSlack = 1.0 + 9.094947017729282e-13;  // 1 + 2^-40: fp64 round
 
 // float index within a node:  0-2 n | 3-5 t | 6 child0 | 7 child1 | 8-10 base (n, t, b) |
 //   bytes 44-55: u[side][6] quantised extents (lo n t b, hi n t b) of child 0 then child 1 |
-//   bytes 56-58: scale exponents e[3] (int8; scale = 2^e) | 59-63 zero
+//   bytes 56-58: biased scale exponents E[3] = e + 127 (scale = 2^e, the fp32 with exponent field E) |
+//   59-63 zero
 struct alignas(16) BNode {
     float f[16];
 };
 static_assert(sizeof(BNode) == 64, "BNode must be 64 B");
 constexpr int kBase = 8;      // float index of base[3]
 constexpr int kQuant = 44;    // byte offset of u[2][6]
-constexpr int kExp = 56;      // byte offset of e[3]
+constexpr int kExp = 56;      // byte offset of E[3]
 
 // 2^e as an fp32 (e in [-126, 127])
 __host__ __device__ inline float exp2_scale(int e) {
@@ -101,11 +102,12 @@ struct NodeV {
         t[0] = at(3); t[1] = at(4); t[2] = at(5);
         frame_b(n, t, b);
     }
+    // scale 2^e of axis k: the biased exponent byte shifted into an fp32 exponent field
+    __device__ float scale(int k) const { return __uint_as_float(((word(14) >> (8 * k)) & 0xffu) << 23); }
     // decoded oriented extents of both children: e0/e1 = lo n t b, hi n t b
     __device__ void extents(float* e0, float* e1) const {
-        const uint32_t w0 = word(11), w1 = word(12), w2 = word(13), w3 = word(14);
-        const float sc[3] = {exp2_scale((int)(int8_t)(w3 & 0xffu)), exp2_scale((int)(int8_t)((w3 >> 8) & 0xffu)),
-                             exp2_scale((int)(int8_t)((w3 >> 16) & 0xffu))};
+        const uint32_t w0 = word(11), w1 = word(12), w2 = word(13);
+        const float sc[3] = {scale(0), scale(1), scale(2)};
         const float bs[3] = {at(kBase), at(kBase + 1), at(kBase + 2)};
         const uint32_t u[12] = {w0 & 0xffu, (w0 >> 8) & 0xffu, (w0 >> 16) & 0xffu, w0 >> 24,
                                 w1 & 0xffu, (w1 >> 8) & 0xffu, (w1 >> 16) & 0xffu, w1 >> 24,
@@ -226,11 +228,14 @@ __device__ inline double closest_on_triangle(const D3& o, const D3& t0, const D3
 
 // ---- conservative fp32 culling (never rejects what the exact fp64 test would accept) ----
 // The query relative to the tree origin, rounded to fp32; e = largest per-axis rounding error (rounded
-// up); pe = bound of the fp32 projection error onto a unit axis (2^-21 * |q|_1 + 2e, rounded up).
+// up); pe = the margin of the slab gaps in node_child_bounds: the fp32 projection error onto a unit
+// axis, pe0 = 2^-21 |q|_1 + 2e, plus 2^-21 |q|_1 + tm for the roundings of the fused gap expressions,
+// tm = 2^-21 * 1.25 * M (tree_margin), all rounded up.
 struct QF {
     float x, y, z, e, pe;
 };
-__device__ inline QF make_qf(const D3& q, const double* origin) {
+__host__ __device__ inline double tree_margin(double half_diagonal) { return 5.9604644775390625e-7 * half_diagonal; }
+__device__ inline QF make_qf(const D3& q, const double* origin, double tm) {
     const double rx = q.x - origin[0], ry = q.y - origin[1], rz = q.z - origin[2];
     QF r;
     r.x = (float)rx;
@@ -238,56 +243,47 @@ __device__ inline QF make_qf(const D3& q, const double* origin) {
     r.z = (float)rz;
     const double e = fmax(fmax(fabs(rx - (double)r.x), fabs(ry - (double)r.y)), fabs(rz - (double)r.z));
     r.e = __double2float_ru(e);
-    r.pe = __double2float_ru(4.76837158203125e-7 * (fabs((double)r.x) + fabs((double)r.y) + fabs((double)r.z)) + 2.0 * e);
+    const double l1 = fabs((double)r.x) + fabs((double)r.y) + fabs((double)r.z);
+    r.pe = __double2float_ru(9.5367431640625e-7 * l1 + 2.0 * e + tm);  // 2^-20 |q|_1
     return r;
 }
 
-// Lower bound of the squared distance from q to an fp32 box: per-axis gaps are shrunk by the fp32
-// subtraction error (<= 2^-24 relative) and the query rounding error, the sum by 3 roundings (2^-21).
-__host__ __device__ inline float box_d2_lo(const QF& q, float lx, float ly, float lz, float hx, float hy, float hz) {
-#ifdef MSH_FP32_CONTRACT
-#pragma clang fp contract(fast)
-#endif
-    const float k = 0.99999988079071044921875f;  // 1 - 2^-23
-    float gx = fmaxf(fmaxf(lx - q.x, q.x - hx), 0.f);
-    float gy = fmaxf(fmaxf(ly - q.y, q.y - hy), 0.f);
-    float gz = fmaxf(fmaxf(lz - q.z, q.z - hz), 0.f);
-    gx = fmaxf(gx * k - q.e, 0.f);
-    gy = fmaxf(gy * k - q.e, 0.f);
-    gz = fmaxf(gz * k - q.e, 0.f);
-    return (gx * gx + gy * gy + gz * gz) * 0.999999523162841796875f;  // 1 - 2^-21
-}
-
-// Lower bound of the squared distance from q to the oriented box {x : lo_k <= a_k . x <= hi_k} with
-// nearly orthonormal fp32 axes (n, t, b): the projections carry an error <= q.pe, the subtraction
-// 2^-24 relative, and the sum of squared slab gaps is divided by lambda_max(A A^T) <= 1 + 1e-6 (fp32
-// axes), covered by the factor 1 - 2^-18.
-__host__ __device__ inline float obb_d2_lo(const QF& q, const float* n, const float* t, const float* b, const float* ext) {
-#ifdef MSH_FP32_CONTRACT
-#pragma clang fp contract(fast)
-#endif
-    const float k = 0.99999988079071044921875f;  // 1 - 2^-23
-    const float pn = n[0] * q.x + n[1] * q.y + n[2] * q.z;
-    const float pt = t[0] * q.x + t[1] * q.y + t[2] * q.z;
-    const float pb = b[0] * q.x + b[1] * q.y + b[2] * q.z;
-    float gn = fmaxf(fmaxf(ext[0] - pn, pn - ext[3]), 0.f);
-    float gt = fmaxf(fmaxf(ext[1] - pt, pt - ext[4]), 0.f);
-    float gb = fmaxf(fmaxf(ext[2] - pb, pb - ext[5]), 0.f);
-    gn = fmaxf(gn * k - q.pe, 0.f);
-    gt = fmaxf(gt * k - q.pe, 0.f);
-    gb = fmaxf(gb * k - q.pe, 0.f);
-    return (gn * gn + gt * gt + gb * gb) * 0.999996185302734375f;  // 1 - 2^-18
-}
-
-// Both children's lower bounds from one node: the oriented-box bound of each child.  (Round 1 also kept
-// an fp32 AABB per child and used max(AABB, OBB): 4 % fewer node visits, but 9 % slower on C3 and twice
-// the node bytes.)
+// Both children's lower bounds of the squared distance from the query to their oriented boxes
+// {x : lo_k <= a_k . x <= hi_k}, axes a = (n, t, b = n x t) in fp32, lo/hi = base + u 2^e.
+// Per axis: p = fl(a . q) (fma dot product, error <= pe0 = 2^-21 |q|_1 + 2e with the query rounding);
+// the gaps are formed as fma(u_lo, 2^e, base - (p + pe)) and fma(-u_hi, 2^e, (p - pe) - base), i.e. the
+// decoded bound and the margin folded into one rounding each.  pe (make_qf) adds 2^-21 (1.25 M + |q|_1)
+// to pe0, M = the tree's largest half-diagonal, which covers the roundings of p +- pe and base - (..)
+// (<= 2^-23 (|base| + |bound| + |p| + pe), and |base|, |bound| <= 1.02 M) and the one of the decoded
+// bound itself, so each computed gap g satisfies g <= (1 + 2^-24) * (true slab gap).  The sum of
+// squares (two fmas) is scaled by 1 - 2^-18, which covers those roundings and the division by
+// lambda_max(A A^T) <= 1 + 1e-6 of the nearly orthonormal fp32 axes.
 __device__ inline void node_child_bounds(const NodeV& nd, const QF& q, float& d0, float& d1) {
-    float n[3], t[3], b[3], e0[6], e1[6];
+    float n[3], t[3], b[3];
     nd.frame(n, t, b);
-    nd.extents(e0, e1);
-    d0 = obb_d2_lo(q, n, t, b, e0);
-    d1 = obb_d2_lo(q, n, t, b, e1);
+    const float p[3] = {fmaf(n[0], q.x, fmaf(n[1], q.y, n[2] * q.z)), fmaf(t[0], q.x, fmaf(t[1], q.y, t[2] * q.z)),
+                        fmaf(b[0], q.x, fmaf(b[1], q.y, b[2] * q.z))};
+    float lo[3], hi[3], sc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float base = nd.at(kBase + k);
+        lo[k] = base - (p[k] + q.pe);  // gap below the box: u_lo 2^e + lo
+        hi[k] = (p[k] - q.pe) - base;  // gap above the box: hi - u_hi 2^e
+        sc[k] = nd.scale(k);
+    }
+    const uint32_t w0 = nd.word(11), w1 = nd.word(12), w2 = nd.word(13);
+    const uint32_t u[12] = {w0 & 0xffu, (w0 >> 8) & 0xffu, (w0 >> 16) & 0xffu, w0 >> 24,
+                            w1 & 0xffu, (w1 >> 8) & 0xffu, (w1 >> 16) & 0xffu, w1 >> 24,
+                            w2 & 0xffu, (w2 >> 8) & 0xffu, (w2 >> 16) & 0xffu, w2 >> 24};
+    float g[2][3];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+            g[c][k] = fmaxf(fmaxf(fmaf((float)u[6 * c + k], sc[k], lo[k]), fmaf(-(float)u[6 * c + 3 + k], sc[k], hi[k])), 0.f);
+    const float c18 = 0.999996185302734375f;  // 1 - 2^-18
+    d0 = fmaf(g[0][0], g[0][0], fmaf(g[0][1], g[0][1], g[0][2] * g[0][2])) * c18;
+    d1 = fmaf(g[1][0], g[1][0], fmaf(g[1][1], g[1][1], g[1][2] * g[1][2])) * c18;
 }
 
 // fp64 oriented-box tools for the ray and triangle kernels (fp32 frame and extents widen exactly to fp64).

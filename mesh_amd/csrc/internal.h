@@ -100,6 +100,7 @@ struct msh_tree {
     void* d_leaves = nullptr;      // T TriRec or PtRec in Morton order
     float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {0, 0, 0};  // bbox of all primitives
     double origin[3] = {0, 0, 0};  // fp64 scene-box centre: all fp32 node bounds are relative to it
+    double half_diag = 0.0;        // largest half-diagonal of the (per-mesh) boxes around their origins
     double* d_orgs = nullptr;      // (B,3) per-mesh origins on the device (B = 1: a copy of origin)
     double* d_boxes = nullptr;     // (B,6) per-mesh boxes (batched trees: query Morton codes)
     uint32_t* d_vorder = nullptr;  // Morton order of the main vertices (lazily built for visibility)
@@ -143,6 +144,8 @@ int query_morton_batch(const msh_tree* tree, const double* d_q, size_t n, size_t
                        hipStream_t s);
 // keys[j] = vals[j] / per (the mesh of element vals[j]), for the second, per-mesh sort phase
 int mesh_keys(const uint32_t* vals, size_t n, size_t per, uint32_t* keys, hipStream_t s);
+// largest distance from origin to a corner of box (lo xyz, hi xyz): msh_tree::half_diag
+double half_diagonal(const double* box, const double* origin);
 // device copy of tree->origin (single-mesh trees; blob unpack)
 int upload_origin(msh_tree* tree, hipStream_t s);
 // Oriented-box pass over the packed leaves (needs the node ranges recorded by build_lbvh).

@@ -71,6 +71,7 @@ struct KnnArgs {
     double* out_w;
     double eps;
     double org[3];  // tree origin: fp32 node bounds are relative to it
+    double tm;      // tree_margin(tree->half_diag): the node bounds' share of the query margin (make_qf)
     // batched trees (msh_batch_build): slot i belongs to mesh i / qper (the batched sort is mesh-major),
     // whose root is node mesh * npm and whose origin is orgs[3 * mesh]; orgs == nullptr: single tree
     const double* orgs;
@@ -97,11 +98,11 @@ __device__ inline int query_root(const KnnArgs& a, size_t i, const D3& q, QF& qf
     if (a.orgs) {
         const size_t mb = i / a.qper;
         const double o[3] = {a.orgs[3 * mb], a.orgs[3 * mb + 1], a.orgs[3 * mb + 2]};
-        qf = make_qf(q, o);
+        qf = make_qf(q, o, a.tm);
         return (int)(mb * a.npm);
     }
     const double o[3] = {a.org[0], a.org[1], a.org[2]};
-    qf = make_qf(q, o);
+    qf = make_qf(q, o, a.tm);
     return 0;
 }
 
@@ -983,6 +984,7 @@ static KnnArgs tree_args(const msh_tree* tree, size_t S) {
     a.leaves = tree->d_leaves;
     a.T = tree->T;
     a.S = S;
+    a.tm = tree_margin(tree->half_diag);
     return a;
 }
 

@@ -37,7 +37,7 @@ def check_mesh(v, f):
     child = fl[:, 6:8].copy().view(np.int32)
     base = fl[:, 8:11]
     u = nodes[:, 44:56].reshape(T - 1, 2, 6).astype(np.float32)
-    ex = nodes[:, 56:59].copy().view(np.int8).astype(np.int32)
+    ex = nodes[:, 56:59].astype(np.int32) - 127  # biased exponent bytes
     scale = np.ldexp(np.float32(1.0), ex).astype(np.float32)  # (T-1, 3)
     # base + u * 2^e in fp32: the product is exact, the sum rounds once (as fmaf in the kernels)
     dec = (np.tile(base, 2)[:, None, :] + u * np.tile(scale, 2)[:, None, :]).astype(np.float32)  # (T-1, 2, 6)
