@@ -91,21 +91,38 @@ __host__ __device__ inline void frame_b(const float* n, const float* t, float* b
 }
 
 // ---- node loads ----
+// bit casts usable on the host (the bound property test) and the device
+__host__ __device__ inline float u2f(uint32_t u) {
+    union { uint32_t u; float f; } c;
+    c.u = u;
+    return c.f;
+}
+__host__ __device__ inline uint32_t f2u(float f) {
+    union { float f; uint32_t u; } c;
+    c.f = f;
+    return c.u;
+}
+// fp32 rounding of x towards +inf
+__host__ __device__ inline float f32_up(double x) {
+    const float f = (float)x;
+    return (double)f < x ? nextafterf(f, INFINITY) : f;
+}
+
 struct NodeV {
     float4 q[4];
-    __device__ float at(int i) const { return reinterpret_cast<const float*>(q)[i]; }
-    __device__ uint32_t word(int i) const { return __float_as_uint(at(i)); }
-    __device__ int child(int s) const { return __float_as_int(at(6 + s)); }
+    __host__ __device__ float at(int i) const { return reinterpret_cast<const float*>(q)[i]; }
+    __host__ __device__ uint32_t word(int i) const { return f2u(at(i)); }
+    __host__ __device__ int child(int s) const { return (int)word(6 + s); }
     // frame axes n, t and b = n x t
-    __device__ void frame(float* n, float* t, float* b) const {
+    __host__ __device__ void frame(float* n, float* t, float* b) const {
         n[0] = at(0); n[1] = at(1); n[2] = at(2);
         t[0] = at(3); t[1] = at(4); t[2] = at(5);
         frame_b(n, t, b);
     }
     // scale 2^e of axis k: the biased exponent byte shifted into an fp32 exponent field
-    __device__ float scale(int k) const { return __uint_as_float(((word(14) >> (8 * k)) & 0xffu) << 23); }
+    __host__ __device__ float scale(int k) const { return u2f(((word(14) >> (8 * k)) & 0xffu) << 23); }
     // decoded oriented extents of both children: e0/e1 = lo n t b, hi n t b
-    __device__ void extents(float* e0, float* e1) const {
+    __host__ __device__ void extents(float* e0, float* e1) const {
         const uint32_t w0 = word(11), w1 = word(12), w2 = word(13);
         const float sc[3] = {scale(0), scale(1), scale(2)};
         const float bs[3] = {at(kBase), at(kBase + 1), at(kBase + 2)};
@@ -235,16 +252,16 @@ struct QF {
     float x, y, z, e, pe;
 };
 __host__ __device__ inline double tree_margin(double half_diagonal) { return 5.9604644775390625e-7 * half_diagonal; }
-__device__ inline QF make_qf(const D3& q, const double* origin, double tm) {
+__host__ __device__ inline QF make_qf(const D3& q, const double* origin, double tm) {
     const double rx = q.x - origin[0], ry = q.y - origin[1], rz = q.z - origin[2];
     QF r;
     r.x = (float)rx;
     r.y = (float)ry;
     r.z = (float)rz;
     const double e = fmax(fmax(fabs(rx - (double)r.x), fabs(ry - (double)r.y)), fabs(rz - (double)r.z));
-    r.e = __double2float_ru(e);
+    r.e = f32_up(e);
     const double l1 = fabs((double)r.x) + fabs((double)r.y) + fabs((double)r.z);
-    r.pe = __double2float_ru(9.5367431640625e-7 * l1 + 2.0 * e + tm);  // 2^-20 |q|_1
+    r.pe = f32_up(9.5367431640625e-7 * l1 + 2.0 * e + tm);  // 2^-20 |q|_1
     return r;
 }
 
@@ -258,7 +275,7 @@ __device__ inline QF make_qf(const D3& q, const double* origin, double tm) {
 // bound itself, so each computed gap g satisfies g <= (1 + 2^-24) * (true slab gap).  The sum of
 // squares (two fmas) is scaled by 1 - 2^-18, which covers those roundings and the division by
 // lambda_max(A A^T) <= 1 + 1e-6 of the nearly orthonormal fp32 axes.
-__device__ inline void node_child_bounds(const NodeV& nd, const QF& q, float& d0, float& d1) {
+__host__ __device__ inline void node_child_bounds(const NodeV& nd, const QF& q, float& d0, float& d1) {
     float n[3], t[3], b[3];
     nd.frame(n, t, b);
     const float p[3] = {fmaf(n[0], q.x, fmaf(n[1], q.y, n[2] * q.z)), fmaf(t[0], q.x, fmaf(t[1], q.y, t[2] * q.z)),
