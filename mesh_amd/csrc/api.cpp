@@ -252,8 +252,11 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
 static const size_t kSortMin = 4096;  // below this the query Morton sort costs more than it saves
 
 // Query order for S point rows (device): below kSortMin the caller's arrays are used as they are;
-// otherwise Morton codes + radix sort give the permutation (ws.vals), and the rows (and normals, when
-// given) are gathered once into slot order (ws.qs / ws.ns) with the inverse permutation (ws.inv).
+// otherwise Morton codes + radix sort give the permutation (ws.vals).  With allow_lazy (closest-point
+// launches without normals) the traversal reads row perm[i] itself and writes the inverse permutation
+// (ws.inv); otherwise the rows (and normals, when given) are gathered once into slot order
+// (ws.qs / ws.ns) with the inverse permutation.  MSH_SLOT_GATHER=1 gathers always (A/B switch: the
+// gather is 3 % slower on C3).
 #ifndef MSH_SLOT_GATHER
 #define MSH_SLOT_GATHER 0
 #endif
@@ -266,9 +269,7 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
     MSH_TRY(ws.vals.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.keys_alt.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.vals_alt.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.qs.reserve(3 * S * sizeof(double)));
     MSH_TRY(ws.inv.reserve(S * sizeof(uint32_t)));
-    if (d_n) MSH_TRY(ws.ns.reserve(3 * S * sizeof(double)));
     MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
     MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
                              ws.vals_alt.as<uint32_t>(), S, 30, ws, s));
@@ -276,6 +277,8 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
         *ord = QueryOrder{d_q, nullptr, ws.vals.as<uint32_t>(), ws.inv.as<uint32_t>(), false};
         return MSH_OK;
     }
+    MSH_TRY(ws.qs.reserve(3 * S * sizeof(double)));
+    if (d_n) MSH_TRY(ws.ns.reserve(3 * S * sizeof(double)));
     MSH_TRY(gather_rows(d_q, d_n, ws.vals.as<uint32_t>(), S, ws.qs.as<double>(), d_n ? ws.ns.as<double>() : nullptr,
                         ws.inv.as<uint32_t>(), s));
     *ord = QueryOrder{ws.qs.as<double>(), d_n ? ws.ns.as<double>() : nullptr, ws.vals.as<uint32_t>(),
