@@ -10,7 +10,8 @@
 //                                      augmenting them with the sorted position; also records each
 //                                      node's contiguous leaf range and split
 //   6. k_depth                         max leaf depth (sizes the traversal stack spill)
-//   7. (after leaf packing) k_obb      one wave per node over its Morton leaf range: area-weighted
+//   7. (after leaf packing) k_obb_lane / k_obb_wave   one lane (<= 32 leaves) or one wave per node over
+//                                      its Morton leaf range: area-weighted
 //                                      normal -> node frame (n, t, b = n x t), then both children's vertex
 //                                      extents along the frame (oriented boxes, thin along the surface),
 //                                      quantised to 8 bits against a per-node base and power-of-two scale
@@ -260,107 +261,167 @@ __device__ inline int leaf_points(const void* leaves, int i, D3* p) {
     return 1;
 }
 
+// Node frame from the area-weighted normal sum (sx, sy, sz): n, t = e - (e.n) n normalised (e the x or y
+// axis), b = n x t in fp32; A = the fp32 axes widened to fp64 (what the vertices are projected on).
+struct ObbFrame {
+    float n[3], t[3], b[3];
+    double A[3][3];
+};
+__device__ inline ObbFrame obb_frame(double sx, double sy, double sz) {
+    const double len = sqrt(sx * sx + sy * sy + sz * sz);
+    const D3 n = (len > 0.0 && len < INFINITY) ? D3{sx / len, sy / len, sz / len} : D3{1.0, 0.0, 0.0};
+    const D3 e = fabs(n.x) < 0.9 ? D3{1.0, 0.0, 0.0} : D3{0.0, 1.0, 0.0};
+    D3 t = vsub(e, vscale(vdot(e, n), n));
+    const double tl = sqrt(vdot(t, t));
+    t = D3{t.x / tl, t.y / tl, t.z / tl};
+    ObbFrame f;
+    f.n[0] = (float)n.x; f.n[1] = (float)n.y; f.n[2] = (float)n.z;
+    f.t[0] = (float)t.x; f.t[1] = (float)t.y; f.t[2] = (float)t.z;
+    frame_b(f.n, f.t, f.b);
+    for (int k = 0; k < 3; ++k) {
+        f.A[0][k] = f.n[k];
+        f.A[1][k] = f.t[k];
+        f.A[2][k] = f.b[k];
+    }
+    return f;
+}
+
+// area vector (p1 - p0) x (p2 - p0) of leaf i (points: none)
 template <bool TRI>
-__global__ __launch_bounds__(kBlock) void k_obb(const void* __restrict__ leaves, const int4* __restrict__ ranges, int nn,
-                                                int npm, BNode* __restrict__ nodes, const double* __restrict__ orgs) {
+__device__ inline D3 leaf_area(const void* leaves, int i) {
+    if (!TRI) return D3{0.0, 0.0, 0.0};
+    D3 p[3];
+    leaf_points<TRI>(leaves, i, p);
+    return vcross(vsub(p[1], p[0]), vsub(p[2], p[0]));
+}
+
+// min / max projections onto the frame of leaf i's points (relative to the origin o)
+template <bool TRI>
+__device__ inline void leaf_extent(const void* leaves, int i, const ObbFrame& f, const double* o, double* mn, double* mx) {
+    D3 p[3];
+    const int np = leaf_points<TRI>(leaves, i, p);
+    for (int c = 0; c < np; ++c) {
+        const double rx = p[c].x - o[0], ry = p[c].y - o[1], rz = p[c].z - o[2];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double pr = f.A[k][0] * rx + f.A[k][1] * ry + f.A[k][2] * rz;
+            mn[k] = fmin(mn[k], pr);
+            mx[k] = fmax(mx[k], pr);
+        }
+    }
+}
+
+// smallest e in [-126, 127] with 254 * 2^e >= range (127 for a non-finite range)
+__device__ inline int scale_exponent(double range) {
+    if (!(range < 1e38)) return 127;
+    int e = range > 0.0 ? ilogb(range / 254.0) : -126;
+    e = max(-126, min(127, e));
+    while (e < 127 && 254.0 * (double)exp2_scale(e) < range) ++e;
+    while (e > -126 && 254.0 * (double)exp2_scale(e - 1) >= range) --e;
+    return e;
+}
+
+// Write node: frame, and both children's fp32 extents ext[side][lo n t b, hi n t b] quantised against
+// base = min lower bound with scale 2^e per axis (254 * 2^e >= range); lower codes round down and upper
+// codes up, checked with the decoder's own expression, so the decoded box contains the fp32 one.
+__device__ inline void encode_node(BNode* node, const ObbFrame& fr, const float (*ext)[6]) {
+    float* f = node->f;
+    float base[3];
+    int ex[3];
+    uint32_t u[12];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        base[k] = fminf(ext[0][k], ext[1][k]);
+        const double top = fmax((double)ext[0][3 + k], (double)ext[1][3 + k]);
+        const int e = scale_exponent(top - (double)base[k]);
+        ex[k] = e;
+        const float sc = exp2_scale(e);
+#pragma unroll
+        for (int side = 0; side < 2; ++side) {
+            const float lo = ext[side][k], hi = ext[side][3 + k];
+            const double ql = floor(((double)lo - (double)base[k]) / (double)sc);
+            const double qh = ceil(((double)hi - (double)base[k]) / (double)sc);
+            uint32_t ul = (uint32_t)fmin(fmax(ql, 0.0), 255.0), uh = (uint32_t)fmin(fmax(qh, 0.0), 255.0);
+            while (ul > 0u && dequant(ul, sc, base[k]) > lo) --ul;
+            while (uh < 255u && dequant(uh, sc, base[k]) < hi) ++uh;
+            u[6 * side + k] = ul;
+            u[6 * side + 3 + k] = uh;
+        }
+    }
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) w[j] = u[4 * j] | (u[4 * j + 1] << 8) | (u[4 * j + 2] << 16) | (u[4 * j + 3] << 24);
+    // biased exponents (e + 127 in [1, 254]): the decoder shifts them into an fp32 exponent field
+    w[3] = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
+    *reinterpret_cast<float4*>(f) = make_float4(fr.n[0], fr.n[1], fr.n[2], fr.t[0]);
+    *reinterpret_cast<float2*>(f + 4) = make_float2(fr.t[1], fr.t[2]);
+    *reinterpret_cast<float4*>(f + 8) = make_float4(base[0], base[1], base[2], __uint_as_float(w[0]));
+    *reinterpret_cast<float4*>(f + 12) = make_float4(__uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3]), 0.0f);
+}
+
+constexpr int kObbLane = 32;  // nodes over at most this many leaves: one lane each; larger: one wave each
+
+// Oriented boxes of nodes over at most kObbLane leaves, one lane per node (most nodes: the lower levels)
+template <bool TRI>
+__global__ __launch_bounds__(kBlock) void k_obb_lane(const void* __restrict__ leaves, const int4* __restrict__ ranges,
+                                                     int nn, int npm, BNode* __restrict__ nodes,
+                                                     const double* __restrict__ orgs) {
+    const int node = blockIdx.x * kBlock + threadIdx.x;
+    if (node >= nn) return;
+    const int4 r = ranges[node];
+    if (r.y - r.x + 1 > kObbLane) return;
+    const int mb = node / npm;  // mesh of the node (npm internal nodes per mesh)
+    const double o[3] = {orgs[3 * mb], orgs[3 * mb + 1], orgs[3 * mb + 2]};
+    double sx = 0, sy = 0, sz = 0;
+    for (int i = r.x; i <= r.y; ++i) {
+        const D3 c = leaf_area<TRI>(leaves, i);
+        sx += c.x; sy += c.y; sz += c.z;
+    }
+    const ObbFrame fr = obb_frame(sx, sy, sz);
+    float ext[2][6];
+    for (int side = 0; side < 2; ++side) {
+        double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+        const int b = side == 0 ? r.x : r.z + 1, e = side == 0 ? r.z : r.y;
+        for (int i = b; i <= e; ++i) leaf_extent<TRI>(leaves, i, fr, o, mn, mx);
+        for (int k = 0; k < 3; ++k) {
+            ext[side][k] = out_lo(mn[k]);
+            ext[side][3 + k] = out_hi(mx[k]);
+        }
+    }
+    encode_node(nodes + node, fr, ext);
+}
+
+// Oriented boxes of nodes over more than kObbLane leaves, one wave per node over its Morton leaf range
+template <bool TRI>
+__global__ __launch_bounds__(kBlock) void k_obb_wave(const void* __restrict__ leaves, const int4* __restrict__ ranges,
+                                                     int nn, int npm, BNode* __restrict__ nodes,
+                                                     const double* __restrict__ orgs) {
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (kBlock / 64);
     for (int node = (blockIdx.x * kBlock + threadIdx.x) >> 6; node < nn; node += waves) {
-        const int mb = node / npm;  // mesh of the node (npm internal nodes per mesh)
-        const double ox = orgs[3 * mb], oy = orgs[3 * mb + 1], oz = orgs[3 * mb + 2];
         const int4 r = ranges[node];
-        // area-weighted normal of the node's triangles (points: no area -> axis-aligned frame)
+        if (r.y - r.x + 1 <= kObbLane) continue;
+        const int mb = node / npm;
+        const double o[3] = {orgs[3 * mb], orgs[3 * mb + 1], orgs[3 * mb + 2]};
         double sx = 0, sy = 0, sz = 0;
-        if (TRI) {
-            for (int i = r.x + lane; i <= r.y; i += 64) {
-                D3 p[3];
-                leaf_points<TRI>(leaves, i, p);
-                const D3 c = vcross(vsub(p[1], p[0]), vsub(p[2], p[0]));
-                sx += c.x; sy += c.y; sz += c.z;
-            }
-            sx = wsum(sx); sy = wsum(sy); sz = wsum(sz);
+        for (int i = r.x + lane; i <= r.y; i += 64) {
+            const D3 c = leaf_area<TRI>(leaves, i);
+            sx += c.x; sy += c.y; sz += c.z;
         }
-        const double len = sqrt(sx * sx + sy * sy + sz * sz);
-        D3 n = (len > 0.0 && len < INFINITY) ? D3{sx / len, sy / len, sz / len} : D3{1.0, 0.0, 0.0};
-        const D3 e = fabs(n.x) < 0.9 ? D3{1.0, 0.0, 0.0} : D3{0.0, 1.0, 0.0};
-        D3 t = vsub(e, vscale(vdot(e, n), n));
-        const double tl = sqrt(vdot(t, t));
-        t = D3{t.x / tl, t.y / tl, t.z / tl};
-        const float n32[3] = {(float)n.x, (float)n.y, (float)n.z};
-        const float t32[3] = {(float)t.x, (float)t.y, (float)t.z};
-        float b32[3];
-        frame_b(n32, t32, b32);
-        const double A[3][3] = {{n32[0], n32[1], n32[2]}, {t32[0], t32[1], t32[2]}, {b32[0], b32[1], b32[2]}};
+        const ObbFrame fr = obb_frame(wsum(sx), wsum(sy), wsum(sz));
         float ext[2][6];
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
-            const int b = side == 0 ? r.x : r.z + 1;
-            const int eidx = side == 0 ? r.z : r.y;
             double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
-            for (int i = b + lane; i <= eidx; i += 64) {
-                D3 p[3];
-                const int np = leaf_points<TRI>(leaves, i, p);
-                for (int c = 0; c < np; ++c) {
-                    const double rx = p[c].x - ox, ry = p[c].y - oy, rz = p[c].z - oz;
-#pragma unroll
-                    for (int k = 0; k < 3; ++k) {
-                        const double pr = A[k][0] * rx + A[k][1] * ry + A[k][2] * rz;
-                        mn[k] = fmin(mn[k], pr);
-                        mx[k] = fmax(mx[k], pr);
-                    }
-                }
-            }
+            const int b = side == 0 ? r.x : r.z + 1, e = side == 0 ? r.z : r.y;
+            for (int i = b + lane; i <= e; i += 64) leaf_extent<TRI>(leaves, i, fr, o, mn, mx);
 #pragma unroll
             for (int k = 0; k < 3; ++k) {
                 ext[side][k] = out_lo(wmin(mn[k]));
                 ext[side][3 + k] = out_hi(wmax(mx[k]));
             }
         }
-        if (lane == 0) {
-            float* f = nodes[node].f;
-            *reinterpret_cast<float4*>(f) = make_float4(n32[0], n32[1], n32[2], t32[0]);
-            *reinterpret_cast<float2*>(f + 4) = make_float2(t32[1], t32[2]);
-            // quantise both children's extents against base = min lower bound, scale 2^e per axis with
-            // 254 * 2^e >= range; lower codes round down and upper codes up, checked with the decoder's
-            // own expression, so the decoded box contains the fp32 one
-            float base[3];
-            int ex[3];
-            uint32_t u[12];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) {
-                base[k] = fminf(ext[0][k], ext[1][k]);
-                const double top = fmax((double)ext[0][3 + k], (double)ext[1][3 + k]);
-                const double range = top - (double)base[k];
-                int e = -126;
-                if (!(range < 1e38)) e = 127;
-                else
-                    while (e < 127 && 254.0 * (double)exp2_scale(e) < range) ++e;
-                ex[k] = e;
-                const float sc = exp2_scale(e);
-#pragma unroll
-                for (int side = 0; side < 2; ++side) {
-                    const float lo = ext[side][k], hi = ext[side][3 + k];
-                    double ql = floor(((double)lo - (double)base[k]) / (double)sc);
-                    double qh = ceil(((double)hi - (double)base[k]) / (double)sc);
-                    uint32_t ul = (uint32_t)fmin(fmax(ql, 0.0), 255.0), uh = (uint32_t)fmin(fmax(qh, 0.0), 255.0);
-                    while (ul > 0u && dequant(ul, sc, base[k]) > lo) --ul;
-                    while (uh < 255u && dequant(uh, sc, base[k]) < hi) ++uh;
-                    u[6 * side + k] = ul;
-                    u[6 * side + 3 + k] = uh;
-                }
-            }
-            f[kBase] = base[0];
-            f[kBase + 1] = base[1];
-            f[kBase + 2] = base[2];
-            uint32_t w[4];
-#pragma unroll
-            for (int j = 0; j < 3; ++j) w[j] = u[4 * j] | (u[4 * j + 1] << 8) | (u[4 * j + 2] << 16) | (u[4 * j + 3] << 24);
-            // biased exponents (e + 127 in [1, 254]): the decoder shifts them into an fp32 exponent field
-            w[3] = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
-            *reinterpret_cast<float4*>(f + 11) = make_float4(__uint_as_float(w[0]), __uint_as_float(w[1]),
-                                                             __uint_as_float(w[2]), __uint_as_float(w[3]));
-            f[15] = 0.0f;
-        }
+        if (lane == 0) encode_node(nodes + node, fr, ext);
     }
 }
 
@@ -433,10 +494,14 @@ int build_obb(msh_tree* tree, bool triangles) {
     hipStream_t s = tree->stream;
     const int4* ranges = tree->ws.ranges.as<int4>();
     const int npm = (int)(tree->T - 1);  // internal nodes per mesh
-    if (triangles)
-        k_obb<true><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
-    else
-        k_obb<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
+    const unsigned lane_blocks = (unsigned)(((size_t)nn + kBlock - 1) / kBlock);
+    if (triangles) {
+        k_obb_lane<true><<<lane_blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
+        k_obb_wave<true><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
+    } else {
+        k_obb_lane<false><<<lane_blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
+        k_obb_wave<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
+    }
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }
