@@ -22,7 +22,8 @@
 //                    ora_brute_nearest   (exhaustive, lexicographic min (d², face))
 //                    ora_point_triangle  (one query / one face: point, part, d²)
 //   normals metric:  ora_cgal_ntree_nearest (CGAL AABB_n_tree semantics), ora_brute_nnearest
-//   rays:            ora_brute_alongnormal, ora_brute_visibility
+//   rays:            ora_cgal_tree_alongnormal, ora_cgal_tree_visibility (CGAL tree traversal,
+//                    the C5 CPU baseline), ora_brute_alongnormal, ora_brute_visibility
 //   tri-tri:         ora_tri_tri_overlap, ora_brute_intersections, ora_brute_selfintersects
 //   vertex NN:       ora_brute_vertex_nn
 #include <algorithm>
@@ -448,6 +449,52 @@ struct CgalTree {
                 }
         }
     }
+    // --- Ray traversal (AABB_tree::all_intersections / do_intersect with a Ray_3 query) ---
+    // Ray_3 / Bbox_3 do_intersect: closed slab test, t in [0, +inf) (CGAL's
+    // do_intersect_bbox_segment_aux with the far end unbounded), in double.
+    static bool ray_box(const P3& p, const P3& d, const Box& b) {
+        double tmin = 0.0, tmax = std::numeric_limits<double>::infinity();
+        const double pc[3] = {p.x, p.y, p.z}, dc[3] = {d.x, d.y, d.z};
+        for (int k = 0; k < 3; ++k) {
+            if (dc[k] == 0.0) {
+                if (pc[k] < b.lo[k] || pc[k] > b.hi[k]) return false;
+                continue;
+            }
+            double t0 = (b.lo[k] - pc[k]) / dc[k], t1 = (b.hi[k] - pc[k]) / dc[k];
+            if (t0 > t1) std::swap(t0, t1);
+            tmin = std::max(tmin, t0);
+            tmax = std::min(tmax, t1);
+            if (tmin > tmax) return false;
+        }
+        return true;
+    }
+    struct RayHit { double t; uint32_t prim; int kind; };
+    // Listing_primitive_traits: every primitive hit, appended in left-first traversal order.
+    template <class F>
+    bool ray_traverse(const P3& p, const P3& d, size_t node, size_t nb, F& on_prim) const {
+        const CgalNode& n = nodes[node];
+        switch (nb) {
+            case 2:
+                if (on_prim(prim[~n.left])) return true;
+                return on_prim(prim[~n.right]);
+            case 3:
+                if (on_prim(prim[~n.left])) return true;
+                if (ray_box(p, d, nodes[n.right].box)) return ray_traverse(p, d, n.right, 2, on_prim);
+                return false;
+            default:
+                if (ray_box(p, d, nodes[n.left].box) && ray_traverse(p, d, n.left, nb / 2, on_prim)) return true;
+                if (ray_box(p, d, nodes[n.right].box)) return ray_traverse(p, d, n.right, nb - nb / 2, on_prim);
+                return false;
+        }
+    }
+    // on_prim returns true to stop (do_intersect's first-hit exit).
+    template <class F>
+    void ray_query(const P3& p, const P3& d, F& on_prim) const {
+        if (mesh.T == 1) { on_prim(prim[0]); return; }
+        // AABB_tree::traversal tests the root box before descending
+        if (!nodes.empty() && ray_box(p, d, nodes[0].box)) ray_traverse(p, d, 0, mesh.T, on_prim);
+    }
+
     ProjN nnearest(const P3& q, const P3& qn) const {
         // hint = any_reference_point_and_id(): first primitive in tree order (AABB_n_tree.h:279)
         ProjN st;
@@ -716,6 +763,99 @@ void ora_cgal_ntree_nearest(void* h, const double* q, const double* n, size_t S,
         CgalTree::ProjN r = t->nnearest(mk(q + 3 * s), mk(n + 3 * s));
         face[s] = r.prim;
         pt[3 * s] = r.point.x; pt[3 * s + 1] = r.point.y; pt[3 * s + 2] = r.point.z;
+    }
+}
+
+// ---- nearest_alongnormal through the CGAL tree (spatialsearchmodule.cpp:272-321): all_intersections
+// of Ray_3(p, n) then Ray_3(p, -n) in traversal order, first minimum distance (std::min_element, :314).
+// Same hit constructions as ora_brute_alongnormal; differs from it only in which face wins an exact tie.
+void ora_cgal_tree_alongnormal(void* h, const double* p, const double* n, size_t S, double* dist, uint32_t* face,
+                               double* pt, int threads, uint64_t* tests) {
+    const CgalTree* t = static_cast<CgalTree*>(h);
+    set_threads(threads);
+    uint64_t total = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : total)
+    for (long s = 0; s < (long)S; ++s) {
+        const P3 pp = mk(p + 3 * s), nn = mk(n + 3 * s);
+        const P3 nneg{-nn.x, -nn.y, -nn.z};
+        double best = 1e100;
+        uint32_t bf = 0xFFFFFFFFu;
+        P3 bp{NAN, NAN, NAN};
+        bool any = false;
+        uint64_t ntest = 0;
+        for (int k = 0; k < 2; ++k) {
+            const P3 d = ray_dir(pp, k ? nneg : nn);
+            auto on_prim = [&](uint32_t f) {
+                ++ntest;
+                const P3 &ta = t->mesh.tri[3 * (size_t)f], &tb = t->mesh.tri[3 * (size_t)f + 1],
+                         &tc = t->mesh.tri[3 * (size_t)f + 2];
+                double tt;
+                const int kind = ray_tri_kind(pp, d, ta, tb, tc, tt);
+                if (!kind) return false;
+                P3 hit;
+                if (kind == 2 || !cgal_plane_line(pp, d, ta, tb, tc, hit)) hit = add(pp, scale(tt, d));
+                const double dd = std::sqrt(sqd(hit, pp));
+                if (!any || dd < best) { best = dd; bf = f; bp = hit; any = true; }
+                return false;
+            };
+            t->ray_query(pp, d, on_prim);
+        }
+        total += ntest;
+        dist[s] = best;
+        face[s] = bf;
+        pt[3 * s] = bp.x; pt[3 * s + 1] = bp.y; pt[3 * s + 2] = bp.z;
+    }
+    if (tests) *tests = total;
+}
+
+// ---- visibility_compute through the CGAL tree (visibility.cpp:75-115): tree.do_intersect(Ray) stops at
+// the first hit.  The tree holds main + extra triangles (py_visibility.cpp:140-163); v are the main
+// vertices.  Cameras in the outer loop as the reference's VisibilityTask; vertices in parallel.
+void ora_cgal_tree_visibility(void* h, const double* v, size_t P, const double* cams, size_t C, const double* normals,
+                              const double* sensors, double min_dist, uint32_t* vis, double* ndc, int threads) {
+    const CgalTree* t = static_cast<CgalTree*>(h);
+    set_threads(threads);
+    // (camera, vertex) pairs in camera-major order, as VisibilityTask visits them; parallel over both.
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long o = 0; o < (long)(C * P); ++o) {
+        const size_t ic = (size_t)o / P, iv = (size_t)o % P;
+        const P3 cam = mk(cams + 3 * ic);
+        P3 xoff{0, 0, 0}, yoff{0, 0, 0}, zoff{0, 0, 0};
+        double planeoff = 0.0;
+        if (sensors) {
+            const double* s = sensors + 9 * ic;
+            xoff = P3{s[0], s[1], s[2]};
+            yoff = P3{s[3], s[4], s[5]};
+            zoff = P3{-s[6], -s[7], -s[8]};
+            planeoff = dot(zoff, add(cam, zoff));
+        }
+        const P3 vv = mk(v + 3 * iv);
+        P3 dir = vec(vv, cam);
+        const double len = std::sqrt(dot(dir, dir));
+        dir = P3{dir.x / len, dir.y / len, dir.z / len};
+        const P3 src = add(vv, scale(min_dist, dir));
+        const P3 d = ray_dir(src, dir);
+        bool hit = false;
+        auto on_prim = [&](uint32_t f) {
+            double tt;
+            hit = ray_tri(src, d, t->mesh.tri[3 * (size_t)f], t->mesh.tri[3 * (size_t)f + 1],
+                          t->mesh.tri[3 * (size_t)f + 2], tt);
+            return hit;
+        };
+        t->ray_query(src, d, on_prim);
+        const uint32_t reach = hit ? 0u : 1u;
+        ndc[o] = normals ? dot(mk(normals + 3 * iv), dir) : 0.0;
+        if (sensors) {
+            if (reach) {
+                const double tp = -(dot(zoff, vv) - planeoff) / dot(zoff, dir);
+                const P3 pi = sub(add(vv, scale(tp, dir)), add(cam, zoff));
+                vis[o] = (std::fabs(dot(pi, xoff)) < dot(xoff, xoff) && std::fabs(dot(pi, yoff)) < dot(yoff, yoff)) ? 1u : 0u;
+            } else {
+                vis[o] = 0u;
+            }
+        } else {
+            vis[o] = reach;
+        }
     }
 }
 

@@ -41,6 +41,12 @@ def lib():
         L.ora_cgal_tree_nearest.restype = None
         L.ora_cgal_ntree_nearest.argtypes = [vp, _c_double_p, _c_double_p, sz, _c_u32_p, _c_double_p, i]
         L.ora_cgal_ntree_nearest.restype = None
+        L.ora_cgal_tree_alongnormal.argtypes = [vp, _c_double_p, _c_double_p, sz, _c_double_p, _c_u32_p, _c_double_p,
+                                                i, _c_u64_p]
+        L.ora_cgal_tree_alongnormal.restype = None
+        L.ora_cgal_tree_visibility.argtypes = [vp, _c_double_p, sz, _c_double_p, sz, _c_double_p, _c_double_p,
+                                               ctypes.c_double, _c_u32_p, _c_double_p, i]
+        L.ora_cgal_tree_visibility.restype = None
         L.ora_brute_nearest.argtypes = [_c_double_p, sz, _c_u32_p, sz, _c_double_p, sz, _c_u32_p, _c_u32_p,
                                         _c_double_p, _c_double_p, i]
         L.ora_brute_nearest.restype = None
@@ -123,6 +129,49 @@ class CgalTree(object):
         pt = np.empty((S, 3))
         lib().ora_cgal_ntree_nearest(self.h, _pd(q), _pd(n), S, _pu(face), _pd(pt), int(threads))
         return face, pt
+
+    def alongnormal(self, p, n, threads=0, count_tests=False):
+        """aabbtree_nearest_alongnormal through the tree (spatialsearchmodule.cpp:272-321):
+        (dist, face, point); no hit -> 1e100, 0xFFFFFFFF, NaN."""
+        p, n = _d(p).reshape(-1, 3), _d(n).reshape(-1, 3)
+        S = p.shape[0]
+        dist = np.empty(S)
+        face = np.empty(S, np.uint32)
+        pt = np.empty((S, 3))
+        tests = np.zeros(1, np.uint64)
+        lib().ora_cgal_tree_alongnormal(self.h, _pd(p), _pd(n), S, _pd(dist), _pu(face), _pd(pt), int(threads),
+                                        tests.ctypes.data_as(_c_u64_p) if count_tests else None)
+        if count_tests:
+            return dist, face, pt, int(tests[0])
+        return dist, face, pt
+
+
+class CgalVisibilityTree(CgalTree):
+    """visibility_compute's tree over main + extra triangles (py_visibility.cpp:140-163), no hint."""
+
+    def __init__(self, v, f, extra_v=None, extra_f=None):
+        v, f = _d(v), _u(f)
+        self.main_v = v
+        if extra_v is not None and extra_f is not None:
+            ev, ef = _d(extra_v), _u(extra_f)
+            f = np.vstack([f, ef + np.uint32(v.shape[0])])
+            v = np.vstack([v, ev])
+        super().__init__(v, f, hint=False)
+
+    def visibility(self, cams, n=None, sensors=None, min_dist=1e-3, threads=0, src_idx=None):
+        """(vis (C,P'), ndc (C,P')) cast from the main vertices (or v[src_idx])."""
+        cams = _d(cams).reshape(-1, 3)
+        v = self.main_v if src_idx is None else _d(self.main_v[np.asarray(src_idx)])
+        if n is not None and src_idx is not None:
+            n = np.asarray(n)[np.asarray(src_idx)]
+        P, C = v.shape[0], cams.shape[0]
+        vis = np.empty((C, P), np.uint32)
+        ndc = np.empty((C, P))
+        nn = _d(n) if n is not None else None
+        ss = _d(sensors) if sensors is not None else None
+        lib().ora_cgal_tree_visibility(self.h, _pd(v), P, _pd(cams), C, _pd(nn), _pd(ss), float(min_dist), _pu(vis),
+                                       _pd(ndc), int(threads))
+        return vis, ndc
 
 
 def brute_nearest(v, f, q, threads=0):

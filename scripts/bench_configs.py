@@ -68,6 +68,27 @@ def cpu_rates(v, f, q, budget_s=6.0):
     return out[0], out[1], host_threads()
 
 
+def cpu_chunk_rates(run, units_per_item, n_items, budget_s=6.0):
+    """run(lo, hi, threads) processes items [lo, hi) on the oracle; returns (1-thread units/s, all-thread
+    units/s, threads): median of 5 timed chunks after 2 warm-ups per mode, chunks sized to the budget."""
+    out = []
+    for threads in (1, host_threads()):
+        n = min(n_items, 50 * threads)
+        t0 = time.perf_counter()
+        run(0, n, threads)
+        rate = n / max(time.perf_counter() - t0, 1e-6)
+        chunk = int(min(max(rate * budget_s / 2 / 7, 8), n_items))
+        rates = []
+        for k in range(7):
+            lo = (k * chunk) % max(n_items - chunk, 1)
+            t0 = time.perf_counter()
+            run(lo, lo + chunk, threads)
+            if k >= 2:
+                rates.append(chunk * units_per_item / (time.perf_counter() - t0))
+        out.append(float(np.median(rates)))
+    return out[0], out[1], host_threads()
+
+
 def c1(reps):
     from mesh_amd.search import AabbTree
     from mesh_amd.mesh import Mesh
@@ -205,6 +226,7 @@ def c5(reps):
                                                       _native.ctypes.byref(leaves)))
     R = C * P
     nn_v, nl_v = nodes.value / R, leaves.value / R
+    cpu = c5_cpu(v, f, p, n, cams, vn) if os.environ.get("MESH_AMD_NO_CPU") != "1" else {}
     b_v = 12 + 48.0 / C + nb * nn_v + lb * nl_v  # 12 B out per ray, 48 B in amortised over C cameras
     return {"config": "C5 bumped icosphere (5,000,000 faces / 2,500,002 v): 10M nearest_alongnormal rays; "
                       "visibility 64 Fibonacci cameras x 2.5M vertices (160M rays), vertex normals",
@@ -217,7 +239,31 @@ def c5(reps):
                            "achieved_GBps": R * b_v / (k_v / 1e3) / 1e9,
                            "frac_of_8TBps": R * b_v / (k_v / 1e3) / 8e12,
                            "visible_fraction": float(vis.double().mean().item())},
-            "build_ms_gpu": info.build_ms}
+            "build_ms_gpu": info.build_ms, **cpu}
+
+
+def c5_cpu(v, f, p, n, cams, vn):
+    """C5 on the oracle's CGAL-tree restatement (median-split tree, no hint; ray/box slab tests, the
+    reference's all_intersections of both rays / do_intersect first-hit exit): rays per second on samples
+    of the same rays (alongnormal) and of the same vertices seen from all 64 cameras (visibility)."""
+    from oracle import oracle as O
+    t0 = time.perf_counter()
+    tree = O.CgalVisibilityTree(v, f)
+    build_s = time.perf_counter() - t0
+    rng = np.random.default_rng(55)
+    sp = rng.permutation(p.shape[0])[:2_000_000]
+    ps, ns = np.ascontiguousarray(p[sp]), np.ascontiguousarray(n[sp])
+    a1, am, th = cpu_chunk_rates(lambda lo, hi, t: tree.alongnormal(ps[lo:hi], ns[lo:hi], threads=t), 1,
+                                 ps.shape[0])
+    sv = rng.permutation(v.shape[0])
+    C = cams.shape[0]
+    v1, vm, _ = cpu_chunk_rates(lambda lo, hi, t: tree.visibility(cams, n=vn, src_idx=sv[lo:hi], threads=t), C,
+                                sv.shape[0])
+    return {"cpu_ref_threads": th, "cpu_tree_build_s": build_s,
+            "cpu_ref_alongnormal_1t_rays_per_s": a1, "cpu_ref_alongnormal_omp_rays_per_s": am,
+            "cpu_ref_visibility_1t_rays_per_s": v1, "cpu_ref_visibility_omp_rays_per_s": vm,
+            "cpu_sample": "random subsets of the same 10M alongnormal rays / of the 2.5M vertices x 64 cameras; "
+                          "median of 5 timed chunks after 2 warm-ups, ~6 s per mode"}
 
 
 def main():

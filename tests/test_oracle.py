@@ -223,3 +223,44 @@ def test_alongnormal_point_is_cgal_plane_line(oracle):
     assert np.allclose(d[hit], np.linalg.norm(pt[hit] - p[hit], axis=1), rtol=0, atol=0)
     off = np.cross(pt[hit] - p[hit], n[hit]) / np.linalg.norm(n[hit], axis=1)[:, None]
     assert np.abs(off).max() < 1e-12
+
+
+def test_cgal_tree_alongnormal_vs_brute(oracle):
+    # the tree traversal (all_intersections of both rays, first minimum) finds the same nearest hit
+    # as the exhaustive scan: equal distance everywhere, equal face and point unless two faces tie
+    v, f = W.geodesic_icosphere(8)
+    p, _ = W.surface_samples(v, f, 3000, seed=23, sigma=0.05)
+    n = np.random.default_rng(24).normal(size=p.shape)
+    p = np.vstack([p, [[5.0, 5.0, 5.0]]])  # misses both ways
+    n = np.vstack([n, [[1.0, 0.0, 0.0]]])
+    td, tf, tpt = oracle.CgalTree(v, f, hint=False).alongnormal(p, n)
+    bd, bf, bpt = oracle.brute_alongnormal(v, f, p, n)
+    assert (td == bd).all()
+    same = tf == bf
+    assert same.mean() > 0.99
+    assert np.array_equal(tpt[same], bpt[same], equal_nan=True)
+    assert td[-1] == 1e100 and tf[-1] == 0xFFFFFFFF
+
+
+def test_cgal_tree_visibility_vs_brute(oracle, ref_tests):
+    # any-hit through the tree == exhaustive any-hit, bit for bit, with extra triangles and sensors
+    v, f = W.geodesic_icosphere(8)
+    v = v * (1.0 + 0.1 * np.sin(5 * v[:, :1]) * np.sin(4 * v[:, 1:2]))
+    cams = W.fibonacci_cameras(5, 3.0)
+    nrm = v / np.linalg.norm(v, axis=1)[:, None]
+    ev = np.array([[1.5, -0.3, -0.3], [1.5, 0.3, -0.3], [1.5, 0.0, 0.4]])
+    ef = np.array([[0, 1, 2]], np.uint32)
+    sens = np.tile([0.5, 0, 0, 0, 0.5, 0, 0, 0, 1.0], (cams.shape[0], 1))
+    for kw in ({}, dict(extra_v=ev, extra_f=ef), dict(sensors=sens, min_dist=0.01)):
+        tree = oracle.CgalVisibilityTree(v, f, kw.get("extra_v"), kw.get("extra_f"))
+        tv, tn = tree.visibility(cams, n=nrm, sensors=kw.get("sensors"), min_dist=kw.get("min_dist", 1e-3))
+        bv, bn = oracle.brute_visibility(v, f, cams, n=nrm, **kw)
+        assert (tv == bv).all() and (tn == bn).all()
+        assert 0.01 < tv.mean() < 0.9
+
+    t = ref_tests["test_visibility_box"]
+
+    def fn(v, f, cams, n=None, extra_v=None, extra_f=None, min_dist=1e-3):
+        return oracle.CgalVisibilityTree(v, f, extra_v, extra_f).visibility(cams, n=n, min_dist=min_dist)
+
+    check_visibility_box(fn, t)
