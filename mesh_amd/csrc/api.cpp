@@ -1079,7 +1079,7 @@ struct BlobHeader {
     double origin[3];
     uint32_t node_bytes, leaf_bytes;
 };
-static const uint64_t kBlobMagic = 0x4d53484c42564833ull;  // "MSHLBVH3"
+static const uint64_t kBlobMagic = 0x4d53484c42564834ull;  // "MSHLBVH4" (interleaved node frame)
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 

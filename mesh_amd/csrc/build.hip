@@ -348,15 +348,16 @@ __device__ inline void encode_node(BNode* node, const ObbFrame& fr, const float 
             u[6 * side + 3 + k] = uh;
         }
     }
-    uint32_t w[4];
+    uint32_t w[3];
 #pragma unroll
     for (int j = 0; j < 3; ++j) w[j] = u[4 * j] | (u[4 * j + 1] << 8) | (u[4 * j + 2] << 16) | (u[4 * j + 3] << 24);
-    // biased exponents (e + 127 in [1, 254]): the decoder shifts them into an fp32 exponent field
-    w[3] = (uint32_t)(ex[0] + 127) | ((uint32_t)(ex[1] + 127) << 8) | ((uint32_t)(ex[2] + 127) << 16);
-    *reinterpret_cast<float4*>(f) = make_float4(fr.n[0], fr.n[1], fr.n[2], fr.t[0]);
-    *reinterpret_cast<float2*>(f + 4) = make_float2(fr.t[1], fr.t[2]);
+    float h[16];
+    encode_frame(h, fr.n, fr.t);
+    encode_scales(h, ex);
+    *reinterpret_cast<float4*>(f) = make_float4(h[0], h[1], h[2], h[3]);
+    *reinterpret_cast<float2*>(f + 4) = make_float2(h[4], h[5]);
     *reinterpret_cast<float4*>(f + 8) = make_float4(base[0], base[1], base[2], __uint_as_float(w[0]));
-    *reinterpret_cast<float4*>(f + 12) = make_float4(__uint_as_float(w[1]), __uint_as_float(w[2]), __uint_as_float(w[3]), 0.0f);
+    *reinterpret_cast<float4*>(f + 12) = make_float4(__uint_as_float(w[1]), __uint_as_float(w[2]), h[14], h[15]);
 }
 
 constexpr int kObbLane = 32;  // nodes over at most this many leaves: one lane each; larger: one wave each

@@ -29,17 +29,17 @@ constexpr int kBlock = 256;          // 4 waves of 64 lanes
 constexpr int kStack = MSH_STACK;           // per-lane LDS stack entries; deeper entries spill to global memory
 constexpr double kSlack = 1.0 + 9.094947017729282e-13;  // 1 + 2^-40: fp64 rounding margin for culls
 
-// float index within a node:  0-2 n | 3-5 t | 6 child0 | 7 child1 | 8-10 base (n, t, b) |
+// float index within a node:  0-5 frame (n0 t0 n1 t1 n2 t2: the (n_k, t_k) pairs are 8-B aligned, so
+//   the node test reads them as packed-fp32 operands) | 6 child0 | 7 child1 | 8-10 base (n, t, b) |
 //   bytes 44-55: u[side][6] quantised extents (lo n t b, hi n t b) of child 0 then child 1 |
-//   bytes 56-58: biased scale exponents E[3] = e + 127 (scale = 2^e, the fp32 with exponent field E) |
-//   59-63 zero
+//   float 14: E0 << 23 | E2, float 15: E1 << 23 — biased scale exponents E = e + 127 (scale = 2^e, the
+//   fp32 with exponent field E: axis 1's scale is float 15 itself, axes 0 and 2 take one and / shift)
 struct alignas(16) BNode {
     float f[16];
 };
 static_assert(sizeof(BNode) == 64, "BNode must be 64 B");
 constexpr int kBase = 8;      // float index of base[3]
 constexpr int kQuant = 44;    // byte offset of u[2][6]
-constexpr int kExp = 56;      // byte offset of E[3]
 
 // 2^e as an fp32 (e in [-126, 127])
 __host__ __device__ inline float exp2_scale(int e) {
@@ -108,6 +108,15 @@ __host__ __device__ inline float f32_up(double x) {
     return (double)f < x ? nextafterf(f, INFINITY) : f;
 }
 
+// node writers shared by the build and the host property test: frame pairs (n_k, t_k) and scale words
+__host__ __device__ inline void encode_frame(float* f, const float* n, const float* t) {
+    f[0] = n[0]; f[1] = t[0]; f[2] = n[1]; f[3] = t[1]; f[4] = n[2]; f[5] = t[2];
+}
+__host__ __device__ inline void encode_scales(float* f, const int* e) {
+    f[14] = u2f(((uint32_t)(e[0] + 127) << 23) | (uint32_t)(e[2] + 127));
+    f[15] = u2f((uint32_t)(e[1] + 127) << 23);
+}
+
 struct NodeV {
     float4 q[4];
     __host__ __device__ float at(int i) const { return reinterpret_cast<const float*>(q)[i]; }
@@ -115,12 +124,14 @@ struct NodeV {
     __host__ __device__ int child(int s) const { return (int)word(6 + s); }
     // frame axes n, t and b = n x t
     __host__ __device__ void frame(float* n, float* t, float* b) const {
-        n[0] = at(0); n[1] = at(1); n[2] = at(2);
-        t[0] = at(3); t[1] = at(4); t[2] = at(5);
+        n[0] = at(0); n[1] = at(2); n[2] = at(4);
+        t[0] = at(1); t[1] = at(3); t[2] = at(5);
         frame_b(n, t, b);
     }
-    // scale 2^e of axis k: the biased exponent byte shifted into an fp32 exponent field
-    __host__ __device__ float scale(int k) const { return u2f(((word(14) >> (8 * k)) & 0xffu) << 23); }
+    // scale 2^e of axis k (encode_scales)
+    __host__ __device__ float scale(int k) const {
+        return k == 0 ? u2f(word(14) & 0x7f800000u) : (k == 1 ? at(15) : u2f(word(14) << 23));
+    }
     // decoded oriented extents of both children: e0/e1 = lo n t b, hi n t b
     __host__ __device__ void extents(float* e0, float* e1) const {
         const uint32_t w0 = word(11), w1 = word(12), w2 = word(13);
@@ -248,20 +259,31 @@ __device__ inline double closest_on_triangle(const D3& o, const D3& t0, const D3
 // up); pe = the margin of the slab gaps in node_child_bounds: the fp32 projection error onto a unit
 // axis, pe0 = 2^-21 |q|_1 + 2e, plus 2^-21 |q|_1 + tm for the roundings of the fused gap expressions,
 // tm = 2^-21 * 1.25 * M (tree_margin), all rounded up.
+// Two-lane fp32 vectors: gfx950 issues their arithmetic as packed v_pk_fma/mul/add_f32.
+typedef float F2 __attribute__((ext_vector_type(2)));
+__host__ __device__ inline F2 f2(float a, float b) {
+    F2 r;
+    r.x = a;
+    r.y = b;
+    return r;
+}
+__host__ __device__ inline F2 f2(float a) { return f2(a, a); }
+__host__ __device__ inline F2 pfma(F2 a, F2 b, F2 c) { return __builtin_elementwise_fma(a, b, c); }
+// xy = (x, y), zp = (z, pe): pairs, so the node test broadcasts any one of them from its register pair
 struct QF {
-    float x, y, z, e, pe;
+    F2 xy, zp;
+    float e;
 };
 __host__ __device__ inline double tree_margin(double half_diagonal) { return 5.9604644775390625e-7 * half_diagonal; }
 __host__ __device__ inline QF make_qf(const D3& q, const double* origin, double tm) {
     const double rx = q.x - origin[0], ry = q.y - origin[1], rz = q.z - origin[2];
+    const float x = (float)rx, y = (float)ry, z = (float)rz;
+    const double e = fmax(fmax(fabs(rx - (double)x), fabs(ry - (double)y)), fabs(rz - (double)z));
+    const double l1 = fabs((double)x) + fabs((double)y) + fabs((double)z);
     QF r;
-    r.x = (float)rx;
-    r.y = (float)ry;
-    r.z = (float)rz;
-    const double e = fmax(fmax(fabs(rx - (double)r.x), fabs(ry - (double)r.y)), fabs(rz - (double)r.z));
+    r.xy = f2(x, y);
+    r.zp = f2(z, f32_up(9.5367431640625e-7 * l1 + 2.0 * e + tm));  // pe: 2^-20 |q|_1 + 2e + tm
     r.e = f32_up(e);
-    const double l1 = fabs((double)r.x) + fabs((double)r.y) + fabs((double)r.z);
-    r.pe = f32_up(9.5367431640625e-7 * l1 + 2.0 * e + tm);  // 2^-20 |q|_1
     return r;
 }
 
@@ -275,32 +297,41 @@ __host__ __device__ inline QF make_qf(const D3& q, const double* origin, double 
 // bound itself, so each computed gap g satisfies g <= (1 + 2^-24) * (true slab gap).  The sum of
 // squares (two fmas) is scaled by 1 - 2^-18, which covers those roundings and the division by
 // lambda_max(A A^T) <= 1 + 1e-6 of the nearly orthonormal fp32 axes.
+// Written with two-lane fp32 vectors so gfx950 issues packed v_pk_fma/mul/add_f32 (two fp32 operations per
+// lane per instruction); every lane computes exactly the scalar expression it replaces:
+//   b = n x t: frame_b's products, as (n1 t2, t1 n2), (n2 t0, t2 n0), (n0 t1, t0 n1), then one subtraction;
+//   p_n = fma(n0, qx, fma(n1, qy, n2 qz)), p_t, p_b likewise;
+//   per axis r = (p + pe - base, (p - pe) - base) = (-(base - (p + pe)), hi side);
+//   per child and axis fma(-u_lo, 2^e, r.x) = -fma(u_lo, 2^e, base - (p + pe)) exactly (round-to-nearest
+//   is symmetric), so the slab gap is max3(-t.x, t.y, 0) with t = fma((-u_lo, -u_hi), 2^e, r).
 __host__ __device__ inline void node_child_bounds(const NodeV& nd, const QF& q, float& d0, float& d1) {
-    float n[3], t[3], b[3];
-    nd.frame(n, t, b);
-    const float p[3] = {fmaf(n[0], q.x, fmaf(n[1], q.y, n[2] * q.z)), fmaf(t[0], q.x, fmaf(t[1], q.y, t[2] * q.z)),
-                        fmaf(b[0], q.x, fmaf(b[1], q.y, b[2] * q.z))};
-    float lo[3], hi[3], sc[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float base = nd.at(kBase + k);
-        lo[k] = base - (p[k] + q.pe);  // gap below the box: u_lo 2^e + lo
-        hi[k] = (p[k] - q.pe) - base;  // gap above the box: hi - u_hi 2^e
-        sc[k] = nd.scale(k);
-    }
-    const uint32_t w0 = nd.word(11), w1 = nd.word(12), w2 = nd.word(13);
+    const F2 P0 = f2(nd.q[0].x, nd.q[0].y), P1 = f2(nd.q[0].z, nd.q[0].w), P2 = f2(nd.q[1].x, nd.q[1].y);
+    const F2 m0 = P1 * P2.yx, m1 = P2 * P0.yx, m2 = P0 * P1.yx;
+    const float b0 = m0.x - m0.y, b1 = m1.x - m1.y, b2 = m2.x - m2.y;
+    // the projections stay scalar: packed, the compiler keeps splatted query pairs live across the loop and
+    // pass 1 spills twice as many registers (C3: -7 %)
+    const F2 pnt = f2(fmaf(P0.x, q.xy.x, fmaf(P1.x, q.xy.y, P2.x * q.zp.x)),
+                      fmaf(P0.y, q.xy.x, fmaf(P1.y, q.xy.y, P2.y * q.zp.x)));
+    const float pb = fmaf(b0, q.xy.x, fmaf(b1, q.xy.y, b2 * q.zp.x));
+    const F2 pe = f2(q.zp.y, -q.zp.y);
+    const F2 r[3] = {(f2(pnt.x) + pe) - f2(nd.q[2].x), (f2(pnt.y) + pe) - f2(nd.q[2].y), (f2(pb) + pe) - f2(nd.q[2].z)};
+    const uint32_t w0 = nd.word(11), w1 = nd.word(12), w2 = nd.word(13), we = nd.word(14);
+    const float sc[3] = {u2f(we & 0x7f800000u), nd.q[3].w, u2f(we << 23)};
+    // codes u[6 c + k] (lo) and u[6 c + 3 + k] (hi) of child c, axis k
     const uint32_t u[12] = {w0 & 0xffu, (w0 >> 8) & 0xffu, (w0 >> 16) & 0xffu, w0 >> 24,
                             w1 & 0xffu, (w1 >> 8) & 0xffu, (w1 >> 16) & 0xffu, w1 >> 24,
                             w2 & 0xffu, (w2 >> 8) & 0xffu, (w2 >> 16) & 0xffu, w2 >> 24};
-    float g[2][3];
+    F2 g[3];  // (child 0, child 1) gap per axis
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-        for (int k = 0; k < 3; ++k)
-            g[c][k] = fmaxf(fmaxf(fmaf((float)u[6 * c + k], sc[k], lo[k]), fmaf(-(float)u[6 * c + 3 + k], sc[k], hi[k])), 0.f);
+    for (int k = 0; k < 3; ++k) {
+        const F2 t0 = pfma(-f2((float)u[k], (float)u[3 + k]), f2(sc[k]), r[k]);
+        const F2 t1 = pfma(-f2((float)u[6 + k], (float)u[9 + k]), f2(sc[k]), r[k]);
+        g[k] = f2(fmaxf(fmaxf(-t0.x, t0.y), 0.f), fmaxf(fmaxf(-t1.x, t1.y), 0.f));
+    }
     const float c18 = 0.999996185302734375f;  // 1 - 2^-18
-    d0 = fmaf(g[0][0], g[0][0], fmaf(g[0][1], g[0][1], g[0][2] * g[0][2])) * c18;
-    d1 = fmaf(g[1][0], g[1][0], fmaf(g[1][1], g[1][1], g[1][2] * g[1][2])) * c18;
+    const F2 d = pfma(g[0], g[0], pfma(g[1], g[1], g[2] * g[2])) * f2(c18);
+    d0 = d.x;
+    d1 = d.y;
 }
 
 // fp64 oriented-box tools for the ray and triangle kernels (fp32 frame and extents widen exactly to fp64).

@@ -37,7 +37,10 @@ def check_mesh(v, f):
     child = fl[:, 6:8].copy().view(np.int32)
     base = fl[:, 8:11]
     u = nodes[:, 44:56].reshape(T - 1, 2, 6).astype(np.float32)
-    ex = nodes[:, 56:59].astype(np.int32) - 127  # biased exponent bytes
+    # biased exponents (common.h encode_scales): float 14 = E0 << 23 | E2, float 15 = E1 << 23
+    w14 = nodes[:, 56:60].copy().view(np.uint32)[:, 0].astype(np.int64)
+    w15 = nodes[:, 60:64].copy().view(np.uint32)[:, 0].astype(np.int64)
+    ex = np.stack([(w14 >> 23) & 0xff, (w15 >> 23) & 0xff, w14 & 0xff], axis=1).astype(np.int32) - 127
     scale = np.ldexp(np.float32(1.0), ex).astype(np.float32)  # (T-1, 3)
     # base + u * 2^e in fp32: the product is exact, the sum rounds once (as fmaf in the kernels)
     dec = (np.tile(base, 2)[:, None, :] + u * np.tile(scale, 2)[:, None, :]).astype(np.float32)  # (T-1, 2, 6)
@@ -62,10 +65,11 @@ def check_mesh(v, f):
     obb_bad = 0
     loose = []
     for x in range(T - 1):
-        nf, tf = fl[x, 0:3].astype(np.float64), fl[x, 3:6].astype(np.float64)
-        b = np.array([fl[x, 1] * fl[x, 5] - fl[x, 2] * fl[x, 4],
-                      fl[x, 2] * fl[x, 3] - fl[x, 0] * fl[x, 5],
-                      fl[x, 0] * fl[x, 4] - fl[x, 1] * fl[x, 3]], dtype=np.float32).astype(np.float64)
+        n32, t32 = fl[x, 0:6:2], fl[x, 1:6:2]  # frame pairs (n_k, t_k), common.h encode_frame
+        nf, tf = n32.astype(np.float64), t32.astype(np.float64)
+        b = np.array([n32[1] * t32[2] - n32[2] * t32[1],
+                      n32[2] * t32[0] - n32[0] * t32[2],
+                      n32[0] * t32[1] - n32[1] * t32[0]], dtype=np.float32).astype(np.float64)
         A = np.stack([nf, tf, b])
         prs = []
         for s in (0, 1):

@@ -111,11 +111,11 @@ int main(int argc, char** argv) {
         BNode bn;
         std::memset(&bn, 0, sizeof(bn));
         float* f = bn.f;
-        f[0] = nf[0]; f[1] = nf[1]; f[2] = nf[2]; f[3] = tf[0]; f[4] = tf[1]; f[5] = tf[2];
+        encode_frame(f, nf, tf);
         f[6] = u2f(~0u);
         f[7] = u2f(~1u);
         uint32_t u[12];
-        uint32_t ex = 0;
+        int ex[3];
         for (int k = 0; k < 3; ++k) {
             float base = (float)std::fmin(mn[0][k], mn[1][k]);
             if ((double)base > std::fmin(mn[0][k], mn[1][k])) base = nextafterf(base, -INFINITY);
@@ -124,14 +124,14 @@ int main(int argc, char** argv) {
             while (e < 127 && 254.0 * (double)exp2_scale(e) < range) ++e;
             const float sc = exp2_scale(e);
             f[kBase + k] = base;
-            ex |= (uint32_t)(e + 127) << (8 * k);
+            ex[k] = e;
             for (int ch = 0; ch < 2; ++ch) {
                 u[6 * ch + k] = code_lo(mn[ch][k], base, sc);
                 u[6 * ch + 3 + k] = code_hi(mx[ch][k], base, sc);
             }
         }
         for (int j = 0; j < 3; ++j) f[11 + j] = u2f(u[4 * j] | (u[4 * j + 1] << 8) | (u[4 * j + 2] << 16) | (u[4 * j + 3] << 24));
-        f[14] = u2f(ex);
+        encode_scales(f, ex);
         NodeV nd;
         std::memcpy(&nd, &bn, sizeof(bn));
         // the decoded boxes must contain the points (what the build guarantees); skip codes that cannot
@@ -195,7 +195,7 @@ int main(int argc, char** argv) {
             QF qf = make_qf(q, origin, tm);
 #endif
 #if defined(MUTATE_QUERY_MARGIN)  // ... and without any margin
-            qf.pe = 0.f;
+            qf.zp.y = 0.f;
 #endif
             float d2[2];
             node_child_bounds(nd, qf, d2[0], d2[1]);
