@@ -740,22 +740,32 @@ int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* n
     *leaves = 0;
     if (S == 0) return MSH_OK;
     hipStream_t s = t->stream;
-    unsigned long long h[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long h[40] = {0};
     {
         WsOrder order(t, s);
         QueryOrder ord;
         MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord, true));
-        MSH_TRY(t->ws.stats.reserve(8 * sizeof(unsigned long long)));
-        MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, 8 * sizeof(unsigned long long), s));
+        MSH_TRY(t->ws.stats.reserve(sizeof(h)));
+        MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, sizeof(h), s));
         MSH_TRY(launch_nearest_stats(t, ord, S, t->ws.stats.as<unsigned long long>(), s));
         MSH_HIP(hipMemcpyAsync(h, t->ws.stats.ptr, sizeof(h), hipMemcpyDeviceToHost, s));
     }
     MSH_HIP(hipStreamSynchronize(s));
     *nodes = h[0];
     *leaves = h[1];
-    if (getenv("MESH_AMD_STATS_DUMP"))  // development: wave-iteration utilisation of pass 1
+    if (getenv("MESH_AMD_STATS_DUMP")) {  // development: wave-iteration utilisation of pass 1
         fprintf(stderr, "[msh stats] S=%zu nodes=%llu leaves=%llu trav_it=%llu trav_lanes=%llu leaf_it=%llu "
                         "leaf_lanes=%llu pass2_items=%llu\n", S, h[0], h[1], h[2], h[3], h[4], h[5], h[6]);
+        // per phase: tiles, sum of per-tile max node steps, sum of lane steps, sum of min(tile max, 128 / 256 /
+        // 512), lanes over 128 / 256 / 512 steps
+        const char* nm[3] = {"super", "lead", "follow"};
+        for (int p = 0; p < 3; ++p) {
+            const unsigned long long* x = h + 8 + 9 * p;
+            fprintf(stderr, "[msh tiles] %s tiles=%llu sum_max=%llu sum_steps=%llu cap128=%llu cap256=%llu "
+                            "cap512=%llu over128=%llu over256=%llu over512=%llu\n", nm[p], x[0], x[1], x[2], x[3],
+                    x[4], x[5], x[6], x[7], x[8]);
+        }
+    }
     return MSH_OK;
 }
 

@@ -559,6 +559,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 nq = 0;
             };
             size_t steps = 0;
+            unsigned tot = 0;  // STATS: node steps of this lane, restarts included
             // Wave-synchronous loop.  Lanes that reach leaves queue them; a lane keeps traversing while
             // its queue has room for a node's two children.  Leaf tests run when the blocked lanes are
             // at least 1/kLeafK of the traversing ones (or nobody can traverse), so the expensive fp64
@@ -601,6 +602,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     enqueue(l0);
                     enqueue(l1);
                     ++steps;
+                    if (STATS) ++tot;
                     if (active && steps >= a.T) active = false;  // each node is entered once: corrupt tree
                     if (active && steps == a.budget) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
@@ -625,6 +627,25 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         // deferred list full: finish here without a budget
                     }
                 }
+            }
+            if (STATS) {  // per-tile step profile of this phase (stats[8 + 9 * phase slot ...])
+                unsigned mx = tot, sm = tot;
+                for (int o = 32; o > 0; o >>= 1) {
+                    mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+                    sm += (unsigned)__shfl_xor((int)sm, o);
+                }
+                unsigned long long* h = a.stats + 8 + 9 * (a.phase == 3 ? 0 : (a.phase == 1 ? 1 : 2));
+                if (lane == 0) {
+                    atomicAdd(h + 0, 1ull);
+                    atomicAdd(h + 1, (unsigned long long)mx);
+                    atomicAdd(h + 2, (unsigned long long)sm);
+                    atomicAdd(h + 3, (unsigned long long)min(mx, 128u));
+                    atomicAdd(h + 4, (unsigned long long)min(mx, 256u));
+                    atomicAdd(h + 5, (unsigned long long)min(mx, 512u));
+                }
+                if (tot > 128) atomicAdd(h + 6, 1ull);
+                if (tot > 256) atomicAdd(h + 7, 1ull);
+                if (tot > 512) atomicAdd(h + 8, 1ull);
             }
             if (deferred) continue;
         }
