@@ -143,13 +143,9 @@ struct TriPol {
         D3 a, b, c;
         uint32_t face;
         load_tri(tris, leaf, a, b, c, face);
-#ifdef MSH_EXP_CHEAPLEAF
-        const double d2 = fmin(fmin(sqdist(q, a), sqdist(q, b)), sqdist(q, c));  // timing experiment only
-#else
         D3 o;
         int part;
         const double d2 = closest_on_triangle(q, a, b, c, o, part);
-#endif
         if (d2 < best || (d2 == best && face < best_face)) {
             best = d2;
             best_face = face;
@@ -423,9 +419,6 @@ constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= t
 constexpr int kLeafQ = MSH_LEAF_Q;  // leaves a lane may hold before it stops traversing (2..4)
 static_assert(kLeafQ >= 2 && kLeafQ <= 4, "kLeafQ must be 2, 3 or 4");
 
-#ifndef MSH_TEST_LOOP
-#define MSH_TEST_LOOP 1
-#endif
 #ifndef MSH_LEAD2
 #define MSH_LEAD2 256
 #endif
@@ -461,13 +454,8 @@ __device__ inline double hint_from_leaders(const KnnArgs& a, size_t i, const D3&
     const size_t base = (i / window) * window;
     const size_t mesh = a.orgs ? i / a.qper : 0;
     double h = INFINITY;
-#ifdef MSH_EXP_SELFHINT
-    for (size_t L = 0; L < window + 1; L += stride) {  // experiment: the slot's own stale result last
-        const size_t li = L < window ? base + L : i;
-#else
     for (size_t L = 0; L < window; L += stride) {
         const size_t li = base + L;
-#endif
         if (li >= a.S) break;
         if (a.orgs && li / a.qper != mesh) continue;
         const uint4 r0 = reinterpret_cast<const uint4*>(a.res + li)[0];
@@ -543,7 +531,6 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 ++nq;
             };
             auto test_queue = [&]() {
-#if MSH_TEST_LOOP
                 // one copy of the fp64 construction in the code (a loop over the queue), not one per entry
 #pragma nounroll
                 for (int k = 0; k < nq; ++k) {
@@ -551,11 +538,6 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     q0 = q1;
                     q1 = q2;
                 }
-#else
-                if (nq > 0) pol.test(q0);
-                if (nq > 1) pol.test(q1);
-                if (kLeafQ > 2 && nq > 2) pol.test(q2);
-#endif
                 nq = 0;
             };
             size_t steps = 0;

@@ -1,11 +1,12 @@
-"""Secondary measurements for BASELINE.md configs C1, C2, C4, C5 (bench.py measures C3, the headline).
+"""Secondary measurements for BASELINE.md configs C1, C2, C4, C5, and C3 through the numpy API (bench.py
+measures C3 device-resident, the headline).
 
 One JSON line per config on stdout: the GPU path through the numpy API (the reference's entry points:
 host arrays in, host arrays out), the device-resident rate (inputs already in HBM) where it differs, the
 kernel time from the library's HIP-event timers, and the oracle's CGAL-faithful CPU restatement on a
 sample (1 thread and all host threads).  Inputs are the seeded synthetic workloads of workloads.py.
 
-    python scripts/bench_configs.py [--configs c1,c2,c4,c5] [--reps 3]
+    python scripts/bench_configs.py [--configs c1,c2,c3np,c4,c5] [--reps 3]
 """
 import argparse
 import json
@@ -127,6 +128,20 @@ def c2(reps):
             "queries_per_s_numpy_api": S / wall, "ms_numpy_api": wall * 1e3,
             "build_ms_gpu": tree.info().build_ms, "build_ms_wall": build_wall * 1e3,
             "cpu_ref_1t_qps": c1t, "cpu_ref_omp_qps": cmt, "cpu_threads": th}
+
+
+def c3np(reps):
+    """C3 through the reference's entry point (the secondary metric of SURVEY §8(d)): 100M host queries in,
+    host arrays out — H2D + sort + traversal + D2H, pipelined through pinned slabs by the library."""
+    from mesh_amd import spatialsearch
+    import workloads as W
+    v, f = W.c3_mesh()
+    q = np.random.default_rng(3).uniform(-1.1, 1.1, (100_000_000, 3))
+    tree = spatialsearch.aabbtree_compute(v, f)
+    _, wall = timed(lambda: spatialsearch.aabbtree_nearest(tree, q), reps)
+    return {"config": "C3 icosphere (1,003,520 faces), 100M uniform host queries, aabbtree_nearest (numpy API)",
+            "queries_per_s_numpy_api": q.shape[0] / wall, "ms_numpy_api": wall * 1e3,
+            "ms_traversal_kernel": kernel_ms("nearest"), "pcie_bytes_per_query": 56}
 
 
 def c4(reps):
@@ -268,12 +283,12 @@ def c5_cpu(v, f, p, n, cams, vn):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--configs", default="c1,c2,c4,c5")
+    ap.add_argument("--configs", default="c1,c2,c3np,c4,c5")
     ap.add_argument("--reps", type=int, default=3)
     args = ap.parse_args()
     from mesh_amd import _native
     _native.set_device(0)
-    fns = {"c1": c1, "c2": c2, "c4": c4, "c5": c5}
+    fns = {"c1": c1, "c2": c2, "c3np": c3np, "c4": c4, "c5": c5}
     for name in args.configs.split(","):
         r = fns[name](args.reps)
         r["name"] = name
