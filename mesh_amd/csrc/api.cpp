@@ -740,7 +740,7 @@ int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* n
     *leaves = 0;
     if (S == 0) return MSH_OK;
     hipStream_t s = t->stream;
-    unsigned long long h[40] = {0};
+    unsigned long long h[48] = {0};
     {
         WsOrder order(t, s);
         QueryOrder ord;
@@ -765,6 +765,8 @@ int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* n
                             "cap512=%llu over128=%llu over256=%llu over512=%llu\n", nm[p], x[0], x[1], x[2], x[3],
                     x[4], x[5], x[6], x[7], x[8]);
         }
+        fprintf(stderr, "[msh pass2] waves=%llu items=%llu visits_sum=%llu visits_max_item=%llu\n", h[6], h[46], h[44],
+                h[45]);
     }
     return MSH_OK;
 }

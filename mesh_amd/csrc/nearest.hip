@@ -666,7 +666,10 @@ __device__ inline double wave_min(double x) {
     return x;
 }
 
-constexpr int kFront = 512;  // frontier entries per wave in pass 2
+#ifndef MSH_FRONT
+#define MSH_FRONT 512
+#endif
+constexpr int kFront = MSH_FRONT;  // frontier entries per wave in pass 2
 
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
@@ -678,7 +681,13 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
     const unsigned total = min(*a.n_deferred, a.max_deferred);
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     unsigned n_nodes = 0, n_leaves = 0;
-    for (unsigned item = blockIdx.x * 4 + wv; item < total; item += gridDim.x * 4) {
+    unsigned* next_item = a.n_deferred + 32;  // items are dealt dynamically: their costs vary widely
+    for (;;) {
+        unsigned item = 0;
+        if (lane == 0) item = atomicAdd(next_item, 1u);
+        item = __shfl(item, 0);
+        if (item >= total) break;
+        const unsigned item_nodes0 = n_nodes, item_leaves0 = n_leaves;
         const DeferRec r = a.deferred[item];
         const size_t i = r.slot;
         const D3 q = load_q(a, i);
@@ -751,6 +760,15 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
             pol.best_face = face;
             pol.best_leaf = leaf;
             write_result<MODE>(a, i, q, pol);
+        }
+        if (STATS) {  // per-item work: stats[44] sum and stats[45] max of node + leaf visits over the wave
+            unsigned w = (n_nodes - item_nodes0) + (n_leaves - item_leaves0);
+            for (int o = 32; o > 0; o >>= 1) w += (unsigned)__shfl_xor((int)w, o);
+            if (lane == 0) {
+                atomicAdd(&a.stats[44], (unsigned long long)w);
+                atomicMax(&a.stats[45], (unsigned long long)w);
+                atomicAdd(&a.stats[46], 1ull);
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }
@@ -884,18 +902,21 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     for (int k = 0; k < 3; ++k) a.org[k] = tree->origin[k];
     const unsigned ncu = (unsigned)device_cus(tree->device);
     Workspace& ws = tree->ws;
-    // counters: 8 group counters (one 128-B line each) + the deferred count
-    MSH_TRY(ws.counters.reserve(9 * 32 * sizeof(unsigned)));
+    // counters: 8 group counters (one 128-B line each) + the deferred count + pass 2's item counter
+    MSH_TRY(ws.counters.reserve(10 * 32 * sizeof(unsigned)));
     a.counters = ws.counters.as<unsigned>();
     a.n_deferred = a.counters + 8 * 32;
-    MSH_HIP(hipMemsetAsync(a.counters, 0, 9 * 32 * sizeof(unsigned), s));
+    MSH_HIP(hipMemsetAsync(a.counters, 0, 10 * 32 * sizeof(unsigned), s));  // + the pass-2 item counter
     // leader ordering: closest-point launches over a Morton-sorted slot order (records in a.res)
     const bool lead = kLead > 1 && (MODE == 0 || MODE == 3) && a.res != nullptr && a.S >= 64 * (size_t)kLead;
     const size_t n_lead = (a.S + kLead - 1) / kLead;
     const unsigned max_tiles = (unsigned)((a.S + 63) / 64);
     const unsigned nblk_max = std::min<unsigned>((max_tiles + 3) / 4, ncu * kKnnBlocksPerCU);
     // pass 2 lanes carry up to kFront/64 dealt subtrees on top of a depth-first path
-    const unsigned nblk2 = ncu * 2u;
+#ifndef MSH_P2_BLOCKS
+#define MSH_P2_BLOCKS 2
+#endif
+    const unsigned nblk2 = ncu * (unsigned)MSH_P2_BLOCKS;
     const int need = tree->max_depth + 1 + kFront / 64 + 1;
     a.spill = nullptr;
     a.spill_depth = 0;
