@@ -260,6 +260,13 @@ static const size_t kSortMin = 4096;  // below this the query Morton sort costs 
 #ifndef MSH_SLOT_GATHER
 #define MSH_SLOT_GATHER 0
 #endif
+// Queries are ordered by the top 24 bits of their 30-bit Morton code (256 cells per axis, 3 radix passes):
+// C3's 100M queries put ~6 in a cell, and the traversal runs the same node counts as with the full code
+// (sort 3.44 -> 3.08 ms, traversal unchanged).  The order within a cell is the caller's (stable sort).
+#ifndef MSH_QSORT_LO
+#define MSH_QSORT_LO 6
+#endif
+constexpr int kQuerySortLo = MSH_QSORT_LO;
 static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_t S, hipStream_t s,
                         QueryOrder* ord, bool allow_lazy = false) {
     *ord = QueryOrder{d_q, d_n, nullptr, nullptr};
@@ -271,8 +278,13 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
     MSH_TRY(ws.vals_alt.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.inv.reserve(S * sizeof(uint32_t)));
     MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
+    bool in_alt = false;
     MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
-                             ws.vals_alt.as<uint32_t>(), S, 30, ws, s));
+                             ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
+    if (in_alt) {  // odd pass count: the sorted pairs are in the alt buffers; swap roles instead of copying
+        std::swap(ws.keys, ws.keys_alt);
+        std::swap(ws.vals, ws.vals_alt);
+    }
     if (allow_lazy && !MSH_SLOT_GATHER && !d_n) {
         *ord = QueryOrder{d_q, nullptr, ws.vals.as<uint32_t>(), ws.inv.as<uint32_t>(), false};
         return MSH_OK;

@@ -121,9 +121,10 @@ struct msh_tree {
 namespace msh {
 
 // ---- radix sort (sort.hip): stable LSD sort of (u32 key, u32 value) pairs on the low `bits` bits.
-// Result ends in keys/vals (the alt buffers are temporaries).
+// Result ends in keys/vals (the alt buffers are temporaries) — or, with in_alt and an odd number of
+// passes, in keys_alt/vals_alt (*in_alt = true) without the copy back.  lo_bit: first key bit sorted.
 int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, size_t n, int bits,
-                     Workspace& ws, hipStream_t s);
+                     Workspace& ws, hipStream_t s, int lo_bit = 0, bool* in_alt = nullptr);
 // exclusive scan of u32 (in place), n elements
 int exclusive_scan_u32(uint32_t* data, size_t n, Workspace& ws, hipStream_t s);
 

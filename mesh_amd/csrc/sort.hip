@@ -193,7 +193,7 @@ int exclusive_scan_u32(uint32_t* data, size_t n, Workspace& ws, hipStream_t s) {
 }
 
 int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, size_t n, int bits,
-                     Workspace& ws, hipStream_t s) {
+                     Workspace& ws, hipStream_t s, int lo_bit, bool* in_alt) {
     if (n <= 1) return MSH_OK;
     if (n > 0xFFFFFFFFull) {
         set_error("radix sort: %zu elements exceed the 32-bit offset range", n);
@@ -205,7 +205,7 @@ int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_
     uint32_t* hist = ws.hist.as<uint32_t>();
     uint32_t *src_k = keys, *src_v = vals, *dst_k = keys_alt, *dst_v = vals_alt;
     int passes = 0;
-    for (int shift = 0; shift < bits; shift += 8, ++passes) {
+    for (int shift = lo_bit; shift < lo_bit + bits; shift += 8, ++passes) {
         k_hist<<<nb, kBlock, 0, s>>>(src_k, n, shift, hist, nb);
         MSH_HIP(hipGetLastError());
         MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
@@ -215,7 +215,8 @@ int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_
         t = src_k; src_k = dst_k; dst_k = t;
         t = src_v; src_v = dst_v; dst_v = t;
     }
-    if (passes & 1) {
+    if (in_alt) *in_alt = (passes & 1) != 0;
+    if ((passes & 1) && !in_alt) {
         MSH_HIP(hipMemcpyAsync(keys, src_k, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
         MSH_HIP(hipMemcpyAsync(vals, src_v, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     }
