@@ -184,6 +184,7 @@ def main():
     k_ms, k_n = _native.timing_get("nearest")
     p1_ms, p1_n = _native.timing_get("knn_pass1")
     p2_ms, p2_n = _native.timing_get("knn_pass2")
+    sl_ms, sl_n = _native.timing_get("knn_lead2")
     ld_ms, ld_n = _native.timing_get("knn_lead")
     fl_ms, fl_n = _native.timing_get("knn_follow")
     s_ms, s_n = _native.timing_get("sort")
@@ -262,6 +263,7 @@ def main():
                      "measured": ({"hbm_GBps": tr["bytes_per_launch"] / avg_kernel_s / 1e9,
                                    "l2_hit_rate": tr.get("l2_hit_rate"), "code": tr.get("code")} if tr else None)},
         "breakdown_ms_per_step": {"traversal": k_ms / max(k_n, 1), "pass1": p1_ms / max(p1_n, 1),
+                                  "pass1_superleaders": sl_ms / max(sl_n, 1),
                                   "pass1_leaders": ld_ms / max(ld_n, 1), "pass1_followers": fl_ms / max(fl_n, 1),
                                   "pass2": p2_ms / max(p2_n, 1), "sort": s_ms / max(s_n, 1),
                                   "morton": m_ms / max(m_n, 1), "gather": g_ms / max(g_n, 1),

@@ -591,9 +591,23 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         if (slot < a.max_deferred) {
                             if (STATS) n_leaves += nq;
                             test_queue();
-                            if (a.phase == 1 || a.phase == 3) {  // nobody may take a hint from it yet
-                                D3 nq3 = D3{NAN, NAN, NAN};
-                                if (a.res) store_qres(a.res + i, MSH_NO_FACE, 0u, nq3.x, nq3.y, nq3.z);
+                            if ((a.phase == 1 || a.phase == 3) && a.res) {
+                                // later phases take hints from this slot before pass 2 answers it: publish the
+                                // closest point of the best face so far (a point on the mesh, so a valid upper
+                                // bound for its neighbours), or NO_FACE when it has none yet
+                                if constexpr (MODE == 0 || MODE == 3) {
+                                    D3 o = D3{NAN, NAN, NAN};
+                                    uint32_t f = MSH_NO_FACE;
+                                    if (pol.best_leaf >= 0) {
+                                        D3 ta, tb, tc;
+                                        int part;
+                                        load_tri(static_cast<const TriRec*>(a.leaves), pol.best_leaf, ta, tb, tc, f);
+                                        closest_on_triangle(q, ta, tb, tc, o, part);
+                                    }
+                                    store_qres(a.res + i, f, 0u, o.x, o.y, o.z);
+                                } else {
+                                    store_qres(a.res + i, MSH_NO_FACE, 0u, NAN, NAN, NAN);
+                                }
                             }
                             DeferRec r;
                             r.slot = (uint32_t)i;
@@ -889,6 +903,13 @@ static int device_cus(int dev) {
 #define MSH_BUDGET 1024
 #endif
 constexpr unsigned kBudget = MSH_BUDGET;  // pass-1 node steps per lane before a query is deferred
+#ifndef MSH_BUDGET3
+#define MSH_BUDGET3 256
+#endif
+// super-leaders: their launch has few tiles (C3: 6104 for 8192 wave slots), so its slowest tile sets its
+// length; with 256 steps the launch takes 1.4 instead of 2.9 ms and pass 2 gets ~18k more (cheap) items
+// (+0.4 ms).  A deferred super-leader publishes its best point so far as its leaders' hint.
+constexpr unsigned kBudget3 = MSH_BUDGET3;
 #ifndef MSH_KNN_BPC
 #define MSH_KNN_BPC 4
 #endif
@@ -932,6 +953,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     a.deferred = dbuf.as<DeferRec>();
     auto pass1 = [&](int phase, size_t nunits, const char* name) -> int {
         a.phase = phase;
+        a.budget = phase == 3 ? kBudget3 : kBudget;
         a.nunits = nunits;
         a.ntiles = (unsigned)((nunits + 63) / 64);
         const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, ncu * kKnnBlocksPerCU);
