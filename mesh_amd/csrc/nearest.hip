@@ -910,6 +910,10 @@ constexpr unsigned kBudget = MSH_BUDGET;  // pass-1 node steps per lane before a
 // length; with 256 steps the launch takes 1.4 instead of 2.9 ms and pass 2 gets ~18k more (cheap) items
 // (+0.4 ms).  A deferred super-leader publishes its best point so far as its leaders' hint.
 constexpr unsigned kBudget3 = MSH_BUDGET3;
+#ifndef MSH_BUDGET1
+#define MSH_BUDGET1 512
+#endif
+constexpr unsigned kBudget1 = MSH_BUDGET1;  // leaders (C3: 13.8 -> 12.6 ms, pass 2 +0.5 ms)
 #ifndef MSH_KNN_BPC
 #define MSH_KNN_BPC 4
 #endif
@@ -953,7 +957,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     a.deferred = dbuf.as<DeferRec>();
     auto pass1 = [&](int phase, size_t nunits, const char* name) -> int {
         a.phase = phase;
-        a.budget = phase == 3 ? kBudget3 : kBudget;
+        a.budget = phase == 3 ? kBudget3 : (phase == 1 ? kBudget1 : kBudget);
         a.nunits = nunits;
         a.ntiles = (unsigned)((nunits + 63) / 64);
         const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, ncu * kKnnBlocksPerCU);
