@@ -683,7 +683,7 @@ __device__ inline double wave_min(double x) {
 #ifndef MSH_FRONT
 #define MSH_FRONT 512
 #endif
-constexpr int kFront = MSH_FRONT;  // frontier entries per wave in pass 2
+constexpr int kFront = MSH_FRONT;  // pass 2: 2 kFront work-list entries per wave (LDS)
 
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
@@ -715,50 +715,54 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
             pol.best_leaf = r.leaf;
         }
         pol.relim();
-        // breadth-first expansion of the top of the tree into <= kFront subtrees
-        int cur = 0, n = 1;
-        if (lane == 0) front[wv][0][0] = make_uint2((unsigned)root, 0u);
+        // Subtree work list, last in first out, expanded 64 entries at a time (one per lane): children
+        // within the bound go back on the list (compacted by ballot), leaf children are tested on the spot.
+        // Taking the 64 newest entries keeps the walk deep-first, so good leaves (and the shared bound)
+        // come early.  Most items finish here at full wave width; a list that would outgrow LDS is dealt
+        // to the lanes' own stacks for depth-first walks.
+        uint2* W = &front[wv][0][0];  // kWork contiguous entries
+        constexpr int kWork = 2 * kFront;
+        int top = 1;
+        if (lane == 0) W[0] = make_uint2((unsigned)root, 0u);
         __builtin_amdgcn_wave_barrier();
-        while (n > 0 && n <= kFront / 2) {
-            int m = 0;
-            for (int base = 0; base < n; base += 64) {
-                const int j = base + lane;
-                bool k0 = false, k1 = false;
-                uint2 e0, e1;
-                if (j < n) {
-                    const uint2 e = front[wv][cur][j];
-                    if (__uint_as_float(e.y) <= pol.limf) {
-                        const NodeV nd = load_node(a.nodes, (int)e.x);
-                        ++n_nodes;
-                        float d0, d1;
-                        node_child_bounds(nd, qf, d0, d1);
-                        const int c0 = nd.child(0), c1 = nd.child(1);
-                        if (d0 <= pol.limf) {
-                            if (c0 < 0) { pol.test(~c0); ++n_leaves; }
-                            else { k0 = true; e0 = make_uint2((unsigned)c0, __float_as_uint(d0)); }
-                        }
-                        if (d1 <= pol.limf) {
-                            if (c1 < 0) { pol.test(~c1); ++n_leaves; }
-                            else { k1 = true; e1 = make_uint2((unsigned)c1, __float_as_uint(d1)); }
-                        }
+        while (top > 0 && top <= kWork - 128) {
+            const int nt = min(64, top);
+            const int base = top - nt;
+            bool k0 = false, k1 = false;
+            uint2 e0, e1;
+            if (lane < nt) {
+                const uint2 e = W[base + lane];
+                if (__uint_as_float(e.y) <= pol.limf) {
+                    const NodeV nd = load_node(a.nodes, (int)e.x);
+                    ++n_nodes;
+                    float d0, d1;
+                    node_child_bounds(nd, qf, d0, d1);
+                    const int c0 = nd.child(0), c1 = nd.child(1);
+                    if (d0 <= pol.limf) {
+                        if (c0 < 0) { pol.test(~c0); ++n_leaves; }
+                        else { k0 = true; e0 = make_uint2((unsigned)c0, __float_as_uint(d0)); }
+                    }
+                    if (d1 <= pol.limf) {
+                        if (c1 < 0) { pol.test(~c1); ++n_leaves; }
+                        else { k1 = true; e1 = make_uint2((unsigned)c1, __float_as_uint(d1)); }
                     }
                 }
-                const unsigned long long b0 = __ballot(k0), b1 = __ballot(k1);
-                const int p0 = m + __popcll(b0 & lt) + __popcll(b1 & lt);
-                if (k0) front[wv][cur ^ 1][p0] = e0;
-                if (k1) front[wv][cur ^ 1][p0 + (k0 ? 1 : 0)] = e1;
-                m += __popcll(b0) + __popcll(b1);
-                pol.shared = fmin(pol.shared, wave_min(pol.best));
-                pol.relim();
             }
             __builtin_amdgcn_wave_barrier();
-            cur ^= 1;
-            n = m;
+            const unsigned long long b0 = __ballot(k0), b1 = __ballot(k1);
+            const int p0 = base + __popcll(b0 & lt) + __popcll(b1 & lt);
+            if (k0) W[p0] = e0;
+            if (k1) W[p0 + (k0 ? 1 : 0)] = e1;
+            top = base + __popcll(b0) + __popcll(b1);
+            __builtin_amdgcn_wave_barrier();
+            pol.shared = fmin(pol.shared, wave_min(pol.best));
+            pol.relim();
         }
-        // deal the frontier to the lanes (entry j -> lane j % 64), then depth-first walks
+        // overflow: deal the list to the lanes (entry j -> lane j % 64), then depth-first walks
+        const int n = top;
         Walker w{0, 0};
         if (lane < n)
-            for (int j = lane + ((n - 1 - lane) / 64) * 64; j >= lane; j -= 64) w.push(front[wv][cur][j], lds, spill);
+            for (int j = lane + ((n - 1 - lane) / 64) * 64; j >= lane; j -= 64) w.push(W[j], lds, spill);
         bool active = w.pop(pol, lds, spill);
         while (__any(active)) {
             if (active) active = w.step<decltype(pol), false>(a.nodes, qf, pol, lds, spill, n_nodes, n_leaves);
@@ -937,12 +941,12 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     const size_t n_lead = (a.S + kLead - 1) / kLead;
     const unsigned max_tiles = (unsigned)((a.S + 63) / 64);
     const unsigned nblk_max = std::min<unsigned>((max_tiles + 3) / 4, ncu * kKnnBlocksPerCU);
-    // pass 2 lanes carry up to kFront/64 dealt subtrees on top of a depth-first path
+    // pass 2 lanes carry up to 2 kFront/64 dealt subtrees on top of a depth-first path
 #ifndef MSH_P2_BLOCKS
 #define MSH_P2_BLOCKS 2
 #endif
     const unsigned nblk2 = ncu * (unsigned)MSH_P2_BLOCKS;
-    const int need = tree->max_depth + 1 + kFront / 64 + 1;
+    const int need = tree->max_depth + 1 + 2 * kFront / 64 + 1;
     a.spill = nullptr;
     a.spill_depth = 0;
     if (need > kStack) {
