@@ -87,6 +87,9 @@ struct KnnArgs {
     // unhinted; phase 1 = leader slots (i % kLead == 0); phase 2 = the other slots, each starting from the
     // upper bound given by its 64-slot tile's leaders (see hint_from_leaders)
     int phase;
+    // direct: the sorted path writes each answer straight to the caller's row perm[i] (no k_unpermute);
+    // slot-order records are kept only for the leader phases, whose records are the followers' hints
+    bool direct;
     size_t nunits;  // work units of this phase (slots it covers)
     DeferRec* deferred;
     unsigned* n_deferred;
@@ -330,12 +333,15 @@ __device__ inline D3 heidrich_bary(const D3& p, const D3& a, const D3& b, const 
 // Outputs of slot i from its policy (winner's leaf -> point / part recomputed exactly).
 template <int MODE, class Pol>
 __device__ inline void write_result(const KnnArgs& a, size_t i, const D3& q, const Pol& pol) {
+    const bool rec = a.res && (!a.direct || a.phase == 1 || a.phase == 3);  // slot-order record
+    const bool out = !a.res || a.direct;                                      // caller's arrays
+    const size_t r = a.res ? (size_t)a.perm[i] : i;                           // caller's row
     if constexpr (MODE == 2) {
         const double dist = pol.best_leaf >= 0 ? sqrt(pol.best) : NAN;
-        if (a.res) store_qres(a.res + i, pol.best_face, 0u, dist, 0.0, 0.0);
-        else {
-            a.out_face[i] = pol.best_face;
-            a.out_dist[i] = dist;
+        if (rec) store_qres(a.res + i, pol.best_face, 0u, dist, 0.0, 0.0);
+        if (out) {
+            a.out_face[r] = pol.best_face;
+            a.out_dist[r] = dist;
         }
         return;
     }
@@ -348,24 +354,24 @@ __device__ inline void write_result(const KnnArgs& a, size_t i, const D3& q, con
         closest_on_triangle(q, ta, tb, tc, o, part);
         if (MODE == 3) w = heidrich_bary(o, ta, tb, tc);
     }
-    if (a.res) {
+    if (rec) {
         store_qres(a.res + i, face, (uint32_t)part, o.x, o.y, o.z);
-        if (MODE == 3) {
+        if (MODE == 3 && !a.direct) {
             a.res_w[3 * i] = w.x;
             a.res_w[3 * i + 1] = w.y;
             a.res_w[3 * i + 2] = w.z;
         }
-        return;
     }
-    a.out_face[i] = face;
-    if (MODE == 0 && a.out_part) a.out_part[i] = (uint32_t)part;
-    a.out_pt[3 * i] = o.x;
-    a.out_pt[3 * i + 1] = o.y;
-    a.out_pt[3 * i + 2] = o.z;
+    if (!out) return;
+    a.out_face[r] = face;
+    if (MODE == 0 && a.out_part) a.out_part[r] = (uint32_t)part;
+    a.out_pt[3 * r] = o.x;
+    a.out_pt[3 * r + 1] = o.y;
+    a.out_pt[3 * r + 2] = o.z;
     if (MODE == 3) {
-        a.out_w[3 * i] = w.x;
-        a.out_w[3 * i + 1] = w.y;
-        a.out_w[3 * i + 2] = w.z;
+        a.out_w[3 * r] = w.x;
+        a.out_w[3 * r + 1] = w.y;
+        a.out_w[3 * r + 2] = w.z;
     }
 }
 
@@ -497,7 +503,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         const size_t i = slot_of(a, k);
         if (i >= a.S) continue;
         const D3 q = load_q(a, i);
-        if (a.inv_w) a.inv_w[a.qperm[i]] = (uint32_t)i;
+        if (a.inv_w && !a.direct) a.inv_w[a.qperm[i]] = (uint32_t)i;
         auto pol = make_pol<MODE>(a, i, q);
         if (!finite3(q)) {  // no distance is defined: NO_FACE / NaN, no traversal
             if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
@@ -1000,6 +1006,11 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     return MSH_OK;
 }
 
+#ifndef MSH_DIRECT_OUT
+#define MSH_DIRECT_OUT 1
+#endif
+constexpr bool kDirectOut = MSH_DIRECT_OUT;
+
 // Slot-order plumbing shared by the point-query launchers: with a permutation the kernels write 32-B
 // records (plus nw weights) into the workspace and k_unpermute scatters them to the caller's arrays.
 template <int MODE, bool STATS>
@@ -1016,9 +1027,17 @@ static int run_knn(msh_tree* tree, KnnArgs a, const QueryOrder& ord, const SlotO
     if (ord.perm) {  // STATS launches keep the records too: followers take their hints from them
         MSH_TRY(ws.res.reserve(a.S * sizeof(QRes)));
         a.res = ws.res.as<QRes>();
-        if (nw) {
+        a.direct = kDirectOut && !STATS && (MODE == 0 || MODE == 3);
+        if (nw && !a.direct) {
             MSH_TRY(ws.res_w.reserve(a.S * (size_t)nw * sizeof(double)));
             a.res_w = ws.res_w.as<double>();
+        }
+        if (a.direct) {
+            a.out_face = o.face;
+            a.out_part = o.part;
+            a.out_pt = o.pt;
+            a.out_dist = o.dist;
+            a.out_w = o.w;
         }
     } else {
         a.out_face = o.face;
@@ -1028,7 +1047,7 @@ static int run_knn(msh_tree* tree, KnnArgs a, const QueryOrder& ord, const SlotO
         a.out_w = o.w;
     }
     MSH_TRY((launch_knn<MODE, STATS>(tree, a, s, timer)));
-    if (ord.perm && !STATS) MSH_TRY(unpermute_results(a.res, a.res_w, nw, ord.inv, a.S, o, s));
+    if (ord.perm && !STATS && !a.direct) MSH_TRY(unpermute_results(a.res, a.res_w, nw, ord.inv, a.S, o, s));
     return MSH_OK;
 }
 
