@@ -265,8 +265,7 @@ struct RayArgs {
     const double* p;
     const double* n;
     size_t S;
-    QRes* res;
-    double* res_w;
+    const uint32_t* perm;  // slot -> caller's row (sorted rays), nullptr: identity
     double* out_dist;
     uint32_t* out_face;
     double* out_pt;
@@ -333,16 +332,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MSH_RAY_
                 traverse_rays<AlongPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
             if (STATS) continue;
             const double dist = pol.best == INFINITY ? 1e100 : pol.best;
-            if (a.res) {
-                store_qres(a.res + i, pol.best_face, 0u, pol.best_pt.x, pol.best_pt.y, pol.best_pt.z);
-                a.res_w[i] = dist;
-            } else {
-                a.out_dist[i] = dist;
-                a.out_face[i] = pol.best_face;
-                a.out_pt[3 * i] = pol.best_pt.x;
-                a.out_pt[3 * i + 1] = pol.best_pt.y;
-                a.out_pt[3 * i + 2] = pol.best_pt.z;
-            }
+            const size_t r = a.perm ? (size_t)a.perm[i] : i;  // the caller's row (scattered store)
+            a.out_dist[r] = dist;
+            a.out_face[r] = pol.best_face;
+            a.out_pt[3 * r] = pol.best_pt.x;
+            a.out_pt[3 * r + 1] = pol.best_pt.y;
+            a.out_pt[3 * r + 2] = pol.best_pt.z;
         } else {
             const size_t ic = i / a.nv, k = i - ic * a.nv;
             const size_t iv = a.vorder ? (size_t)a.vorder[k] : a.v0 + k;  // vertex (global index)
@@ -420,23 +415,9 @@ int launch_alongnormal(const msh_tree* tree, const QueryOrder& ord, size_t S, co
     RayArgs a{};
     a.nodes = tree->d_nodes; a.tris = static_cast<const TriRec*>(tree->d_leaves); a.T = tree->T;
     a.p = ord.q; a.n = ord.n;
-    if (ord.perm) {
-        MSH_TRY(t->ws.res.reserve(S * sizeof(QRes)));
-        MSH_TRY(t->ws.res_w.reserve(S * sizeof(double)));
-        a.res = t->ws.res.as<QRes>();
-        a.res_w = t->ws.res_w.as<double>();
-    } else {
-        a.out_dist = o.w; a.out_face = o.face; a.out_pt = o.pt;
-    }
-    MSH_TRY((launch_rays<0, false>(t, a, S, s, "alongnormal")));
-    if (ord.perm) {
-        SlotOut oo{};
-        oo.face = o.face;
-        oo.pt = o.pt;
-        oo.w = o.w;
-        MSH_TRY(unpermute_results(a.res, a.res_w, 1, ord.inv, S, oo, s));
-    }
-    return MSH_OK;
+    a.perm = ord.perm;  // rays run in slot order and store their answers to the caller's rows
+    a.out_dist = o.w; a.out_face = o.face; a.out_pt = o.pt;
+    return launch_rays<0, false>(t, a, S, s, "alongnormal");
 }
 
 // Morton order of the main-mesh vertices in the scene box (cached on the handle: visibility sources)
