@@ -348,19 +348,83 @@ __device__ inline FrameD frame_d(const NodeV& nd) {
     f.a[2] = D3{b[0], b[1], b[2]};
     return f;
 }
-// Lower bound of the squared distance from p (projections pp[3] onto the frame) to the oriented box ext:
-// gaps shrunk by a 2^-40 relative margin of the projections, the sum divided by lambda_max(A A^T) <= 1 + 1e-6
-// (covered by 1 - 2^-18).
-__device__ inline double obb_d2_lo_d(const double* pp, const float* ext) {
-    double s = 0.0;
+
+// v_rcp_f32 on the device (1 ulp); the host property test uses the correctly rounded quotient
+__host__ __device__ inline float rcp_f32(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_rcpf(x);
+#else
+    return 1.0f / x;
+#endif
+}
+// ---- conservative fp32 node test of a ray (never rejects a box the ray meets at a real hit) ----
+// The ray o + t d (o relative to the tree origin) is modelled in fp32 as o_f + s u_f, u = d / |d| (s = t |d|).
+// Every hit x lies in the scene ball |x| <= M (M = the tree's half-diagonal), so only |s| <= s_max =
+// |o| + M matters.  Per node axis a_k (fp32 frame, |a_k| <= 1 + 1e-6): po = fl(a_k . o_f) and
+// pd = fl(a_k . u_f) by fma chains.  With u = 2^-24 the model's slab coordinate po + s pd differs from the
+// real a_k . x(s) by <= 4.01u |o| (rounding of o and of the dot) + s_max 4.01u (the same for u); forming
+// the slab sides (ext - (po + mg)) and (ext - (po - mg)) adds <= u(2|o| + 1.02M + 2mg) (ext is the decoded
+// fp32 bound the build verified, |ext| <= 1.02M).  All of it is below mg = 2^-20 (|o| + M) + 2^-100, so a
+// real hit at s* satisfies side_lo <= s* pd <= side_hi, i.e. s* lies in [side_lo, side_hi] / pd.  The
+// computed endpoints side * rcp(pd) are within 3u relative of those quotients (v_rcp_f32: 1 ulp), so the
+// interval test is widened by 2^-20 (|s_near| + |s_far|).  pd == 0 (or flushed) gives +-inf endpoints, or
+// NaN where a side is exactly 0; fminf / fmaxf drop a NaN operand, which only loosens the test, and a model
+// line exactly on a widened side cannot carry a real hit (mg has slack well above every rounding).  A ray
+// the fp32 model cannot represent (|o| + M beyond 2^100) takes every box (`wide`).
+struct RayF {
+    float o[3], u[3];
+    float mg, slo, shi;  // margin, parameter range [slo, shi] in units of |d|
+    bool wide;
+};
+__host__ __device__ inline RayF make_rayf(const D3& o, const D3& d, double M, bool line) {
+    RayF r;
+    const double on = sqrt(vdot(o, o)), dn = sqrt(vdot(d, d));
+    const double smax = (on + M) * (1.0 + 9.5367431640625e-7);
+    r.wide = !(on + M < 1.2676506002282294e30) || !(dn > 0.0 && dn < INFINITY);  // 2^100; NaN -> wide
+    const double inv = r.wide ? 0.0 : 1.0 / dn;
+    r.o[0] = (float)o.x; r.o[1] = (float)o.y; r.o[2] = (float)o.z;
+    r.u[0] = (float)(d.x * inv); r.u[1] = (float)(d.y * inv); r.u[2] = (float)(d.z * inv);
+    r.mg = f32_up(9.5367431640625e-7 * (on + M) + 7.888609052210118e-31);
+    r.shi = f32_up(smax);
+    r.slo = line ? -r.shi : 0.f;
+    return r;
+}
+
+// Both children of a node: does the ray's parameter range meet the child's oriented box, and at which
+// entry parameter (the near-first key of the visibility traversal).
+__host__ __device__ inline void ray_child_slabs(const NodeV& nd, const RayF& r, bool& h0, bool& h1, float& s0, float& s1) {
+    if (r.wide) {
+        h0 = h1 = true;
+        s0 = s1 = r.slo;
+        return;
+    }
+#if defined(MUTATE_RAY_MARGIN)  // tests/csrc/bound_check.cpp's sensitivity check: must find violations
+    const float mg = 0.f;
+#else
+    const float mg = r.mg;
+#endif
+    float A[3][3], e0[6], e1[6];
+    nd.frame(A[0], A[1], A[2]);
+    nd.extents(e0, e1);
+    float n0 = r.slo, f0 = r.shi, n1 = r.slo, f1 = r.shi;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const double lo = ext[k], hi = ext[3 + k];
-        double g = fmax(fmax(lo - pp[k], pp[k] - hi), 0.0);
-        g = fmax(g - 9.094947017729282e-13 * (fabs(pp[k]) + fabs(lo) + fabs(hi)), 0.0);
-        s += g * g;
+        const float po = fmaf(A[k][0], r.o[0], fmaf(A[k][1], r.o[1], A[k][2] * r.o[2]));
+        const float pd = fmaf(A[k][0], r.u[0], fmaf(A[k][1], r.u[1], A[k][2] * r.u[2]));
+        const float inv = rcp_f32(pd);
+        const float gl = po + mg, gh = po - mg;
+        const float a0 = (e0[k] - gl) * inv, b0 = (e0[3 + k] - gh) * inv;
+        const float a1 = (e1[k] - gl) * inv, b1 = (e1[3 + k] - gh) * inv;
+        n0 = fmaxf(n0, fminf(a0, b0));
+        f0 = fminf(f0, fmaxf(a0, b0));
+        n1 = fmaxf(n1, fminf(a1, b1));
+        f1 = fminf(f1, fmaxf(a1, b1));
     }
-    return s * 0.999996185302734375;  // 1 - 2^-18
+    const float w = 9.5367431640625e-7f;  // 2^-20
+    h0 = n0 <= f0 + w * (fabsf(n0) + fabsf(f0));
+    h1 = n1 <= f1 + w * (fabsf(n1) + fabsf(f1));
+    s0 = n0;
+    s1 = n1;
 }
 
 // Per-lane traversal stack: entry sp lives in LDS (lds[sp * kBlock], lane-interleaved) for

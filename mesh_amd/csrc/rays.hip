@@ -17,8 +17,9 @@
 // product of two parallel vectors (0 up to rounding) and its point is not finite.
 //
 // Execution shape: one lane per ray, persistent near-first traversal over the same 64-B nodes as K2:
-// box tests are fp64 slab tests of the ray against each child's oriented box (the ray projected once
-// per node onto the node frame), with a relative margin.  alongnormal rays are Morton-sorted by
+// box tests are conservative fp32 slab tests of the ray against both children's oriented boxes (the ray
+// projected once per node onto the node frame; make_rayf / ray_child_slabs), and alongnormal also bounds
+// the children's distance from p with K2's packed test.  alongnormal rays are Morton-sorted by
 // their source and gathered into slot order like K2's queries; visibility rays run vertex-major per
 // camera over a Morton order of the vertices (cached per tree), so neighbouring lanes cast
 // neighbouring, nearly parallel rays.
@@ -89,54 +90,6 @@ __device__ inline bool cgal_plane_line(const D3& p, const D3& d, const D3& a, co
 
 __device__ inline D3 ray_dir(const D3& p, const D3& v) { return vsub(vadd(p, v), p); }
 
-// 1 / x from the hardware reciprocal estimate and two Newton steps (rcp + 4 fma instead of the ~11
-// instructions of an IEEE division): relative error far below the slab test's 2^-40 tolerance.  Where the
-// estimate is not finite (|x| subnormal) the result is NaN, and the slab test's fmin / fmax then drop that
-// axis — conservative, never a lost hit.
-__device__ inline double rcp_nr(double x) {
-    double r = __builtin_amdgcn_rcp(x);
-    r = fma(r, fma(-x, r, 1.0), r);
-    return fma(r, fma(-x, r, 1.0), r);
-}
-
-// A line o + t d (o relative to the tree origin) projected onto a node frame: o_k = a_k . o, d_k = a_k . d,
-// inv_k = 1 / d_k (flat_k when d_k == 0).  One projection serves both children of a node.
-struct RayProj {
-    double o[3], inv[3];
-    bool flat[3];
-};
-__device__ inline RayProj ray_proj(const FrameD& f, const D3& o, const D3& d) {
-    RayProj r;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        // fused dot products (the slab margin covers their rounding as it does the unfused ones')
-        r.o[k] = fma(f.a[k].x, o.x, fma(f.a[k].y, o.y, f.a[k].z * o.z));
-        const double dk = fma(f.a[k].x, d.x, fma(f.a[k].y, d.y, f.a[k].z * d.z));
-        r.flat[k] = dk == 0.0;
-        r.inv[k] = r.flat[k] ? 0.0 : rcp_nr(dk);
-    }
-    return r;
-}
-
-// Slab test of the line, t in [tlo, thi], against the oriented box {x : lo_k <= a_k . x <= hi_k};
-// tnear = entry parameter.  The slabs are widened by a 2^-40 relative margin for the fp64 projections.
-__device__ inline bool slab(const RayProj& r, const float* ext, double tlo, double thi, double& tnear) {
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const double m = 9.094947017729282e-13 * (fabs((double)ext[k]) + fabs((double)ext[3 + k]) + fabs(r.o[k])) + 1e-300;
-        const double lo = (double)ext[k] - m, hi = (double)ext[3 + k] + m;
-        if (r.flat[k]) {
-            if (r.o[k] < lo || r.o[k] > hi) return false;
-        } else {
-            const double t1 = (lo - r.o[k]) * r.inv[k], t2 = (hi - r.o[k]) * r.inv[k];
-            tlo = fmax(tlo, fmin(t1, t2));
-            thi = fmin(thi, fmax(t1, t2));
-        }
-    }
-    tnear = tlo;
-    return tlo <= thi + 1e-12 * (fabs(tlo) + fabs(thi)) + 1e-300;
-}
-
 // ---- generic traversal: the policy decides box hits (and ordering key) and leaf tests ----
 template <class Pol, bool STATS>
 __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, Pol& pol, uint2* __restrict__ lds,
@@ -150,12 +103,9 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
     for (size_t guard = 0; guard < T; ++guard) {
         const NodeV nd = load_node(nodes, node);
         if (STATS) ++n_nodes;
-        double k0, k1;
-        float e0[6], e1[6];
-        nd.extents(e0, e1);
-        const RayProj rp = pol.project(frame_d(nd));
-        bool h0 = pol.box(rp, e0, k0);
-        bool h1 = pol.box(rp, e1, k1);
+        bool h0, h1;
+        float k0, k1;
+        pol.children(nd, h0, h1, k0, k1);
         const int c0 = nd.child(0), c1 = nd.child(1);
         if (h0 && c0 < 0) {
             pol.test(~c0);
@@ -173,9 +123,9 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
         h1 = h1 && pol.keep(k1);
         if (h0 && h1) {
             int nearc = c0, farc = c1;
-            double kf = k1;
+            float kf = k1;
             if (k1 < k0) { nearc = c1; farc = c0; kf = k0; }
-            const uint2 e = make_uint2((unsigned)farc, __float_as_uint(__double2float_rd(kf)));
+            const uint2 e = make_uint2((unsigned)farc, __float_as_uint(kf));
             stack_put(lds, spill, sp, e);
             ++sp;
             node = nearc;
@@ -187,7 +137,7 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
         while (sp > 0) {
             --sp;
             const uint2 e = stack_get(lds, spill, sp);
-            if (pol.keep((double)__uint_as_float(e.y))) {
+            if (pol.keep(__uint_as_float(e.y))) {
                 node = (int)e.x;
                 found = true;
                 break;
@@ -197,24 +147,26 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
     }
 }
 
-// nearest hit along +-n; key = squared point-box distance (a lower bound of any hit's distance^2)
+// nearest hit along +-n (the line through p); key = lower bound of the squared distance from p to the
+// child's box (K2's packed fp32 bound, node_child_bounds), which also prunes against the best hit so far
 struct AlongPol {
     const TriRec* __restrict__ tris;
     D3 p, dp, dm;
-    D3 pr;        // p relative to the tree origin (node bounds are origin-relative)
+    RayF rf;      // the line, fp32 model
+    QF qf;        // p for the distance bound
     double best;  // distance
     uint32_t best_face;
     D3 best_pt;
     __device__ double lim2() const { return best == INFINITY ? INFINITY : best * best * kSlack; }
-    __device__ RayProj project(const FrameD& f) const { return ray_proj(f, pr, dp); }
-    // the line through p (both directions) meets the box, and the box is within the best distance
-    __device__ bool box(const RayProj& r, const float* ext, double& key) const {
-        key = obb_d2_lo_d(r.o, ext);
-        if (key > lim2()) return false;
-        double tn;
-        return slab(r, ext, -INFINITY, INFINITY, tn);
+    __device__ void children(const NodeV& nd, bool& h0, bool& h1, float& k0, float& k1) const {
+        float s0, s1;
+        ray_child_slabs(nd, rf, h0, h1, s0, s1);
+        node_child_bounds(nd, qf, k0, k1);
+        const double l = lim2();
+        h0 = h0 && (double)k0 <= l;
+        h1 = h1 && (double)k1 <= l;
     }
-    __device__ bool keep(double key) const { return key <= lim2(); }
+    __device__ bool keep(float key) const { return (double)key <= lim2(); }
     __device__ bool done() const { return false; }
     __device__ void test(int leaf) {
         D3 a, b, c;
@@ -242,11 +194,12 @@ struct AlongPol {
 struct AnyPol {
     const TriRec* __restrict__ tris;
     D3 src, d;
-    D3 sr;  // src relative to the tree origin
+    RayF rf;
     bool hit;
-    __device__ RayProj project(const FrameD& f) const { return ray_proj(f, sr, d); }
-    __device__ bool box(const RayProj& r, const float* ext, double& key) const { return slab(r, ext, 0.0, INFINITY, key); }
-    __device__ bool keep(double) const { return !hit; }
+    __device__ void children(const NodeV& nd, bool& h0, bool& h1, float& k0, float& k1) const {
+        ray_child_slabs(nd, rf, h0, h1, k0, k1);
+    }
+    __device__ bool keep(float) const { return !hit; }
     __device__ bool done() const { return hit; }
     __device__ void test(int leaf) {
         D3 a, b, c;
@@ -286,6 +239,7 @@ struct RayArgs {
     uint2* spill;
     int spill_depth;
     double org[3];  // tree origin
+    double M;       // the tree's half-diagonal (hits lie within M of org)
 };
 
 __device__ inline unsigned dequeue_tile_r(unsigned* counters, unsigned ntiles, unsigned group) {
@@ -326,8 +280,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MSH_RAY_
             const D3 p = D3{a.p[3 * i], a.p[3 * i + 1], a.p[3 * i + 2]};
             const D3 n = D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]};
             const D3 dp = ray_dir(p, n), pr = vsub(p, org);
-            AlongPol pol{a.tris, p, dp, ray_dir(p, D3{-n.x, -n.y, -n.z}), pr, INFINITY, MSH_NO_FACE,
-                         D3{NAN, NAN, NAN}};
+            AlongPol pol{a.tris, p, dp, ray_dir(p, D3{-n.x, -n.y, -n.z}), make_rayf(pr, dp, a.M, true),
+                         make_qf(p, a.org, tree_margin(a.M)), INFINITY, MSH_NO_FACE, D3{NAN, NAN, NAN}};
             if (finite_d3(p) && finite_d3(dp))
                 traverse_rays<AlongPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
             if (STATS) continue;
@@ -349,7 +303,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MSH_RAY_
             dir = D3{dir.x / len, dir.y / len, dir.z / len};
             const D3 src = vadd(vv, vscale(a.min_dist, dir));
             const D3 d = ray_dir(src, dir);
-            AnyPol pol{a.tris, src, d, vsub(src, org), false};
+            AnyPol pol{a.tris, src, d, make_rayf(vsub(src, org), d, a.M, false), false};
             if (finite_d3(src) && finite_d3(d))
                 traverse_rays<AnyPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
             if (STATS) continue;
@@ -392,6 +346,7 @@ static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, c
     }
     a.S = nrays;
     for (int k = 0; k < 3; ++k) a.org[k] = tree->origin[k];
+    a.M = tree->half_diag;
     a.ntiles = (unsigned)((nrays + 63) / 64);
     const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, (unsigned)device_cus_r(tree->device) * 5u);
     MSH_TRY(tree->ws.counters.reserve(9 * 32 * sizeof(unsigned)));

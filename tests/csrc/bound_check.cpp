@@ -5,7 +5,9 @@
 // placements (queries on / just off the points, far away, at a large offset from the origin), codes
 // chosen as tight as the contract allows.  Prints "violations=N" (and the worst cases) and exits 1 when
 // N > 0.  -DMUTATE_TREE_TERM / -DMUTATE_QUERY_MARGIN drop a margin term: those builds must fail (the
-// test's sensitivity check, tests/test_abi.py).
+// test's sensitivity check, tests/test_abi.py).  The same nodes check the ray kernels' fp32 slab test
+// (common.h make_rayf / ray_child_slabs): a ray or line through a point of a child must take that child;
+// -DMUTATE_RAY_MARGIN drops its margin and must fail.
 //   hipcc -O2 -std=c++17 -ffp-contract=off -x hip bound_check.cpp -I<csrc> -o bound_check && ./bound_check 200000
 #include <cmath>
 #include <cstdio>
@@ -48,7 +50,7 @@ int main(int argc, char** argv) {
             if (l > 0.1 && l <= 1.0) return D3{x / l, y / l, z / l};
         }
     };
-    long viol = 0, checks = 0, tight = 0, skipped = 0, skipped_anchor = 0;
+    long viol = 0, checks = 0, tight = 0, skipped = 0, skipped_anchor = 0, ray_checks = 0, ray_viol = 0, ray_skipped = 0;
     double worst = 0.0;
     for (long tr = 0; tr < trials; ++tr) {
         // scene scale, node size relative to it, offset of the tree origin
@@ -168,6 +170,65 @@ int main(int argc, char** argv) {
                 ++skipped_anchor;
             }
         }
+        // rays (ray_child_slabs + make_rayf): every ray or line through a point of a child must take that child.
+        // Directions at random, along a frame axis (parallel to two slab pairs) or grazing the n = const faces;
+        // the ray starts at the point or up to 1e3 scene sizes before it (behind it too for lines).
+        {
+            double M = half_diag;
+            const D3 an = D3{anchor.x - origin[0], anchor.y - origin[1], anchor.z - origin[2]};
+            M = std::fmax(M, std::sqrt(vdot(an, an))) * (1.0 + 1e-9);
+            for (int ri = 0; ri < 8; ++ri) {
+                const int ch = at_origin && ri % 2 == 0 ? 1 : (int)(rng() % 2);
+                const D3 x = at_origin && ri % 2 == 0 ? anchor : pts[ch][rng() % 6];
+                const int dk = (int)(rng() % 4);
+                D3 d = unit();
+                if (dk == 1) {
+                    const int ax = (int)(rng() % 3);
+                    d = D3{A[ax][0], A[ax][1], A[ax][2]};
+                } else if (dk == 2) {
+                    const double g = std::pow(10.0, -(double)(3 + rng() % 8)) * U(rng);
+                    d = D3{A[1][0] + g * A[0][0], A[1][1] + g * A[0][1], A[1][2] + g * A[0][2]};
+                } else if (dk == 3) {
+                    d = vscale(std::pow(10.0, (double)((int)(rng() % 13) - 6)), d);  // any length
+                }
+                const bool line = rng() % 2 == 0;
+                const int sk = (int)(rng() % 4);
+                double s = sk == 0 ? 0.0 : (sk == 1 ? node * std::pow(10.0, -(double)(rng() % 8))
+                                                    : S * std::pow(10.0, (double)(rng() % 4)));
+                s /= std::sqrt(vdot(d, d));
+                if (line && rng() % 2 == 0) s = -s;
+                const D3 o = D3{x.x - s * d.x, x.y - s * d.y, x.z - s * d.z};
+                // the rounded origin moves the ray off x by ~1 ulp of |o|: keep the rays that still pass a point
+                // of the decoded box (x' = o + s d in long double)
+                {
+                    const long double xr[3] = {(long double)o.x + (long double)s * d.x - origin[0],
+                                               (long double)o.y + (long double)s * d.y - origin[1],
+                                               (long double)o.z + (long double)s * d.z - origin[2]};
+                    const float* e = ch == 0 ? e0 : e1;
+                    bool in = true;
+                    for (int k = 0; k < 3; ++k) {
+                        const long double pr = A[k][0] * xr[0] + A[k][1] * xr[1] + A[k][2] * xr[2];
+                        in = in && pr >= (long double)e[k] && pr <= (long double)e[3 + k];
+                    }
+                    if (!in) {
+                        ++ray_skipped;
+                        continue;
+                    }
+                }
+                const RayF rf = make_rayf(D3{o.x - origin[0], o.y - origin[1], o.z - origin[2]}, d, M, line);
+                bool h[2];
+                float s0, s1;
+                ray_child_slabs(nd, rf, h[0], h[1], s0, s1);
+                ++ray_checks;
+                if (!h[ch]) {
+                    ++viol;
+                    ++ray_viol;
+                    if (ray_viol <= 5)
+                        std::fprintf(stderr, "ray violation: dk=%d sk=%d line=%d S=%g node=%g off=%g s=%g\n", dk, sk,
+                                     (int)line, S, node, off, s);
+                }
+            }
+        }
         // queries: on a point, just off it (1e-12 .. 1e-3 node), inside the box, far away
         for (int qi = 0; qi < 8; ++qi) {
             const int ch = (int)(rng() % 2), pi = (int)(rng() % 6);
@@ -219,7 +280,8 @@ int main(int argc, char** argv) {
             }
         }
     }
-    std::printf("trials=%ld skipped=%ld anchors_skipped=%ld checks=%ld tight=%ld violations=%ld worst_rel=%g\n", trials,
-                skipped, skipped_anchor, checks, tight, viol, worst);
+    std::printf("trials=%ld skipped=%ld anchors_skipped=%ld checks=%ld tight=%ld ray_checks=%ld ray_skipped=%ld ray_violations=%ld "
+                "violations=%ld worst_rel=%g\n", trials, skipped, skipped_anchor, checks, tight, ray_checks, ray_skipped, ray_viol,
+                viol, worst);
     return viol == 0 && skipped == 0 ? 0 : 1;
 }

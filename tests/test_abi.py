@@ -113,12 +113,13 @@ def test_bad_face_index_rejected_before_device():
     assert b"references vertex 7" in L.msh_last_error()
 
 
-@pytest.mark.parametrize("mutation", [None, "MUTATE_TREE_TERM", "MUTATE_QUERY_MARGIN"])
+@pytest.mark.parametrize("mutation", [None, "MUTATE_TREE_TERM", "MUTATE_QUERY_MARGIN", "MUTATE_RAY_MARGIN"])
 def test_child_box_bound_is_conservative(tmp_path, mutation):
     """The traversal's fp32 child-box bound (common.h node_child_bounds with make_qf's margin) never exceeds
-    the squared distance from the fp64 query to a point its box contains: 300k random and adversarial
-    nodes/queries on a host build of the kernels' own header.  The mutated builds (one margin term dropped)
-    must find violations, which shows the cases reach the margins."""
+    the squared distance from the fp64 query to a point its box contains, and the ray kernels' fp32 slab
+    test (make_rayf / ray_child_slabs) takes every child a ray passes a point of: 300k random and
+    adversarial nodes/queries/rays on a host build of the kernels' own header.  The mutated builds (one
+    margin term dropped) must find violations, which shows the cases reach the margins."""
     import subprocess
     exe = str(tmp_path / "bound_check")
     cmd = ["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-x", "hip",
@@ -129,7 +130,7 @@ def test_child_box_bound_is_conservative(tmp_path, mutation):
     subprocess.check_call(cmd)
     out = subprocess.run([exe, "300000"], capture_output=True, text=True, timeout=300)
     line = [x for x in out.stdout.splitlines() if x.startswith("trials=")][-1]
-    viol = int(line.split("violations=")[1].split()[0])
+    viol = int(line.split(" violations=")[1].split()[0])
     if mutation is None:
         assert out.returncode == 0 and viol == 0, out.stdout + out.stderr
     else:

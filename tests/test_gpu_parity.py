@@ -154,6 +154,49 @@ def test_c3_full_size_properties(oracle):
     assert np.all(np.abs(pt[idx] - cpt) <= 1e-6 * diag)
 
 
+def test_c3_headline_stream(oracle):
+    # The exact stream bench.py times (100M uniform queries generated in HBM, seed 3, the device entry
+    # point): shell bounds on every answer, and bit-exact against the exhaustive oracle on 2000 rows
+    # (1500 at random + the 500 closest to the centre, where the deferred pass 2 answers).
+    import torch
+    from mesh_amd import spatialsearch
+    from mesh_amd.distributed import nearest_device
+    v, f = W.c3_mesh()
+    S = 100_000_000
+    g = torch.Generator(device="cuda:0")
+    g.manual_seed(3)
+    dq = (torch.rand((S, 3), generator=g, dtype=torch.float64, device="cuda:0") * 2.2 - 1.1).contiguous()
+    t = spatialsearch.aabbtree_compute(v, f)
+    df = torch.empty(S, dtype=torch.int32, device="cuda:0")
+    dp = torch.empty(S, dtype=torch.int32, device="cuda:0")
+    dpt = torch.empty((S, 3), dtype=torch.float64, device="cuda:0")
+    nearest_device(t, dq, df, dp, dpt)
+    torch.cuda.synchronize()
+    q = dq.cpu().numpy()
+    del dq
+    face = df.cpu().numpy().view(np.uint32)
+    part = dp.cpu().numpy().view(np.uint32)
+    pt = dpt.cpu().numpy()
+    del df, dp, dpt
+    assert face.max() < f.shape[0] and part.max() <= 6 and np.isfinite(pt).all()
+    # every vertex is on the unit sphere and every face plane at least r_in from the centre, so the
+    # surface lies in the shell r_in <= |x| <= 1: d >= max(|q| - 1, r_in - |q|), and the face under the
+    # radial projection of q is within one edge length: d <= ||q| - 1| + e_max
+    tri = v[f.astype(np.int64)]
+    nrm = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
+    r_in = float(np.min(np.abs(np.einsum("ij,ij->i", nrm, tri[:, 0])) / np.linalg.norm(nrm, axis=1)))
+    e_max = float(max(np.linalg.norm(tri[:, i] - tri[:, (i + 1) % 3], axis=1).max() for i in range(3)))
+    d = np.sqrt(np.einsum("ij,ij->i", pt - q, pt - q))
+    r = np.sqrt(np.einsum("ij,ij->i", q, q))
+    tol = 1e-12
+    assert np.all(d >= np.maximum(r - 1.0, r_in - r) - tol)
+    assert np.all(d <= np.abs(r - 1.0) + e_max + tol)
+    idx = np.concatenate([np.random.default_rng(5).choice(S, 1500, replace=False), np.argpartition(r, 500)[:500]])
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[idx])
+    assert np.array_equal(face[idx], bf), "faces differ at %s" % idx[np.nonzero(face[idx] != bf)[0][:10]]
+    assert np.array_equal(part[idx], bp) and np.array_equal(pt[idx], bpt)
+
+
 def test_normals_random_bit_exact(oracle):
     from mesh_amd import aabb_normals
     v, f = W.c2_mesh()
