@@ -362,9 +362,10 @@ __host__ __device__ inline float rcp_f32(float x) {
 // Every hit x lies in the scene ball |x| <= M (M = the tree's half-diagonal), so only |s| <= s_max =
 // |o| + M matters.  Per node axis a_k (fp32 frame, |a_k| <= 1 + 1e-6): po = fl(a_k . o_f) and
 // pd = fl(a_k . u_f) by fma chains.  With u = 2^-24 the model's slab coordinate po + s pd differs from the
-// real a_k . x(s) by <= 4.01u |o| (rounding of o and of the dot) + s_max 4.01u (the same for u); forming
-// the slab sides (ext - (po + mg)) and (ext - (po - mg)) adds <= u(2|o| + 1.02M + 2mg) (ext is the decoded
-// fp32 bound the build verified, |ext| <= 1.02M).  All of it is below mg = 2^-20 (|o| + M) + 2^-100, so a
+// real a_k . x(s) by <= 4.01u |o| (rounding of o and of the dot) + s_max 4.01u (the same for u).  A slab
+// side is formed as fma(code, 2^e, base - (po +- mg)), the decoded bound and the margin in one rounding:
+// against the decoded fp32 bound the build verified (|bound|, |base| <= 1.02M) that adds <= u(3|o| + 3.06M
+// + 3mg).  All of it is below mg = 2^-20 (|o| + M) + 2^-100, so a
 // real hit at s* satisfies side_lo <= s* pd <= side_hi, i.e. s* lies in [side_lo, side_hi] / pd.  The
 // computed endpoints side * rcp(pd) are within 3u relative of those quotients (v_rcp_f32: 1 ulp), so the
 // interval test is widened by 2^-20 (|s_near| + |s_far|).  pd == 0 (or flushed) gives +-inf endpoints, or
@@ -403,22 +404,33 @@ __host__ __device__ inline void ray_child_slabs(const NodeV& nd, const RayF& r, 
 #else
     const float mg = r.mg;
 #endif
-    float A[3][3], e0[6], e1[6];
-    nd.frame(A[0], A[1], A[2]);
-    nd.extents(e0, e1);
+    // frame pairs (n_k, t_k) and b = n x t exactly as frame_b / node_child_bounds form them
+    const F2 P0 = f2(nd.q[0].x, nd.q[0].y), P1 = f2(nd.q[0].z, nd.q[0].w), P2 = f2(nd.q[1].x, nd.q[1].y);
+    const F2 m0 = P1 * P2.yx, m1 = P2 * P0.yx, m2 = P0 * P1.yx;
+    const float bx = m0.x - m0.y, by = m1.x - m1.y, bz = m2.x - m2.y;
+    // (n, t) projections of origin and direction as packed fma chains, b's scalar
+    const F2 po_nt = pfma(P0, f2(r.o[0]), pfma(P1, f2(r.o[1]), P2 * f2(r.o[2])));
+    const F2 pd_nt = pfma(P0, f2(r.u[0]), pfma(P1, f2(r.u[1]), P2 * f2(r.u[2])));
+    const float po[3] = {po_nt.x, po_nt.y, fmaf(bx, r.o[0], fmaf(by, r.o[1], bz * r.o[2]))};
+    const float pd[3] = {pd_nt.x, pd_nt.y, fmaf(bx, r.u[0], fmaf(by, r.u[1], bz * r.u[2]))};
+    const uint32_t w0 = nd.word(11), w1 = nd.word(12), w2 = nd.word(13), we = nd.word(14);
+    const float sc[3] = {u2f(we & 0x7f800000u), nd.q[3].w, u2f(we << 23)};
+    const uint32_t u[12] = {w0 & 0xffu, (w0 >> 8) & 0xffu, (w0 >> 16) & 0xffu, w0 >> 24,
+                            w1 & 0xffu, (w1 >> 8) & 0xffu, (w1 >> 16) & 0xffu, w1 >> 24,
+                            w2 & 0xffu, (w2 >> 8) & 0xffu, (w2 >> 16) & 0xffu, w2 >> 24};
+    const F2 pm = f2(mg, -mg);
     float n0 = r.slo, f0 = r.shi, n1 = r.slo, f1 = r.shi;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        const float po = fmaf(A[k][0], r.o[0], fmaf(A[k][1], r.o[1], A[k][2] * r.o[2]));
-        const float pd = fmaf(A[k][0], r.u[0], fmaf(A[k][1], r.u[1], A[k][2] * r.u[2]));
-        const float inv = rcp_f32(pd);
-        const float gl = po + mg, gh = po - mg;
-        const float a0 = (e0[k] - gl) * inv, b0 = (e0[3 + k] - gh) * inv;
-        const float a1 = (e1[k] - gl) * inv, b1 = (e1[3 + k] - gh) * inv;
-        n0 = fmaxf(n0, fminf(a0, b0));
-        f0 = fminf(f0, fmaxf(a0, b0));
-        n1 = fmaxf(n1, fminf(a1, b1));
-        f1 = fminf(f1, fmaxf(a1, b1));
+        const F2 inv = f2(rcp_f32(pd[k]));
+        // (base - (po + mg), base - (po - mg)); each slab side is one fma of the code, the scale and that
+        const F2 g = f2(nd.at(kBase + k)) - (f2(po[k]) + pm);
+        const F2 t0 = pfma(f2((float)u[k], (float)u[3 + k]), f2(sc[k]), g) * inv;
+        const F2 t1 = pfma(f2((float)u[6 + k], (float)u[9 + k]), f2(sc[k]), g) * inv;
+        n0 = fmaxf(n0, fminf(t0.x, t0.y));
+        f0 = fminf(f0, fmaxf(t0.x, t0.y));
+        n1 = fmaxf(n1, fminf(t1.x, t1.y));
+        f1 = fminf(f1, fmaxf(t1.x, t1.y));
     }
     const float w = 9.5367431640625e-7f;  // 2^-20
     h0 = n0 <= f0 + w * (fabsf(n0) + fabsf(f0));

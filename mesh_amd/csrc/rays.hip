@@ -151,12 +151,12 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
 // child's box (K2's packed fp32 bound, node_child_bounds), which also prunes against the best hit so far
 struct AlongPol {
     const TriRec* __restrict__ tris;
-    D3 p, dp, dm;
+    D3 p, n;      // the rays (p, n) and (p, -n); directions ray_dir(p, +-n) are formed per leaf test
     RayF rf;      // the line, fp32 model
     QF qf;        // p for the distance bound
     double best;  // distance
     uint32_t best_face;
-    D3 best_pt;
+    int best_leaf;  // the hit point is rebuilt from it at the end (hit()), not carried through the walk
     __device__ double lim2() const { return best == INFINITY ? INFINITY : best * best * kSlack; }
     __device__ void children(const NodeV& nd, bool& h0, bool& h1, float& k0, float& k1) const {
         float s0, s1;
@@ -168,25 +168,45 @@ struct AlongPol {
     }
     __device__ bool keep(float key) const { return (double)key <= lim2(); }
     __device__ bool done() const { return false; }
+    // hit point and distance of the ray along +n (k = 0) or -n (k = 1); false: no hit
+    __device__ bool along(int k, const D3& a, const D3& b, const D3& c, D3& hit, double& dist) const {
+        const D3 d = ray_dir(p, k == 0 ? n : D3{-n.x, -n.y, -n.z});
+        double t;
+        const int kind = ray_tri(p, d, a, b, c, t);
+        if (!kind) return false;
+        if (kind == 2 || !cgal_plane_line(p, d, a, b, c, hit)) hit = vadd(p, vscale(t, d));
+        dist = sqrt(sqdist(hit, p));
+        return true;
+    }
     __device__ void test(int leaf) {
         D3 a, b, c;
         uint32_t face;
         load_tri(tris, leaf, a, b, c, face);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-            const D3& d = k == 0 ? dp : dm;
-            double t;
-            const int kind = ray_tri(p, d, a, b, c, t);
-            if (!kind) continue;
             D3 hit;
-            if (kind == 2 || !cgal_plane_line(p, d, a, b, c, hit)) hit = vadd(p, vscale(t, d));
-            const double dist = sqrt(sqdist(hit, p));
+            double dist;
+            if (!along(k, a, b, c, hit, dist)) continue;
             if (dist < best || (dist == best && face < best_face)) {
                 best = dist;
                 best_face = face;
-                best_pt = hit;
+                best_leaf = leaf;
             }
         }
+    }
+    // the winning hit: the first direction of the best leaf at the best distance (the one test() kept)
+    __device__ D3 hit() const {
+        D3 out = D3{NAN, NAN, NAN};
+        if (best_leaf < 0) return out;
+        D3 a, b, c;
+        uint32_t face;
+        load_tri(tris, best_leaf, a, b, c, face);
+        for (int k = 0; k < 2; ++k) {
+            D3 h;
+            double dist;
+            if (along(k, a, b, c, h, dist) && dist == best) return h;
+        }
+        return out;
     }
 };
 
@@ -258,10 +278,13 @@ __device__ inline unsigned dequeue_tile_r(unsigned* counters, unsigned ntiles, u
 __device__ inline bool finite_d3(const D3& x) { return isfinite(x.x) && isfinite(x.y) && isfinite(x.z); }
 
 #ifndef MSH_RAY_WAVES
-#define MSH_RAY_WAVES 4  // 4 waves per SIMD: alongnormal 163 -> 128 VGPRs (+5 % on C5), visibility already fits
+#define MSH_RAY_WAVES 4  // visibility: 4 waves per SIMD (127 VGPRs, no spills)
+#endif
+#ifndef MSH_ALONG_WAVES
+#define MSH_ALONG_WAVES 3  // alongnormal: at 4 waves the fp64 leaf test spills 37 VGPRs (C5: 7.41 vs 6.62 ms)
 #endif
 template <int MODE, bool STATS>  // MODE 0 alongnormal, 1 visibility
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MSH_RAY_WAVES))) void k_rays(RayArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? MSH_ALONG_WAVES : MSH_RAY_WAVES))) void k_rays(RayArgs a) {
     unsigned n_nodes = 0, n_leaves = 0;
     __shared__ uint2 stk[kStack * kBlock];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -280,8 +303,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MSH_RAY_
             const D3 p = D3{a.p[3 * i], a.p[3 * i + 1], a.p[3 * i + 2]};
             const D3 n = D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]};
             const D3 dp = ray_dir(p, n), pr = vsub(p, org);
-            AlongPol pol{a.tris, p, dp, ray_dir(p, D3{-n.x, -n.y, -n.z}), make_rayf(pr, dp, a.M, true),
-                         make_qf(p, a.org, tree_margin(a.M)), INFINITY, MSH_NO_FACE, D3{NAN, NAN, NAN}};
+            AlongPol pol{a.tris, p, n, make_rayf(pr, dp, a.M, true), make_qf(p, a.org, tree_margin(a.M)), INFINITY,
+                         MSH_NO_FACE, -1};
             if (finite_d3(p) && finite_d3(dp))
                 traverse_rays<AlongPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
             if (STATS) continue;
@@ -289,9 +312,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MSH_RAY_
             const size_t r = a.perm ? (size_t)a.perm[i] : i;  // the caller's row (scattered store)
             a.out_dist[r] = dist;
             a.out_face[r] = pol.best_face;
-            a.out_pt[3 * r] = pol.best_pt.x;
-            a.out_pt[3 * r + 1] = pol.best_pt.y;
-            a.out_pt[3 * r + 2] = pol.best_pt.z;
+            const D3 h = pol.hit();
+            a.out_pt[3 * r] = h.x;
+            a.out_pt[3 * r + 1] = h.y;
+            a.out_pt[3 * r + 2] = h.z;
         } else {
             const size_t ic = i / a.nv, k = i - ic * a.nv;
             const size_t iv = a.vorder ? (size_t)a.vorder[k] : a.v0 + k;  // vertex (global index)
