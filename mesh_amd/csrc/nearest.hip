@@ -943,7 +943,13 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     a.n_deferred = a.counters + 8 * 32;
     MSH_HIP(hipMemsetAsync(a.counters, 0, 10 * 32 * sizeof(unsigned), s));  // + the pass-2 item counter
     // leader ordering: closest-point launches over a Morton-sorted slot order (records in a.res)
-    const bool lead = kLead > 1 && (MODE == 0 || MODE == 3) && a.res != nullptr && a.S >= 64 * (size_t)kLead;
+// leader phases only for trees of >= MSH_LEAD_MIN_T leaves: on a small tree the hint saves little and the
+// three dependent launches serialise their slowest tiles (C1: 0.56 -> 0.29 ms)
+#ifndef MSH_LEAD_MIN_T
+#define MSH_LEAD_MIN_T 4096
+#endif
+    const bool lead = kLead > 1 && (MODE == 0 || MODE == 3) && a.res != nullptr && a.S >= 64 * (size_t)kLead &&
+                      a.T >= (size_t)MSH_LEAD_MIN_T;
     const size_t n_lead = (a.S + kLead - 1) / kLead;
     const unsigned max_tiles = (unsigned)((a.S + 63) / 64);
     const unsigned nblk_max = std::min<unsigned>((max_tiles + 3) / 4, ncu * kKnnBlocksPerCU);
@@ -968,6 +974,13 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     auto pass1 = [&](int phase, size_t nunits, const char* name) -> int {
         a.phase = phase;
         a.budget = phase == 3 ? kBudget3 : (phase == 1 ? kBudget1 : kBudget);
+        // small trees: a query that walks T/16 nodes (the centre of a coarse closed mesh) goes to the
+        // wave-cooperative pass 2 instead of holding its tile for up to T serial steps (C1, 840 faces:
+        // traversal 1.15 -> 0.56 ms; with no leader phases below, 0.29 ms)
+#ifndef MSH_SMALL_DIV
+#define MSH_SMALL_DIV 16
+#endif
+        a.budget = std::min<unsigned>(a.budget, (unsigned)std::max<size_t>(64, a.T / MSH_SMALL_DIV));
         a.nunits = nunits;
         a.ntiles = (unsigned)((nunits + 63) / 64);
         const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, ncu * kKnnBlocksPerCU);
