@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <memory>
 
+#include <vector>
+
 #include "internal.h"
 
 namespace msh {
@@ -221,15 +223,20 @@ __device__ inline float out_hi(double x) { return up1(__double2float_ru(x)); }
 __global__ __launch_bounds__(kBlock) void k_depth(const uint32_t* __restrict__ parent, int B, int n,
                                                   unsigned* __restrict__ out) {
     const long long leaf = (long long)blockIdx.x * kBlock + threadIdx.x;
-    if (leaf >= (long long)B * n) return;
-    const uint32_t root = (uint32_t)((leaf / n) * (n - 1));
-    unsigned d = 1;
-    uint32_t p = parent[(size_t)B * (n - 1) + leaf];
-    while ((p >> 1) != root && d < 4096u) {
-        p = parent[p >> 1];
-        ++d;
+    unsigned d = 0;
+    if (leaf < (long long)B * n) {
+        const uint32_t root = (uint32_t)((leaf / n) * (n - 1));
+        d = 1;
+        uint32_t p = parent[(size_t)B * (n - 1) + leaf];
+        while ((p >> 1) != root && d < 4096u) {
+            p = parent[p >> 1];
+            ++d;
+        }
     }
-    atomicMax(out, d);
+    // one atomic per wave: 41M same-address atomics (C4) took 7.3 ms
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) d = max(d, (unsigned)__shfl_xor((int)d, o, 64));
+    if ((threadIdx.x & 63) == 0 && d > 0) atomicMax(out, d);
 }
 
 // ---- oriented boxes: one wave per internal node ----
@@ -267,9 +274,12 @@ struct ObbFrame {
     float n[3], t[3], b[3];
     double A[3][3];
 };
-__device__ inline ObbFrame obb_frame(double sx, double sy, double sz) {
+// sa = the sum of the area vectors' lengths: a node whose normals cancel (|s| <= 1e-6 sa: a closed surface,
+// e.g. the root of a sphere) has no meaningful normal, and its rounding-noise direction would give its
+// children arbitrarily tilted boxes; it takes the axis frame (n = x) instead.
+__device__ inline ObbFrame obb_frame(double sx, double sy, double sz, double sa) {
     const double len = sqrt(sx * sx + sy * sy + sz * sz);
-    const D3 n = (len > 0.0 && len < INFINITY) ? D3{sx / len, sy / len, sz / len} : D3{1.0, 0.0, 0.0};
+    const D3 n = (len > 1e-6 * sa && len < INFINITY) ? D3{sx / len, sy / len, sz / len} : D3{1.0, 0.0, 0.0};
     const D3 e = fabs(n.x) < 0.9 ? D3{1.0, 0.0, 0.0} : D3{0.0, 1.0, 0.0};
     D3 t = vsub(e, vscale(vdot(e, n), n));
     const double tl = sqrt(vdot(t, t));
@@ -360,7 +370,12 @@ __device__ inline void encode_node(BNode* node, const ObbFrame& fr, const float 
     *reinterpret_cast<float4*>(f + 12) = make_float4(__uint_as_float(w[1]), __uint_as_float(w[2]), h[14], h[15]);
 }
 
-constexpr int kObbLane = 32;  // nodes over at most this many leaves: one lane each; larger: one wave each
+constexpr int kObbLane = 32;    // nodes over at most this many leaves: one lane each; up to kObbBig: one wave each
+#ifndef MSH_OBB_BIG
+#define MSH_OBB_BIG 4096
+#endif
+constexpr int kObbBig = MSH_OBB_BIG;  // larger nodes (the top levels): kObbChunk-leaf chunks, one block per chunk
+constexpr int kObbChunk = 1024;
 
 // Oriented boxes of nodes over at most kObbLane leaves, one lane per node (most nodes: the lower levels)
 template <bool TRI>
@@ -373,12 +388,13 @@ __global__ __launch_bounds__(kBlock) void k_obb_lane(const void* __restrict__ le
     if (r.y - r.x + 1 > kObbLane) return;
     const int mb = node / npm;  // mesh of the node (npm internal nodes per mesh)
     const double o[3] = {orgs[3 * mb], orgs[3 * mb + 1], orgs[3 * mb + 2]};
-    double sx = 0, sy = 0, sz = 0;
+    double sx = 0, sy = 0, sz = 0, sa = 0;
     for (int i = r.x; i <= r.y; ++i) {
         const D3 c = leaf_area<TRI>(leaves, i);
         sx += c.x; sy += c.y; sz += c.z;
+        sa += sqrt(vdot(c, c));
     }
-    const ObbFrame fr = obb_frame(sx, sy, sz);
+    const ObbFrame fr = obb_frame(sx, sy, sz, sa);
     float ext[2][6];
     for (int side = 0; side < 2; ++side) {
         double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -396,20 +412,21 @@ __global__ __launch_bounds__(kBlock) void k_obb_lane(const void* __restrict__ le
 template <bool TRI>
 __global__ __launch_bounds__(kBlock) void k_obb_wave(const void* __restrict__ leaves, const int4* __restrict__ ranges,
                                                      int nn, int npm, BNode* __restrict__ nodes,
-                                                     const double* __restrict__ orgs) {
+                                                     const double* __restrict__ orgs, int maxr) {
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (kBlock / 64);
     for (int node = (blockIdx.x * kBlock + threadIdx.x) >> 6; node < nn; node += waves) {
         const int4 r = ranges[node];
-        if (r.y - r.x + 1 <= kObbLane) continue;
+        if (r.y - r.x + 1 <= kObbLane || r.y - r.x + 1 > maxr) continue;
         const int mb = node / npm;
         const double o[3] = {orgs[3 * mb], orgs[3 * mb + 1], orgs[3 * mb + 2]};
-        double sx = 0, sy = 0, sz = 0;
+        double sx = 0, sy = 0, sz = 0, sa = 0;
         for (int i = r.x + lane; i <= r.y; i += 64) {
             const D3 c = leaf_area<TRI>(leaves, i);
             sx += c.x; sy += c.y; sz += c.z;
+            sa += sqrt(vdot(c, c));
         }
-        const ObbFrame fr = obb_frame(wsum(sx), wsum(sy), wsum(sz));
+        const ObbFrame fr = obb_frame(wsum(sx), wsum(sy), wsum(sz), wsum(sa));
         float ext[2][6];
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
@@ -424,6 +441,157 @@ __global__ __launch_bounds__(kBlock) void k_obb_wave(const void* __restrict__ le
         }
         if (lane == 0) encode_node(nodes + node, fr, ext);
     }
+}
+
+// ---- nodes over more than kObbBig leaves: one wave per node would leave the root's wave walking T leaves
+// alone (C5, 5M faces: 85 ms).  Their ranges are cut into kObbChunk-leaf chunks, one block per chunk; the
+// partial area sums are added in chunk order (deterministic) into the frame, the partial extents are
+// min / max-reduced, and the node is encoded as k_obb_wave would.
+__global__ __launch_bounds__(kBlock) void k_big_count(const int4* __restrict__ ranges, int nn, unsigned* __restrict__ count) {
+    const int node = blockIdx.x * kBlock + threadIdx.x;
+    bool big = false;
+    if (node < nn) {
+        const int4 r = ranges[node];
+        big = r.y - r.x + 1 > kObbBig;
+    }
+    const unsigned long long m = __ballot(big);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(count, (unsigned)__popcll(m));
+}
+__global__ __launch_bounds__(kBlock) void k_big_nodes(const int4* __restrict__ ranges, int nn, int* __restrict__ list,
+                                                      int4* __restrict__ lr, unsigned* __restrict__ count) {
+    const int node = blockIdx.x * kBlock + threadIdx.x;
+    if (node >= nn) return;
+    const int4 r = ranges[node];
+    if (r.y - r.x + 1 <= kObbBig) return;
+    const unsigned k = atomicAdd(count, 1u);
+    list[k] = node;
+    lr[k] = r;
+}
+
+// block reduction in a fixed order (waves, then the 4 wave results in order)
+__device__ inline double block_sum(double x, double* sh) {
+    x = wsum(x);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+    __syncthreads();
+    return ((sh[0] + sh[1]) + sh[2]) + sh[3];
+}
+__device__ inline double block_min(double x, double* sh) {
+    x = wmin(x);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+    __syncthreads();
+    return fmin(fmin(sh[0], sh[1]), fmin(sh[2], sh[3]));
+}
+__device__ inline double block_max(double x, double* sh) {
+    x = wmax(x);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = x;
+    __syncthreads();
+    return fmax(fmax(sh[0], sh[1]), fmax(sh[2], sh[3]));
+}
+
+// item = (big node b, chunk c): partial area sum of the chunk's leaves
+template <bool TRI>
+__global__ __launch_bounds__(kBlock) void k_big_area(const void* __restrict__ leaves, const int4* __restrict__ lr,
+                                                     const int2* __restrict__ items, double* __restrict__ part) {
+    __shared__ double sh[4];
+    const int2 it = items[blockIdx.x];
+    const int4 r = lr[it.x];
+    const int b = r.x + it.y * kObbChunk, e = min(r.y, b + kObbChunk - 1);
+    double sx = 0, sy = 0, sz = 0, sa = 0;
+    for (int i = b + (int)threadIdx.x; i <= e; i += kBlock) {
+        const D3 c = leaf_area<TRI>(leaves, i);
+        sx += c.x; sy += c.y; sz += c.z;
+        sa += sqrt(vdot(c, c));
+    }
+    sx = block_sum(sx, sh);
+    sy = block_sum(sy, sh);
+    sz = block_sum(sz, sh);
+    sa = block_sum(sa, sh);
+    if (threadIdx.x == 0) {
+        part[4 * blockIdx.x] = sx;
+        part[4 * blockIdx.x + 1] = sy;
+        part[4 * blockIdx.x + 2] = sz;
+        part[4 * blockIdx.x + 3] = sa;
+    }
+}
+
+// one thread per big node: the frame from its chunks' area sums, in chunk order
+__global__ __launch_bounds__(kBlock) void k_big_frame(int nbig, const int* __restrict__ off, const double* __restrict__ part,
+                                                      ObbFrame* __restrict__ frames) {
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= nbig) return;
+    double sx = 0, sy = 0, sz = 0, sa = 0;
+    for (int k = off[b]; k < off[b + 1]; ++k) {
+        sx += part[4 * k];
+        sy += part[4 * k + 1];
+        sz += part[4 * k + 2];
+        sa += part[4 * k + 3];
+    }
+    frames[b] = obb_frame(sx, sy, sz, sa);
+}
+
+// partial extents of a chunk on its node's frame, per side of the node's split: ext[item][side][lo k, hi k]
+template <bool TRI>
+__global__ __launch_bounds__(kBlock) void k_big_extent(const void* __restrict__ leaves, const int* __restrict__ list,
+                                                       const int4* __restrict__ lr, const int2* __restrict__ items,
+                                                       const ObbFrame* __restrict__ frames, int npm,
+                                                       const double* __restrict__ orgs, double* __restrict__ ext) {
+    __shared__ double sh[4];
+    const int2 it = items[blockIdx.x];
+    const int4 r = lr[it.x];
+    const ObbFrame fr = frames[it.x];
+    const int mb = list[it.x] / npm;
+    const double o[3] = {orgs[3 * mb], orgs[3 * mb + 1], orgs[3 * mb + 2]};
+    const int b = r.x + it.y * kObbChunk, e = min(r.y, b + kObbChunk - 1);
+    double mn[2][3], mx[2][3];
+#pragma unroll
+    for (int side = 0; side < 2; ++side)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            mn[side][k] = INFINITY;
+            mx[side][k] = -INFINITY;
+        }
+    for (int i = b + (int)threadIdx.x; i <= e; i += kBlock) {
+        if (i <= r.z) leaf_extent<TRI>(leaves, i, fr, o, mn[0], mx[0]);
+        else leaf_extent<TRI>(leaves, i, fr, o, mn[1], mx[1]);
+    }
+    double* out = ext + 12 * (size_t)blockIdx.x;
+#pragma unroll
+    for (int side = 0; side < 2; ++side)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const double lo = block_min(mn[side][k], sh);
+            const double hi = block_max(mx[side][k], sh);
+            if (threadIdx.x == 0) {
+                out[6 * side + k] = lo;
+                out[6 * side + 3 + k] = hi;
+            }
+        }
+}
+
+// one thread per big node: reduce its chunks' extents and encode the node
+__global__ __launch_bounds__(kBlock) void k_big_encode(int nbig, const int* __restrict__ list, const int* __restrict__ off,
+                                                       const ObbFrame* __restrict__ frames, const double* __restrict__ ext,
+                                                       BNode* __restrict__ nodes) {
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    if (b >= nbig) return;
+    double m[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) m[j] = (j % 6) < 3 ? INFINITY : -INFINITY;
+    for (int k = off[b]; k < off[b + 1]; ++k)
+#pragma unroll
+        for (int j = 0; j < 12; ++j) m[j] = (j % 6) < 3 ? fmin(m[j], ext[12 * (size_t)k + j]) : fmax(m[j], ext[12 * (size_t)k + j]);
+    float e[2][6];
+#pragma unroll
+    for (int side = 0; side < 2; ++side)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            e[side][k] = out_lo(m[6 * side + k]);
+            e[side][3 + k] = out_hi(m[6 * side + 3 + k]);
+        }
+    encode_node(nodes + list[b], frames[b], e);
 }
 
 // leaf k holds primitive order[k] = b*T + t of mesh b; its face id is the mesh-local t (+ face_base)
@@ -488,6 +656,92 @@ int pack_point_leaves(const double* d_v, const uint32_t* d_order, size_t P, PtRe
     return MSH_OK;
 }
 
+// nodes over more than kObbBig leaves (k_big_*): list them, cut their ranges into chunks (host-side item
+// map, a few thousand entries), then partial sums / frames / partial extents / encode
+static int build_obb_big(msh_tree* tree, bool triangles, const int4* ranges, int nn, int npm, hipStream_t s,
+                         int& maxr) {
+    // meshes of up to 4 kObbBig faces: their largest nodes are short work for one wave, and the list /
+    // item set-up (a few allocations and host round trips) would cost more (C2: 1.7 -> 2.5 ms)
+    if (tree->T <= 4 * (size_t)kObbBig) return MSH_OK;
+    struct Tmp {
+        void* p = nullptr;
+        ~Tmp() { if (p) (void)hipFree(p); }
+    } t_list, t_lr, t_cnt, t_items, t_off, t_part, t_frames, t_ext;
+    const unsigned nblk = (unsigned)(((size_t)nn + kBlock - 1) / kBlock);
+    MSH_HIP(hipMalloc(&t_cnt.p, sizeof(unsigned)));
+    MSH_HIP(hipMemsetAsync(t_cnt.p, 0, sizeof(unsigned), s));
+    k_big_count<<<nblk, kBlock, 0, s>>>(ranges, nn, static_cast<unsigned*>(t_cnt.p));
+    MSH_HIP(hipGetLastError());
+    unsigned nbig = 0;
+    MSH_HIP(hipMemcpyAsync(&nbig, t_cnt.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+    MSH_HIP(hipStreamSynchronize(s));
+    if (nbig == 0) return MSH_OK;
+    MSH_HIP(hipMalloc(&t_list.p, (size_t)nbig * sizeof(int)));
+    MSH_HIP(hipMalloc(&t_lr.p, (size_t)nbig * sizeof(int4)));
+    MSH_HIP(hipMemsetAsync(t_cnt.p, 0, sizeof(unsigned), s));
+    k_big_nodes<<<nblk, kBlock, 0, s>>>(ranges, nn, static_cast<int*>(t_list.p), static_cast<int4*>(t_lr.p),
+                                        static_cast<unsigned*>(t_cnt.p));
+    MSH_HIP(hipGetLastError());
+    std::vector<int> list(nbig);
+    std::vector<int4> lr(nbig);
+    MSH_HIP(hipMemcpyAsync(list.data(), t_list.p, nbig * sizeof(int), hipMemcpyDeviceToHost, s));
+    MSH_HIP(hipMemcpyAsync(lr.data(), t_lr.p, nbig * sizeof(int4), hipMemcpyDeviceToHost, s));
+    MSH_HIP(hipStreamSynchronize(s));
+    // node order (the atomic list order is arbitrary), chunk items per node
+    std::vector<int> idx(nbig);
+    for (unsigned b = 0; b < nbig; ++b) idx[b] = (int)b;
+    std::sort(idx.begin(), idx.end(), [&](int x, int y) { return list[x] < list[y]; });
+    std::vector<int> slist(nbig), off(nbig + 1, 0);
+    std::vector<int4> slr(nbig);
+    std::vector<int2> items;
+    for (unsigned j = 0; j < nbig; ++j) {
+        slist[j] = list[idx[j]];
+        slr[j] = lr[idx[j]];
+        const int n = slr[j].y - slr[j].x + 1;
+        const int nch = (n + kObbChunk - 1) / kObbChunk;
+        for (int c = 0; c < nch; ++c) items.push_back(make_int2((int)j, c));
+        off[j + 1] = (int)items.size();
+    }
+    const size_t ni = items.size();
+    // a degenerate (caterpillar-like) tree has O(T^2 / kObbChunk) items: leave its big nodes to k_obb_wave
+    if (ni > ((size_t)1 << 22)) return MSH_OK;
+    MSH_HIP(hipMalloc(&t_items.p, ni * sizeof(int2)));
+    MSH_HIP(hipMalloc(&t_off.p, (nbig + 1) * sizeof(int)));
+    MSH_HIP(hipMalloc(&t_part.p, ni * 4 * sizeof(double)));
+    MSH_HIP(hipMalloc(&t_frames.p, nbig * sizeof(ObbFrame)));
+    MSH_HIP(hipMalloc(&t_ext.p, ni * 12 * sizeof(double)));
+    MSH_HIP(hipMemcpyAsync(t_list.p, slist.data(), nbig * sizeof(int), hipMemcpyHostToDevice, s));
+    MSH_HIP(hipMemcpyAsync(t_lr.p, slr.data(), nbig * sizeof(int4), hipMemcpyHostToDevice, s));
+    MSH_HIP(hipMemcpyAsync(t_items.p, items.data(), ni * sizeof(int2), hipMemcpyHostToDevice, s));
+    MSH_HIP(hipMemcpyAsync(t_off.p, off.data(), (nbig + 1) * sizeof(int), hipMemcpyHostToDevice, s));
+    const int* d_list = static_cast<const int*>(t_list.p);
+    const int4* d_lr = static_cast<const int4*>(t_lr.p);
+    const int2* d_items = static_cast<const int2*>(t_items.p);
+    const int* d_off = static_cast<const int*>(t_off.p);
+    double* d_part = static_cast<double*>(t_part.p);
+    ObbFrame* d_frames = static_cast<ObbFrame*>(t_frames.p);
+    double* d_ext = static_cast<double*>(t_ext.p);
+    const unsigned nb = (nbig + kBlock - 1) / kBlock;
+    if (triangles) {
+        k_big_area<true><<<(unsigned)ni, kBlock, 0, s>>>(tree->d_leaves, d_lr, d_items, d_part);
+    } else {
+        k_big_area<false><<<(unsigned)ni, kBlock, 0, s>>>(tree->d_leaves, d_lr, d_items, d_part);
+    }
+    k_big_frame<<<nb, kBlock, 0, s>>>((int)nbig, d_off, d_part, d_frames);
+    if (triangles) {
+        k_big_extent<true><<<(unsigned)ni, kBlock, 0, s>>>(tree->d_leaves, d_list, d_lr, d_items, d_frames, npm,
+                                                          tree->d_orgs, d_ext);
+    } else {
+        k_big_extent<false><<<(unsigned)ni, kBlock, 0, s>>>(tree->d_leaves, d_list, d_lr, d_items, d_frames, npm,
+                                                           tree->d_orgs, d_ext);
+    }
+    k_big_encode<<<nb, kBlock, 0, s>>>((int)nbig, d_list, d_off, d_frames, d_ext, tree->d_nodes);
+    MSH_HIP(hipGetLastError());
+    MSH_HIP(hipStreamSynchronize(s));  // the temporaries are freed on return
+    maxr = kObbBig;
+    return MSH_OK;
+}
+
 int build_obb(msh_tree* tree, bool triangles) {
     if (tree->T < 2) return MSH_OK;
     const int nn = (int)(tree->B * (tree->T - 1));
@@ -496,12 +750,18 @@ int build_obb(msh_tree* tree, bool triangles) {
     const int4* ranges = tree->ws.ranges.as<int4>();
     const int npm = (int)(tree->T - 1);  // internal nodes per mesh
     const unsigned lane_blocks = (unsigned)(((size_t)nn + kBlock - 1) / kBlock);
+    int maxr = 0x7fffffff;
     if (triangles) {
         k_obb_lane<true><<<lane_blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
-        k_obb_wave<true><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
     } else {
         k_obb_lane<false><<<lane_blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
-        k_obb_wave<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
+    }
+    MSH_HIP(hipGetLastError());
+    MSH_TRY(build_obb_big(tree, triangles, ranges, nn, npm, s, maxr));
+    if (triangles) {
+        k_obb_wave<true><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs, maxr);
+    } else {
+        k_obb_wave<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs, maxr);
     }
     MSH_HIP(hipGetLastError());
     return MSH_OK;

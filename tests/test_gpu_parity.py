@@ -430,12 +430,14 @@ def test_device_api_matches_host_api():
     assert np.array_equal(dpt.cpu().numpy(), pt)
 
 
-@pytest.mark.parametrize("name", ["ico", "c2", "offset"])
+@pytest.mark.parametrize("name", ["ico", "ico60", "c2", "offset"])
 def test_tree_bounds_contain_primitives(name):
     # every child's quantised oriented box (frame n, t, n x t) contains all vertices below it
     from scripts.check_tree import check_mesh
     if name == "ico":
         v, f = W.geodesic_icosphere(20)
+    elif name == "ico60":  # 72,000 faces: several levels of nodes over kObbBig leaves, up to 71 chunks each
+        v, f = W.geodesic_icosphere(60)
     elif name == "c2":
         v, f = W.c2_mesh()
     else:
