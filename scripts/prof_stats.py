@@ -7,6 +7,6 @@ import sys
 con = sqlite3.connect(sys.argv[1])
 with open(sys.argv[2], "w", newline="") as fh:
     w = csv.writer(fh)
-    w.writerow(["name", "calls", "total_ns", "average_ns", "percentage"])
+    w.writerow(["name", "calls", "total_us", "average_us", "percentage"])  # rocpd top_kernels durations are in us
     for row in con.execute("select name, total_calls, total_duration, average, percentage from top_kernels"):
         w.writerow(row)
