@@ -59,7 +59,7 @@ typedef struct msh_tree_info {
     uint64_t n_meshes;   /* meshes in a batched tree (msh_batch_build), 1 otherwise */
     uint32_t node_bytes; /* bytes of one internal node as stored in HBM (one traversal step reads it) */
     uint32_t leaf_bytes; /* bytes of one leaf record (triangle: 9 x f64 + face id; point: 3 x f64 + id) */
-    int32_t max_depth;   /* deepest leaf below the root */
+    int32_t max_depth;   /* upper bound of the deepest leaf below the root (sizes traversal stacks) */
 } msh_tree_info;
 
 /* Layout of a packed tree blob (msh_tree_blob_*), readable on the host without a device. */

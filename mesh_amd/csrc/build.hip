@@ -9,7 +9,7 @@
 //   5. k_karras                        Karras (HPG 2012) internal-node emission; codes made unique by
 //                                      augmenting them with the sorted position; also records each
 //                                      node's contiguous leaf range and split
-//   6. k_depth                         max leaf depth (sizes the traversal stack spill)
+//   6. (in k_karras)                   a bound of the leaf depth from the prefix lengths (sizes the stack spill)
 //   7. (after leaf packing) k_obb_lane / k_obb_wave   one lane (<= 32 leaves) or one wave per node over
 //                                      its Morton leaf range: area-weighted
 //                                      normal -> node frame (n, t, b = n x t), then both children's vertex
@@ -179,11 +179,10 @@ __device__ inline int lbvh_delta(const uint32_t* __restrict__ k, int n, int i, i
 // global (internal >= 0, leaf = ~global leaf).  parent[c]: (parent << 1) | side for internal c in
 // [0, B(n-1)) and global leaf l at B(n-1) + l.  ranges[g] = (first leaf, last leaf, split gamma, 0),
 // global leaf positions: the left child covers [first, gamma].
-__global__ __launch_bounds__(kBlock) void k_karras(const uint32_t* __restrict__ all_keys, int B, int n,
-                                                   BNode* __restrict__ nodes, uint32_t* __restrict__ parent,
-                                                   int4* __restrict__ ranges) {
-    const long long gi = (long long)blockIdx.x * kBlock + threadIdx.x;
-    if (gi >= (long long)B * (n - 1)) return;
+// node gi of k_karras; returns its depth bound delta(node) - delta(root) + 1
+__device__ inline unsigned karras_node(const uint32_t* __restrict__ all_keys, int B, int n, long long gi,
+                                       BNode* __restrict__ nodes, uint32_t* __restrict__ parent,
+                                       int4* __restrict__ ranges) {
     const int mb = (int)(gi / (n - 1)), i = (int)(gi - (long long)mb * (n - 1));
     const uint32_t* keys = all_keys + (size_t)mb * n;
     const int nb = mb * (n - 1), lb = mb * n;  // node / leaf base of this mesh
@@ -212,7 +211,24 @@ __global__ __launch_bounds__(kBlock) void k_karras(const uint32_t* __restrict__ 
     const size_t leaf0 = (size_t)B * (n - 1);
     parent[left >= 0 ? (size_t)left : leaf0 + ~left] = ((uint32_t)g << 1) | 0u;
     parent[right >= 0 ? (size_t)right : leaf0 + ~right] = ((uint32_t)g << 1) | 1u;
+    return (unsigned)(dnode - lbvh_delta(keys, n, 0, n - 1) + 1);
 }
+
+// depth_bound: every step down a Karras tree lengthens the common key prefix (delta) by at least one bit,
+// so a leaf below node x lies at most delta(x) - delta(root) + 1 internal nodes deep; the maximum of
+// that over the nodes bounds the tree depth (it sizes the traversal stacks' spill areas) without walking
+// every leaf to its root (C4: 7.3 ms of dependent parent loads for 41M leaves).
+__global__ __launch_bounds__(kBlock) void k_karras(const uint32_t* __restrict__ all_keys, int B, int n,
+                                                   BNode* __restrict__ nodes, uint32_t* __restrict__ parent,
+                                                   int4* __restrict__ ranges, unsigned* __restrict__ depth_bound) {
+    const long long gi = (long long)blockIdx.x * kBlock + threadIdx.x;
+    unsigned dep = 0;
+    if (gi < (long long)B * (n - 1)) dep = karras_node(all_keys, B, n, gi, nodes, parent, ranges);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) dep = max(dep, (unsigned)__shfl_xor((int)dep, o, 64));
+    if ((threadIdx.x & 63) == 0 && dep > 0) atomicMax(depth_bound, dep);
+}
+
 
 __device__ inline float down1(float x) { return nextafterf(x, -INFINITY); }
 __device__ inline float up1(float x) { return nextafterf(x, INFINITY); }
@@ -220,25 +236,6 @@ __device__ inline float out_lo(double x) { return down1(__double2float_rd(x)); }
 __device__ inline float out_hi(double x) { return up1(__double2float_ru(x)); }
 
 // depth of every leaf (root's children = 1); out = max
-__global__ __launch_bounds__(kBlock) void k_depth(const uint32_t* __restrict__ parent, int B, int n,
-                                                  unsigned* __restrict__ out) {
-    const long long leaf = (long long)blockIdx.x * kBlock + threadIdx.x;
-    unsigned d = 0;
-    if (leaf < (long long)B * n) {
-        const uint32_t root = (uint32_t)((leaf / n) * (n - 1));
-        d = 1;
-        uint32_t p = parent[(size_t)B * (n - 1) + leaf];
-        while ((p >> 1) != root && d < 4096u) {
-            p = parent[p >> 1];
-            ++d;
-        }
-    }
-    // one atomic per wave: 41M same-address atomics (C4) took 7.3 ms
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) d = max(d, (unsigned)__shfl_xor((int)d, o, 64));
-    if ((threadIdx.x & 63) == 0 && d > 0) atomicMax(out, d);
-}
-
 // ---- oriented boxes: one wave per internal node ----
 __device__ inline double wsum(double x) {
 #pragma unroll
@@ -831,13 +828,11 @@ int build_lbvh(msh_tree* tree, const double* d_lo, const double* d_hi, size_t T,
     MSH_TRY(ws.vals.reserve((2 * T - 1) * sizeof(uint32_t)));
     MSH_TRY(ws.ranges.reserve((T - 1) * sizeof(int4)));
     uint32_t* parent = ws.vals.as<uint32_t>();
-    k_karras<<<nblocks(T - 1), kBlock, 0, s>>>(keys, 1, (int)T, tree->d_nodes, parent, ws.ranges.as<int4>());
-    MSH_HIP(hipGetLastError());
     // node bounds come from k_obb (build_obb), after the leaves are packed
     uint32_t* flags = ws.flags.as<uint32_t>();
     unsigned* d_depth = flags + T;
     MSH_HIP(hipMemsetAsync(d_depth, 0, sizeof(unsigned), s));
-    k_depth<<<nblocks(T), kBlock, 0, s>>>(parent, 1, (int)T, d_depth);
+    k_karras<<<nblocks(T - 1), kBlock, 0, s>>>(keys, 1, (int)T, tree->d_nodes, parent, ws.ranges.as<int4>(), d_depth);
     MSH_HIP(hipGetLastError());
     unsigned depth = 0;
     MSH_HIP(hipMemcpyAsync(&depth, d_depth, sizeof(unsigned), hipMemcpyDeviceToHost, s));
@@ -900,13 +895,11 @@ int build_lbvh_batch(msh_tree* tree, const double* d_lo, const double* d_hi, siz
     MSH_TRY(ws.vals.reserve((nn + n) * sizeof(uint32_t)));
     MSH_TRY(ws.ranges.reserve(nn * sizeof(int4)));
     uint32_t* parent = ws.vals.as<uint32_t>();
-    k_karras<<<nblocks(nn), kBlock, 0, s>>>(keys, (int)B, (int)T, tree->d_nodes, parent, ws.ranges.as<int4>());
-    MSH_HIP(hipGetLastError());
     MSH_TRY(ws.flags.reserve(nn * sizeof(uint32_t) + 64));
     uint32_t* flags = ws.flags.as<uint32_t>();
     unsigned* d_depth = flags + nn;
     MSH_HIP(hipMemsetAsync(d_depth, 0, sizeof(unsigned), s));
-    k_depth<<<nblocks(n), kBlock, 0, s>>>(parent, (int)B, (int)T, d_depth);
+    k_karras<<<nblocks(nn), kBlock, 0, s>>>(keys, (int)B, (int)T, tree->d_nodes, parent, ws.ranges.as<int4>(), d_depth);
     MSH_HIP(hipGetLastError());
     unsigned depth = 0;
     MSH_HIP(hipMemcpyAsync(&depth, d_depth, sizeof(unsigned), hipMemcpyDeviceToHost, s));

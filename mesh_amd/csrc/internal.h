@@ -114,7 +114,7 @@ struct msh_tree {
     hipStream_t s_up = nullptr, s_down = nullptr;
     hipEvent_t e_up[2] = {nullptr, nullptr}, e_run[2] = {nullptr, nullptr}, e_down[2] = {nullptr, nullptr};
     double build_ms = 0.0;
-    int max_depth = 0;             // deepest leaf (root children = 1)
+    int max_depth = 0;             // bound of the deepest leaf (root children = 1): k_karras prefix lengths
     msh::Workspace ws;
 };
 
