@@ -367,6 +367,86 @@ __device__ inline void encode_node(BNode* node, const ObbFrame& fr, const float 
     *reinterpret_cast<float4*>(f + 12) = make_float4(__uint_as_float(w[1]), __uint_as_float(w[2]), h[14], h[15]);
 }
 
+// ---- area prefix sums: a node's frame needs the area-weighted normal sum over its Morton leaf range,
+// which is P[last + 1] - P[first] for the exclusive prefix P of the leaves' (area vector, |area|) in
+// leaf order — one O(T) scan instead of a pass over every node's range (O(T log T) leaf reads).  The scan
+// is two-level with a fixed association (deterministic); the differences lose ~1e-16 |P| to
+// cancellation, far below what the fp32 frame keeps.
+constexpr int kScanPer = 8;                      // leaves per thread
+constexpr int kScanBlock = kBlock * kScanPer;    // leaves per block
+__device__ inline double4 d4add(const double4& a, const double4& b) {
+    return make_double4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+// exclusive block scan of one double4 per thread (fixed order: wave inclusive shuffles, then wave totals)
+__device__ inline double4 block_exscan(double4 v, double4* sh, double4& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double4 inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const double4 u = make_double4(__shfl_up(inc.x, o, 64), __shfl_up(inc.y, o, 64), __shfl_up(inc.z, o, 64),
+                                       __shfl_up(inc.w, o, 64));
+        if (lane >= o) inc = d4add(inc, u);
+    }
+    if (lane == 63) sh[w] = inc;
+    __syncthreads();
+    double4 off = make_double4(0, 0, 0, 0);
+    for (int k = 0; k < w; ++k) off = d4add(off, sh[k]);
+    total = d4add(d4add(d4add(sh[0], sh[1]), sh[2]), sh[3]);
+    __syncthreads();
+    return d4add(off, make_double4(inc.x - v.x, inc.y - v.y, inc.z - v.z, inc.w - v.w));
+}
+template <bool TRI>
+__device__ inline double4 leaf_area4(const void* leaves, int i) {
+    const D3 a = leaf_area<TRI>(leaves, i);
+    return make_double4(a.x, a.y, a.z, sqrt(vdot(a, a)));
+}
+// block-local inclusive prefixes P[i + 1] of the block's leaves, and the block total
+template <bool TRI>
+__global__ __launch_bounds__(kBlock) void k_area_scan(const void* __restrict__ leaves, int n, double4* __restrict__ P,
+                                                      double4* __restrict__ btot) {
+    __shared__ double4 sh[4];
+    const int base = blockIdx.x * kScanBlock + threadIdx.x * kScanPer;
+    double4 loc[kScanPer];
+    double4 run = make_double4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k) {
+        const int i = base + k;
+        if (i < n) run = d4add(run, leaf_area4<TRI>(leaves, i));
+        loc[k] = run;
+    }
+    double4 total;
+    const double4 off = block_exscan(run, sh, total);
+#pragma unroll
+    for (int k = 0; k < kScanPer; ++k)
+        if (base + k < n) P[base + k + 1] = d4add(off, loc[k]);
+    if (threadIdx.x == 0) btot[blockIdx.x] = total;
+}
+// exclusive scan of the block totals in place (one block, each thread a contiguous run)
+__global__ __launch_bounds__(kBlock) void k_area_scan_tops(double4* __restrict__ btot, int nb) {
+    __shared__ double4 sh[4];
+    const int per = (nb + kBlock - 1) / kBlock, b0 = threadIdx.x * per, b1 = min(nb, b0 + per);
+    double4 run = make_double4(0, 0, 0, 0);
+    for (int b = b0; b < b1; ++b) run = d4add(run, btot[b]);
+    double4 total;
+    double4 off = block_exscan(run, sh, total);
+    for (int b = b0; b < b1; ++b) {
+        const double4 t = btot[b];
+        btot[b] = off;
+        off = d4add(off, t);
+    }
+}
+__global__ __launch_bounds__(kBlock) void k_area_scan_add(double4* __restrict__ P, int n, const double4* __restrict__ btot) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i == 0) P[0] = make_double4(0, 0, 0, 0);
+    if (i >= n) return;
+    P[i + 1] = d4add(btot[i / kScanBlock], P[i + 1]);
+}
+// the frame of the leaf range [first, last]
+__device__ inline ObbFrame range_frame(const double4* __restrict__ P, int first, int last) {
+    const double4 a = P[last + 1], b = P[first];
+    return obb_frame(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+}
+
 constexpr int kObbLane = 32;    // nodes over at most this many leaves: one lane each; up to kObbBig: one wave each
 #ifndef MSH_OBB_BIG
 #define MSH_OBB_BIG 4096
@@ -378,20 +458,14 @@ constexpr int kObbChunk = 1024;
 template <bool TRI>
 __global__ __launch_bounds__(kBlock) void k_obb_lane(const void* __restrict__ leaves, const int4* __restrict__ ranges,
                                                      int nn, int npm, BNode* __restrict__ nodes,
-                                                     const double* __restrict__ orgs) {
+                                                     const double* __restrict__ orgs, const double4* __restrict__ P) {
     const int node = blockIdx.x * kBlock + threadIdx.x;
     if (node >= nn) return;
     const int4 r = ranges[node];
     if (r.y - r.x + 1 > kObbLane) return;
     const int mb = node / npm;  // mesh of the node (npm internal nodes per mesh)
     const double o[3] = {orgs[3 * mb], orgs[3 * mb + 1], orgs[3 * mb + 2]};
-    double sx = 0, sy = 0, sz = 0, sa = 0;
-    for (int i = r.x; i <= r.y; ++i) {
-        const D3 c = leaf_area<TRI>(leaves, i);
-        sx += c.x; sy += c.y; sz += c.z;
-        sa += sqrt(vdot(c, c));
-    }
-    const ObbFrame fr = obb_frame(sx, sy, sz, sa);
+    const ObbFrame fr = range_frame(P, r.x, r.y);
     float ext[2][6];
     for (int side = 0; side < 2; ++side) {
         double mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -409,7 +483,8 @@ __global__ __launch_bounds__(kBlock) void k_obb_lane(const void* __restrict__ le
 template <bool TRI>
 __global__ __launch_bounds__(kBlock) void k_obb_wave(const void* __restrict__ leaves, const int4* __restrict__ ranges,
                                                      int nn, int npm, BNode* __restrict__ nodes,
-                                                     const double* __restrict__ orgs, int maxr) {
+                                                     const double* __restrict__ orgs, int maxr,
+                                                     const double4* __restrict__ P) {
     const int lane = threadIdx.x & 63;
     const int waves = gridDim.x * (kBlock / 64);
     for (int node = (blockIdx.x * kBlock + threadIdx.x) >> 6; node < nn; node += waves) {
@@ -417,13 +492,7 @@ __global__ __launch_bounds__(kBlock) void k_obb_wave(const void* __restrict__ le
         if (r.y - r.x + 1 <= kObbLane || r.y - r.x + 1 > maxr) continue;
         const int mb = node / npm;
         const double o[3] = {orgs[3 * mb], orgs[3 * mb + 1], orgs[3 * mb + 2]};
-        double sx = 0, sy = 0, sz = 0, sa = 0;
-        for (int i = r.x + lane; i <= r.y; i += 64) {
-            const D3 c = leaf_area<TRI>(leaves, i);
-            sx += c.x; sy += c.y; sz += c.z;
-            sa += sqrt(vdot(c, c));
-        }
-        const ObbFrame fr = obb_frame(wsum(sx), wsum(sy), wsum(sz), wsum(sa));
+        const ObbFrame fr = range_frame(P, r.x, r.y);
         float ext[2][6];
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
@@ -488,45 +557,12 @@ __device__ inline double block_max(double x, double* sh) {
     return fmax(fmax(sh[0], sh[1]), fmax(sh[2], sh[3]));
 }
 
-// item = (big node b, chunk c): partial area sum of the chunk's leaves
-template <bool TRI>
-__global__ __launch_bounds__(kBlock) void k_big_area(const void* __restrict__ leaves, const int4* __restrict__ lr,
-                                                     const int2* __restrict__ items, double* __restrict__ part) {
-    __shared__ double sh[4];
-    const int2 it = items[blockIdx.x];
-    const int4 r = lr[it.x];
-    const int b = r.x + it.y * kObbChunk, e = min(r.y, b + kObbChunk - 1);
-    double sx = 0, sy = 0, sz = 0, sa = 0;
-    for (int i = b + (int)threadIdx.x; i <= e; i += kBlock) {
-        const D3 c = leaf_area<TRI>(leaves, i);
-        sx += c.x; sy += c.y; sz += c.z;
-        sa += sqrt(vdot(c, c));
-    }
-    sx = block_sum(sx, sh);
-    sy = block_sum(sy, sh);
-    sz = block_sum(sz, sh);
-    sa = block_sum(sa, sh);
-    if (threadIdx.x == 0) {
-        part[4 * blockIdx.x] = sx;
-        part[4 * blockIdx.x + 1] = sy;
-        part[4 * blockIdx.x + 2] = sz;
-        part[4 * blockIdx.x + 3] = sa;
-    }
-}
-
-// one thread per big node: the frame from its chunks' area sums, in chunk order
-__global__ __launch_bounds__(kBlock) void k_big_frame(int nbig, const int* __restrict__ off, const double* __restrict__ part,
+// one thread per big node: its frame
+__global__ __launch_bounds__(kBlock) void k_big_frame(int nbig, const int4* __restrict__ lr, const double4* __restrict__ P,
                                                       ObbFrame* __restrict__ frames) {
     const int b = blockIdx.x * kBlock + threadIdx.x;
     if (b >= nbig) return;
-    double sx = 0, sy = 0, sz = 0, sa = 0;
-    for (int k = off[b]; k < off[b + 1]; ++k) {
-        sx += part[4 * k];
-        sy += part[4 * k + 1];
-        sz += part[4 * k + 2];
-        sa += part[4 * k + 3];
-    }
-    frames[b] = obb_frame(sx, sy, sz, sa);
+    frames[b] = range_frame(P, lr[b].x, lr[b].y);
 }
 
 // partial extents of a chunk on its node's frame, per side of the node's split: ext[item][side][lo k, hi k]
@@ -656,14 +692,14 @@ int pack_point_leaves(const double* d_v, const uint32_t* d_order, size_t P, PtRe
 // nodes over more than kObbBig leaves (k_big_*): list them, cut their ranges into chunks (host-side item
 // map, a few thousand entries), then partial sums / frames / partial extents / encode
 static int build_obb_big(msh_tree* tree, bool triangles, const int4* ranges, int nn, int npm, hipStream_t s,
-                         int& maxr) {
+                         int& maxr, const double4* P) {
     // meshes of up to 4 kObbBig faces: their largest nodes are short work for one wave, and the list /
     // item set-up (a few allocations and host round trips) would cost more (C2: 1.7 -> 2.5 ms)
     if (tree->T <= 4 * (size_t)kObbBig) return MSH_OK;
     struct Tmp {
         void* p = nullptr;
         ~Tmp() { if (p) (void)hipFree(p); }
-    } t_list, t_lr, t_cnt, t_items, t_off, t_part, t_frames, t_ext;
+    } t_list, t_lr, t_cnt, t_items, t_off, t_frames, t_ext;
     const unsigned nblk = (unsigned)(((size_t)nn + kBlock - 1) / kBlock);
     MSH_HIP(hipMalloc(&t_cnt.p, sizeof(unsigned)));
     MSH_HIP(hipMemsetAsync(t_cnt.p, 0, sizeof(unsigned), s));
@@ -704,7 +740,6 @@ static int build_obb_big(msh_tree* tree, bool triangles, const int4* ranges, int
     if (ni > ((size_t)1 << 22)) return MSH_OK;
     MSH_HIP(hipMalloc(&t_items.p, ni * sizeof(int2)));
     MSH_HIP(hipMalloc(&t_off.p, (nbig + 1) * sizeof(int)));
-    MSH_HIP(hipMalloc(&t_part.p, ni * 4 * sizeof(double)));
     MSH_HIP(hipMalloc(&t_frames.p, nbig * sizeof(ObbFrame)));
     MSH_HIP(hipMalloc(&t_ext.p, ni * 12 * sizeof(double)));
     MSH_HIP(hipMemcpyAsync(t_list.p, slist.data(), nbig * sizeof(int), hipMemcpyHostToDevice, s));
@@ -715,16 +750,10 @@ static int build_obb_big(msh_tree* tree, bool triangles, const int4* ranges, int
     const int4* d_lr = static_cast<const int4*>(t_lr.p);
     const int2* d_items = static_cast<const int2*>(t_items.p);
     const int* d_off = static_cast<const int*>(t_off.p);
-    double* d_part = static_cast<double*>(t_part.p);
     ObbFrame* d_frames = static_cast<ObbFrame*>(t_frames.p);
     double* d_ext = static_cast<double*>(t_ext.p);
     const unsigned nb = (nbig + kBlock - 1) / kBlock;
-    if (triangles) {
-        k_big_area<true><<<(unsigned)ni, kBlock, 0, s>>>(tree->d_leaves, d_lr, d_items, d_part);
-    } else {
-        k_big_area<false><<<(unsigned)ni, kBlock, 0, s>>>(tree->d_leaves, d_lr, d_items, d_part);
-    }
-    k_big_frame<<<nb, kBlock, 0, s>>>((int)nbig, d_off, d_part, d_frames);
+    k_big_frame<<<nb, kBlock, 0, s>>>((int)nbig, d_lr, P, d_frames);
     if (triangles) {
         k_big_extent<true><<<(unsigned)ni, kBlock, 0, s>>>(tree->d_leaves, d_list, d_lr, d_items, d_frames, npm,
                                                           tree->d_orgs, d_ext);
@@ -742,25 +771,42 @@ static int build_obb_big(msh_tree* tree, bool triangles, const int4* ranges, int
 int build_obb(msh_tree* tree, bool triangles) {
     if (tree->T < 2) return MSH_OK;
     const int nn = (int)(tree->B * (tree->T - 1));
+    const int nl = (int)(tree->B * tree->T);
     const unsigned blocks = (unsigned)std::min<size_t>(((size_t)nn + 3) / 4, 65536);
     hipStream_t s = tree->stream;
     const int4* ranges = tree->ws.ranges.as<int4>();
     const int npm = (int)(tree->T - 1);  // internal nodes per mesh
     const unsigned lane_blocks = (unsigned)(((size_t)nn + kBlock - 1) / kBlock);
+    // area prefix sums over all leaves (batched trees: the meshes' leaf ranges are disjoint)
+    struct Tmp {
+        void* p = nullptr;
+        ~Tmp() { if (p) (void)hipFree(p); }
+    } t_P, t_tot;
+    const int nsb = (nl + kScanBlock - 1) / kScanBlock;
+    MSH_HIP(hipMalloc(&t_P.p, ((size_t)nl + 1) * sizeof(double4)));
+    MSH_HIP(hipMalloc(&t_tot.p, (size_t)nsb * sizeof(double4)));
+    double4* P = static_cast<double4*>(t_P.p);
+    double4* tot = static_cast<double4*>(t_tot.p);
+    if (triangles) k_area_scan<true><<<(unsigned)nsb, kBlock, 0, s>>>(tree->d_leaves, nl, P, tot);
+    else k_area_scan<false><<<(unsigned)nsb, kBlock, 0, s>>>(tree->d_leaves, nl, P, tot);
+    k_area_scan_tops<<<1, kBlock, 0, s>>>(tot, nsb);
+    k_area_scan_add<<<(unsigned)(((size_t)nl + kBlock - 1) / kBlock), kBlock, 0, s>>>(P, nl, tot);
+    MSH_HIP(hipGetLastError());
     int maxr = 0x7fffffff;
     if (triangles) {
-        k_obb_lane<true><<<lane_blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
+        k_obb_lane<true><<<lane_blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs, P);
     } else {
-        k_obb_lane<false><<<lane_blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs);
+        k_obb_lane<false><<<lane_blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs, P);
     }
     MSH_HIP(hipGetLastError());
-    MSH_TRY(build_obb_big(tree, triangles, ranges, nn, npm, s, maxr));
+    MSH_TRY(build_obb_big(tree, triangles, ranges, nn, npm, s, maxr, P));
     if (triangles) {
-        k_obb_wave<true><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs, maxr);
+        k_obb_wave<true><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs, maxr, P);
     } else {
-        k_obb_wave<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs, maxr);
+        k_obb_wave<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs, maxr, P);
     }
     MSH_HIP(hipGetLastError());
+    MSH_HIP(hipStreamSynchronize(s));  // P is freed on return
     return MSH_OK;
 }
 
