@@ -428,6 +428,12 @@ static_assert(kLeafQ >= 2 && kLeafQ <= 4, "kLeafQ must be 2, 3 or 4");
 #ifndef MSH_LEAD2
 #define MSH_LEAD2 256
 #endif
+#ifndef MSH_FWIN
+#define MSH_FWIN 64  // followers take their bound from the leaders of their MSH_FWIN-slot window
+#endif
+#ifndef MSH_LWIN
+#define MSH_LWIN 8   // leaders take theirs from the MSH_LWIN super-leaders of their window (4: -1.1 %)
+#endif
 // second level: one super-leader per kLead2 slots (0: off), run first and unhinted; the other leaders
 // then start from the bound of the 4 super-leaders of their 4 * kLead2-slot window
 constexpr unsigned kLead2 = MSH_LEAD2;
@@ -512,7 +518,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         double hint = INFINITY;
         if constexpr (MODE == 0 || MODE == 3) {
             if (a.phase == 2 || (a.phase == 1 && kLead2 > 0)) {
-                hint = a.phase == 2 ? hint_from_leaders(a, i, q, 64, kLead) : hint_from_leaders(a, i, q, 4 * kLead2, kLead2);
+                hint = a.phase == 2 ? hint_from_leaders(a, i, q, MSH_FWIN, kLead) : hint_from_leaders(a, i, q, MSH_LWIN * kLead2, kLead2);
                 pol.shared = hint;
                 pol.relim();
             }
