@@ -833,12 +833,26 @@ __global__ __launch_bounds__(kBlock) void k_query_morton(const double* __restric
     vals[i] = (uint32_t)i;
 }
 
+#ifndef MSH_QBOX_MARGIN
+#define MSH_QBOX_MARGIN 0.1f
+#endif
+constexpr float kQueryBoxMargin = MSH_QBOX_MARGIN;
 int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* keys, uint32_t* vals, hipStream_t s) {
     if (S == 0) return MSH_OK;
     TimedLaunch tl("morton", s);
-    k_query_morton<<<(unsigned)((S + kBlock - 1) / kBlock), kBlock, 0, s>>>(
-        d_q, S, tree->scene_lo[0], tree->scene_lo[1], tree->scene_lo[2], tree->scene_hi[0], tree->scene_hi[1],
-        tree->scene_hi[2], keys, vals);
+    // The cells span the scene box widened by 10 % of its extent on each side: queries just outside the
+    // mesh box (scan points, a query box a little larger than the mesh) keep their spatial order instead of
+    // being clamped onto the boundary cells in the caller's order (C3: 25 % of the queries lie outside
+    // the unit sphere's box; 1143 -> 1154-1158 M q/s for 5-20 % margins; a reduction over the queries to
+    // fit the box exactly cost 0.9 ms and gained nothing net)
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        const float e = tree->scene_hi[k] - tree->scene_lo[k];
+        lo[k] = tree->scene_lo[k] - kQueryBoxMargin * e;
+        hi[k] = tree->scene_hi[k] + kQueryBoxMargin * e;
+    }
+    k_query_morton<<<(unsigned)((S + kBlock - 1) / kBlock), kBlock, 0, s>>>(d_q, S, lo[0], lo[1], lo[2], hi[0], hi[1],
+                                                                           hi[2], keys, vals);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }
