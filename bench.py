@@ -4,8 +4,12 @@ Workload: class-I geodesic icosphere, frequency 224 = 1,003,520
 vertices; every GPU answers its own shard of 100M queries uniform in [-1.1, 1.1]^3 (seed 3 + rank),
 generated directly in HBM.  One step = one pass of the hot path over one batch resident in HBM:
 query Morton codes -> LDS radix sort -> LBVH traversal with fp64 CGAL-construction refinement ->
-results scattered back to query order (face u32, part u32, point 3 x f64).  The BVH build is setup
-(reported as build_ms); for N > 1 it is built on rank 0 and replicated with one RCCL broadcast.
+results scattered back to query order (face u32, part u32, point 3 x f64), and for N > 1 the all-gather
+of every rank's (face, part, point) slab into the whole answer on every rank (SURVEY §8(d)'s primary
+metric; RCCL over xGMI, each batch's gather overlapped with the next batch's traversal by a
+double-buffered ResultRing, every gather finished inside the timed region).  `value_without_allgather`
+repeats the steps without the exchange.  The BVH build is setup (reported as build_ms); for N > 1 it is
+built on rank 0 and replicated with one RCCL broadcast.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--queries Q]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -97,18 +101,23 @@ def cpu_baseline(v, f, budget_s):
             obj("all", "OpenMP over queries on %d host threads" % out["all"][2]))
 
 
-def load_traffic(workload, S):
+def load_traffic(workload, S, build_id):
     """profiles/pmc_traffic.json (scripts/pmc_summary.py): PMC HBM bytes per launch of the traversal
-    kernels for this workload, or None when no profile of this workload exists."""
+    kernels, and the latency-side counters of the same session.  Returned only when it was measured on
+    this workload AND on the kernels of the loaded library (its build_id, msh_build_id: a hash of the
+    sources) — otherwise (None, reason), so a profile of other code is never paired with this timing."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(p) as fh:
             d = json.load(fh)
-        if d.get("workload") == workload and int(d.get("queries")) == S:
-            return d
-    except (OSError, ValueError, TypeError):
-        pass
-    return None
+    except (OSError, ValueError) as e:
+        return None, "no PMC profile (%s)" % type(e).__name__
+    if d.get("workload") != workload or int(d.get("queries") or 0) != S:
+        return None, "PMC profile is of another workload"
+    if d.get("build_id") != build_id:
+        return None, "PMC profile is of build %s (code %s), not of the loaded build %s" % (
+            d.get("build_id"), d.get("code"), build_id)
+    return d, None
 
 
 def main():
@@ -128,7 +137,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from mesh_amd import _native, spatialsearch
-    from mesh_amd.distributed import gather_results, nearest_device, replicate_tree
+    from mesh_amd.distributed import nearest_device, replicate_tree
     import workloads as W
 
     _native.set_device(local)
@@ -155,31 +164,56 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(3 + rank)
     q = (torch.rand((S, 3), generator=g, dtype=torch.float64, device=dev) * 2.2 - 1.1).contiguous()
-    face = torch.empty(S, dtype=torch.int32, device=dev)
-    part = torch.empty(S, dtype=torch.int32, device=dev)
-    pt = torch.empty((S, 3), dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    slabs = [(torch.empty(S, dtype=torch.int32, device=dev), torch.empty(S, dtype=torch.int32, device=dev),
+              torch.empty((S, 3), dtype=torch.float64, device=dev)) for _ in range(2 if world > 1 else 1)]
+    ring = None
+    if world > 1:
+        from mesh_amd.distributed import ResultRing
+        gathered = (torch.empty(world * S, dtype=torch.int32, device=dev),
+                    torch.empty(world * S, dtype=torch.int32, device=dev),
+                    torch.empty((world * S, 3), dtype=torch.float64, device=dev))
+        ring = ResultRing(slabs, gathered)
 
-    def step():
-        nearest_device(tree, q, face, part, pt, stream=stream)
+    def answer(slab):
+        nearest_device(tree, q, slab[0], slab[1], slab[2], stream=stream)
+
+    def step():  # one batch: the query pipeline, and for N > 1 the all-gather of its results
+        if ring is None:
+            answer(slabs[0])
+        else:
+            ring.step(answer)
+
+    def timed(run, steps):
+        """barrier + sync, `steps` calls of run (every gather drained), sync + barrier; max over ranks"""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            run()
+        if ring is not None:
+            ring.drain()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
     for _ in range(args.warmup):
         step()
+    if ring is not None:
+        ring.drain()
     torch.cuda.synchronize()
 
-    # ---- timed region ----
+    # ---- timed region: K steps (N > 1: each with its result all-gather) ----
     _native.timing_reset()
     _native.timing_enable(True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(step, args.steps)
     _native.timing_enable(False)
     k_ms, k_n = _native.timing_get("nearest")
     p1_ms, p1_n = _native.timing_get("knn_pass1")
@@ -191,27 +225,9 @@ def main():
     m_ms, m_n = _native.timing_get("morton")
     g_ms, g_n = _native.timing_get("gather")
     u_ms, u_n = _native.timing_get("unpermute")
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
-    # ---- N > 1: the same steps followed by the result all-gather of SURVEY §8(d)'s primary metric ----
-    elapsed_ag = None
-    if world > 1:
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-            gather_results(face, S * world)
-            gather_results(part, S * world)
-            gather_results(pt, S * world)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed_ag = float(t.item())
+    # ---- N > 1: the same steps without the exchange (reported beside value, never as value) ----
+    elapsed_no_ag = timed(lambda: answer(slabs[0]), args.steps) if world > 1 else None
 
     # ---- instrumented traversal (untimed): algorithmic bytes ----
     nodes, leaves = _native.ctypes.c_uint64(0), _native.ctypes.c_uint64(0)
@@ -234,7 +250,8 @@ def main():
     avg_kernel_s = (k_ms / max(k_n, 1)) / 1e3
     achieved = S * bytes_per_query / avg_kernel_s / 1e9
     achieved_s8d = S * bytes_per_query_s8d / avg_kernel_s / 1e9
-    tr = load_traffic(workload, S)
+    build_id = _native.build_id()
+    tr, tr_reason = load_traffic(workload, S, build_id)
     traffic = tr.get("bytes_per_launch") if tr else None
     total_q = S * world * args.steps
     out = {
@@ -261,7 +278,17 @@ def main():
                      "s8d_64B_nodes": {"bytes_per_query": bytes_per_query_s8d, "achieved": achieved_s8d,
                                        "frac": achieved_s8d / HBM_PEAK_GBS},
                      "measured": ({"hbm_GBps": tr["bytes_per_launch"] / avg_kernel_s / 1e9,
-                                   "l2_hit_rate": tr.get("l2_hit_rate"), "code": tr.get("code")} if tr else None)},
+                                   "l2_hit_rate": tr.get("l2_hit_rate"), "code": tr.get("code"),
+                                   "build_id": tr.get("build_id"), "pmc_traversal_ms": tr.get("traversal_ms")}
+                                  if tr else None),
+                     "traffic_note": tr_reason,
+                     # latency side: what bounds the kernel (node steps issued per second, live; lane
+                     # occupancy and memory waits from the same build's SQ counters)
+                     "latency": {"node_steps_per_s": S * n_node / avg_kernel_s,
+                                 "leaf_tests_per_s": S * n_leaf / avg_kernel_s,
+                                 "lanes_active_valu": tr.get("lanes_active_valu") if tr else None,
+                                 "wave_cycles_waiting_frac": tr.get("wave_cycles_waiting_frac") if tr else None,
+                                 "wave_cycles_valu_frac": tr.get("wave_cycles_valu_frac") if tr else None}},
         "breakdown_ms_per_step": {"traversal": k_ms / max(k_n, 1), "pass1": p1_ms / max(p1_n, 1),
                                   "pass1_superleaders": sl_ms / max(sl_n, 1),
                                   "pass1_leaders": ld_ms / max(ld_n, 1), "pass1_followers": fl_ms / max(fl_n, 1),
@@ -269,11 +296,13 @@ def main():
                                   "morton": m_ms / max(m_n, 1), "gather": g_ms / max(g_n, 1),
                                   "unpermute": u_ms / max(u_n, 1)},
         "build_ms": build_ms,
+        "build_id": build_id,
         "bvh_broadcast_ms": bcast_ms,
     }
-    if elapsed_ag is not None:
-        out["value_with_allgather"] = total_q / elapsed_ag
-        out["ms_per_step_with_allgather"] = elapsed_ag / args.steps * 1e3
+    if elapsed_no_ag is not None:
+        out["value_without_allgather"] = total_q / elapsed_no_ag
+        out["ms_per_step_without_allgather"] = elapsed_no_ag / args.steps * 1e3
+        out["allgather_bytes_per_step"] = world * S * 32  # (face u32, part u32, point 3 x f64) of every rank
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"], out["cpu_baseline_allcores"] = cpu_baseline(v, f, args.cpu_seconds)
     print(json.dumps(out), flush=True)

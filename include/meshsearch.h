@@ -74,6 +74,10 @@ typedef struct msh_blob_info {
 /* ---- library / device ---- */
 const char* msh_last_error(void);
 int msh_version(void);
+/* Identity of the built kernels: the first 16 hex digits of the SHA-256 of mesh_amd/csrc's sources (and any
+ * extra compile flags).  Profiles are keyed by it, so a measurement is only ever paired with the code it
+ * measured (bench.py roofline.traffic). */
+const char* msh_build_id(void);
 int msh_device_count(int* n);
 /* Device used by subsequent builds on the calling thread (default: current HIP device). */
 int msh_set_device(int device);
@@ -158,7 +162,8 @@ int msh_visibility_device(msh_tree* tree, const double* d_cams, size_t C, const 
 /* Mesh.estimate_vertex_normals (mesh.py:208-216): per vertex, the sum in ascending face order of the
  * faces' cross products (v1 - v0) x (v2 - v0) (tri_normals.py:23-24), divided by its norm (0 -> 1). */
 int msh_vertex_normals(const double* v, size_t P, const uint32_t* f, size_t T, double* vn);
-/* device pointers; returns when the result is in d_vn (stream may be NULL) */
+/* device pointers; returns when the result is in d_vn (stream may be NULL).  A face index >= P is
+ * detected on the device: MSH_EINVAL, d_vn unspecified, no out-of-bounds access. */
 int msh_vertex_normals_device(const double* d_v, size_t P, const uint32_t* d_f, size_t T, double* d_vn, void* stream);
 
 /* ---- batched trees: scan-to-mesh registration over many meshes (BASELINE configs[3], C4) ----

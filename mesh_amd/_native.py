@@ -30,6 +30,7 @@ _lock = threading.Lock()
 SIGNATURES = [
     ("msh_last_error", ctypes.c_char_p, []),
     ("msh_version", _i, []),
+    ("msh_build_id", ctypes.c_char_p, []),
     ("msh_device_count", _i, [ctypes.POINTER(_i)]),
     ("msh_set_device", _i, [_i]),
     ("msh_tree_build", _i, [_c_double_p, _sz, _c_u32_p, _sz, ctypes.POINTER(_vp)]),
@@ -186,6 +187,26 @@ class Handle(object):
 
     def __repr__(self):
         return "<meshsearch tree kind=%s at 0x%x>" % (self.kind, self.ptr or 0)
+
+
+def build_id():
+    """Identity of the loaded libmeshsearch.so's kernels (msh_build_id): SHA-256 prefix of its sources."""
+    return lib().msh_build_id().decode()
+
+
+def source_build_id(extra=""):
+    """The build identity the current mesh_amd/csrc sources would get (the Makefile's SRC_HASH)."""
+    import hashlib
+    import os
+    csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+    names = sorted(["sort.hip", "build.hip", "nearest.hip", "rays.hip", "tritri.hip", "geometry.hip", "api.cpp",
+                    "loaders.cpp", "common.h", "internal.h"])
+    h = hashlib.sha256()
+    for p in [os.path.join(csrc, n) for n in names] + [os.path.join(csrc, "..", "..", "include", "meshsearch.h")]:
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    h.update(extra.encode())
+    return h.hexdigest()[:16]
 
 
 def device_count():

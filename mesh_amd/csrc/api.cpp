@@ -160,6 +160,7 @@ static void free_tree(msh_tree* t) {
     if (t->d_boxes) (void)hipFree(t->d_boxes);
     if (t->d_leaves) (void)hipFree(t->d_leaves);
     if (t->d_vorder) (void)hipFree(t->d_vorder);
+    if (t->d_vorder_shard) (void)hipFree(t->d_vorder_shard);
     for (int b = 0; b < 2; ++b) {
         if (t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
         if (t->d_stage[b]) (void)hipFree(t->d_stage[b]);
@@ -550,6 +551,11 @@ extern "C" {
 const char* msh_last_error(void) { return g_err.c_str(); }
 
 int msh_version(void) { return 2; }
+
+#ifndef MSH_SRC_HASH
+#define MSH_SRC_HASH "unknown"
+#endif
+const char* msh_build_id(void) { return MSH_SRC_HASH; }
 
 int msh_device_count(int* n) {
     int c = 0;
@@ -1052,12 +1058,21 @@ int msh_vertex_normals_device(const double* d_v, size_t P, const uint32_t* d_f, 
     MSH_TRY(use_device(dev));
     hipStream_t s = static_cast<hipStream_t>(stream);
     Workspace ws;
-    int st = vertex_normals(d_v, P, d_f, T, d_vn, ws, s);
+    int st = ws.flags.reserve(sizeof(uint32_t));
+    uint32_t h_err = 0;
+    if (st == MSH_OK && hipMemsetAsync(ws.flags.ptr, 0, sizeof(uint32_t), s) != hipSuccess) st = MSH_EDEVICE;
+    if (st == MSH_OK) st = vertex_normals(d_v, P, d_f, T, d_vn, ws, s, ws.flags.as<uint32_t>());
+    if (st == MSH_OK && hipMemcpyAsync(&h_err, ws.flags.ptr, sizeof(uint32_t), hipMemcpyDeviceToHost, s) != hipSuccess)
+        st = MSH_EDEVICE;
     hipError_t e = hipStreamSynchronize(s);  // the scratch below is released on return
     ws.release();
     if (st == MSH_OK && e != hipSuccess) {
         set_error("vertex normals: %s", hipGetErrorString(e));
         st = MSH_EDEVICE;
+    }
+    if (st == MSH_OK && h_err) {
+        set_error("msh_vertex_normals_device: face index out of range (>= %zu vertices)", P);
+        st = MSH_EINVAL;
     }
     return st;
 }

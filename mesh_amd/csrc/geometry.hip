@@ -14,11 +14,19 @@
 
 namespace msh {
 
-__global__ __launch_bounds__(kBlock) void k_face_normals(const double* __restrict__ v, const uint32_t* __restrict__ f,
-                                                         size_t T, double* __restrict__ fn) {
+// Face indices are checked here (device callers hand over unchecked faces): a face with an index >= P
+// raises *err and contributes a zero normal instead of reading past v.
+__global__ __launch_bounds__(kBlock) void k_face_normals(const double* __restrict__ v, size_t P,
+                                                         const uint32_t* __restrict__ f, size_t T,
+                                                         double* __restrict__ fn, uint32_t* __restrict__ err) {
     const size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x;
     if (t >= T) return;
     const size_t i0 = f[3 * t], i1 = f[3 * t + 1], i2 = f[3 * t + 2];
+    if (i0 >= P || i1 >= P || i2 >= P) {
+        *err = 1u;
+        fn[3 * t] = fn[3 * t + 1] = fn[3 * t + 2] = 0.0;
+        return;
+    }
     const D3 a = D3{v[3 * i0], v[3 * i0 + 1], v[3 * i0 + 2]};
     const D3 b = D3{v[3 * i1], v[3 * i1 + 1], v[3 * i1 + 2]};
     const D3 c = D3{v[3 * i2], v[3 * i2 + 1], v[3 * i2 + 2]};
@@ -28,20 +36,22 @@ __global__ __launch_bounds__(kBlock) void k_face_normals(const double* __restric
     fn[3 * t + 2] = n.z;
 }
 
-// keys = vertex of corner e (f flattened), vals = e
-__global__ __launch_bounds__(kBlock) void k_corner_keys(const uint32_t* __restrict__ f, size_t n, uint32_t* __restrict__ keys,
-                                                        uint32_t* __restrict__ vals) {
+// keys = vertex of corner e (f flattened; an index >= P becomes P, which sorts last), vals = e
+__global__ __launch_bounds__(kBlock) void k_corner_keys(const uint32_t* __restrict__ f, size_t n, size_t P,
+                                                        uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
     if (e >= n) return;
-    keys[e] = f[e];
+    keys[e] = f[e] < P ? f[e] : (uint32_t)P;
     vals[e] = (uint32_t)e;
 }
 
-__global__ __launch_bounds__(kBlock) void k_vertex_ranges(const uint32_t* __restrict__ keys, size_t n,
+// sorted corner keys == P (out-of-range faces, flagged by k_face_normals) sort last and are skipped
+__global__ __launch_bounds__(kBlock) void k_vertex_ranges(const uint32_t* __restrict__ keys, size_t n, size_t P,
                                                           uint32_t* __restrict__ first, uint32_t* __restrict__ end) {
     const size_t p = (size_t)blockIdx.x * kBlock + threadIdx.x;
     if (p >= n) return;
     const uint32_t k = keys[p];
+    if (k >= P) return;
     if (p == 0 || keys[p - 1] != k) first[k] = (uint32_t)p;
     if (p + 1 == n || keys[p + 1] != k) end[k] = (uint32_t)(p + 1);
 }
@@ -68,7 +78,7 @@ __global__ __launch_bounds__(kBlock) void k_vertex_sum(const double* __restrict_
 static unsigned nblk(size_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 int vertex_normals(const double* d_v, size_t P, const uint32_t* d_f, size_t T, double* d_vn, Workspace& ws,
-                   hipStream_t s) {
+                   hipStream_t s, uint32_t* d_err) {
     if (P == 0) return MSH_OK;
     const size_t n = 3 * T;
     if (n > 0xFFFFFFFFull) {
@@ -87,15 +97,15 @@ int vertex_normals(const double* d_v, size_t P, const uint32_t* d_f, size_t T, d
     uint32_t* end = first + P;
     MSH_HIP(hipMemsetAsync(first, 0, 2 * P * sizeof(uint32_t), s));
     if (T) {
-        k_face_normals<<<nblk(T), kBlock, 0, s>>>(d_v, d_f, T, fn);
+        k_face_normals<<<nblk(T), kBlock, 0, s>>>(d_v, P, d_f, T, fn, d_err);
         MSH_HIP(hipGetLastError());
-        k_corner_keys<<<nblk(n), kBlock, 0, s>>>(d_f, n, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>());
+        k_corner_keys<<<nblk(n), kBlock, 0, s>>>(d_f, n, P, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>());
         MSH_HIP(hipGetLastError());
-        int bits = 1;
-        while (bits < 32 && ((size_t)1 << bits) < P) ++bits;
+        int bits = 1;  // keys are <= P (P marks an out-of-range index)
+        while (bits < 32 && ((size_t)1 << bits) <= P) ++bits;
         MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
                                  ws.vals_alt.as<uint32_t>(), n, bits, ws, s));
-        k_vertex_ranges<<<nblk(n), kBlock, 0, s>>>(ws.keys.as<uint32_t>(), n, first, end);
+        k_vertex_ranges<<<nblk(n), kBlock, 0, s>>>(ws.keys.as<uint32_t>(), n, P, first, end);
         MSH_HIP(hipGetLastError());
     }
     k_vertex_sum<<<nblk(P), kBlock, 0, s>>>(fn, ws.vals.as<uint32_t>(), first, end, P, d_vn);

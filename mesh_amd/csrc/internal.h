@@ -104,6 +104,8 @@ struct msh_tree {
     double* d_orgs = nullptr;      // (B,3) per-mesh origins on the device (B = 1: a copy of origin)
     double* d_boxes = nullptr;     // (B,6) per-mesh boxes (batched trees: query Morton codes)
     uint32_t* d_vorder = nullptr;  // Morton order of the main vertices (lazily built for visibility)
+    uint32_t* d_vorder_shard = nullptr;  // Morton order of vertices [vshard_v0, +vshard_nv) (last shard asked for)
+    size_t vshard_v0 = 0, vshard_nv = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ws_done = nullptr;  // recorded after the last launch that used `ws` (stream ordering)
     // host-call staging (lazily created, grow-only): two pinned host slabs, two device slabs, copy
@@ -201,8 +203,9 @@ int launch_tri_intersect(const msh_tree* tree, const TriRec* d_qtris, size_t Tq,
 // ---- mesh geometry (geometry.hip) ----
 // area-weighted vertex normals of (P,3) v over (T,3) f: sum of the faces' cross products in ascending
 // face order per vertex, normalised (mesh.py:208-216)
+// d_err (device u32, zeroed by the caller) is set when a face index is >= P (those faces are ignored)
 int vertex_normals(const double* d_v, size_t P, const uint32_t* d_f, size_t T, double* d_vn, Workspace& ws,
-                   hipStream_t s);
+                   hipStream_t s, uint32_t* d_err);
 
 // ---- timing ----
 struct TimedLaunch {

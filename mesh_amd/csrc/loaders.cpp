@@ -36,6 +36,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
+#include <new>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -122,20 +125,37 @@ struct msh_ply {
 
 using msh::set_error;
 
-extern "C" {
+namespace {
 
-int msh_obj_load(const char* path, msh_obj** out) {
-    if (!path || !out) {
-        set_error("msh_obj_load: null argument");
+// Runs a loader body so that no C++ exception crosses the extern "C" boundary: an allocation failure
+// becomes MSH_ENOMEM, anything else MSH_EINVAL, each with a message (the Python shim raises the module's
+// error for both).
+template <class F>
+int guarded(const char* what, F&& body) {
+    try {
+        return body();
+    } catch (const std::bad_alloc&) {
+        set_error("%s: out of memory", what);
+        return MSH_ENOMEM;
+    } catch (const std::length_error&) {
+        set_error("%s: sizes too large", what);
+        return MSH_ENOMEM;
+    } catch (const std::exception& e) {
+        set_error("%s: %s", what, e.what());
+        return MSH_EINVAL;
+    } catch (...) {
+        set_error("%s: unknown error", what);
         return MSH_EINVAL;
     }
-    *out = nullptr;
+}
+
+int obj_load(const char* path, msh_obj** out) {
     Mapped m;
     if (!m.open(path)) {
         set_error("Could not load file");
         return MSH_EINVAL;
     }
-    msh_obj* o = new msh_obj();
+    std::unique_ptr<msh_obj> o(new msh_obj());
     o->v.reserve(30000);
     o->f.reserve(100000);
     bool next_v_is_land = false;
@@ -216,8 +236,21 @@ int msh_obj_load(const char* path, msh_obj** out) {
         }
         p = nl ? nl + 1 : end;
     }
-    *out = o;
+    *out = o.release();
     return MSH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int msh_obj_load(const char* path, msh_obj** out) {
+    if (!path || !out) {
+        set_error("msh_obj_load: null argument");
+        return MSH_EINVAL;
+    }
+    *out = nullptr;
+    return guarded("msh_obj_load", [&] { return obj_load(path, out); });
 }
 
 int msh_obj_sizes(const msh_obj* o, uint64_t* s) {
@@ -369,16 +402,16 @@ struct Reader {
     }
 };
 
-}  // namespace
+// Fewest bytes one instance of `el` can occupy in the body (binary: the scalar sizes plus each list's
+// count; ascii: one character and one separator per value, a list at least its count), never below 1, so
+// an element count that the bytes after end_header cannot hold is refused before anything is allocated.
+size_t min_elem_bytes(const Elem& el, int mode) {
+    size_t b = 0;
+    for (const auto& pr : el.props) b += mode == 0 ? 2 : psize(pr.list ? pr.count : pr.item);
+    return b ? b : 1;
+}
 
-extern "C" {
-
-int msh_ply_load(const char* path, msh_ply** out) {
-    if (!path || !out) {
-        set_error("msh_ply_load: null argument");
-        return MSH_EINVAL;
-    }
-    *out = nullptr;
+int ply_load(const char* path, msh_ply** out) {
     Mapped m;
     if (!m.open(path) || m.n < 4 || std::memcmp(m.p, "ply\n", 4) != 0) {
         set_error("Failed to open PLY file.");
@@ -415,7 +448,10 @@ int msh_ply_load(const char* path, msh_ply** out) {
         } else if (w[0] == "element" && w.size() == 3) {
             Elem el;
             el.name = w[1];
-            el.n = strtol(w[2].c_str(), nullptr, 10);
+            char* e = nullptr;
+            errno = 0;
+            el.n = strtol(w[2].c_str(), &e, 10);
+            if (e == w[2].c_str() || *e || errno == ERANGE || el.n < 0) break;  // not a count: bad header
             elems.push_back(el);
         } else if (w[0] == "property" && !elems.empty()) {
             Prop pr;
@@ -441,7 +477,19 @@ int msh_ply_load(const char* path, msh_ply** out) {
         set_error("plyread_mex: Bad raw header.");
         return MSH_EINVAL;
     }
-    msh_ply* o = new msh_ply();
+    {
+        const size_t left = (size_t)(end - p) + (mode == 0 ? 1 : 0);  // ascii: the last value needs no separator
+        size_t need = 0;
+        for (const auto& el : elems) {
+            const size_t mb = min_elem_bytes(el, mode);
+            if ((size_t)el.n > left / mb || need > left - (size_t)el.n * mb) {
+                set_error("Read failed. %s: element '%s' count %ld exceeds the file", path, el.name.c_str(), el.n);
+                return MSH_EINVAL;
+            }
+            need += (size_t)el.n * mb;
+        }
+    }
+    std::unique_ptr<msh_ply> o(new msh_ply());
     // which vertex properties exist (plyutils.c has_color / has_normals)
     auto find = [&](const std::string& e) -> Elem* {
         for (auto& x : elems)
@@ -510,12 +558,24 @@ int msh_ply_load(const char* path, msh_ply** out) {
         if (!r.ok) break;
     }
     if (!r.ok) {
-        delete o;
         set_error("Read failed. %s", path);
         return MSH_EINVAL;
     }
-    *out = o;
+    *out = o.release();
     return MSH_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int msh_ply_load(const char* path, msh_ply** out) {
+    if (!path || !out) {
+        set_error("msh_ply_load: null argument");
+        return MSH_EINVAL;
+    }
+    *out = nullptr;
+    return guarded("msh_ply_load", [&] { return ply_load(path, out); });
 }
 
 int msh_ply_sizes(const msh_ply* o, uint64_t* s) {

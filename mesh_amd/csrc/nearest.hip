@@ -4,12 +4,13 @@
 // (K8, search.ClosestPointTree) and the barycentric variant (K9: nearest + Heidrich weights of the
 // closest point, mesh.py:218-222 / geometry/barycentric_coordinates_of_projection.py:9-49).
 //
-// Query pipeline (S >= kSortMin queries):
-//   k_query_morton -> radix sort (sort.hip) -> k_gather_queries: the query rows are copied ONCE into
-//   Morton (slot) order, coalesced, and the inverse permutation is recorded.  The traversal kernels
-//   read slot-order queries and write one 32-B slot-order record per query (coalesced), and
-//   k_unpermute moves the records back to query order (coalesced writes, one 32-B gathered read).
-//   Below kSortMin the kernels read and write the caller's arrays directly.
+// Query pipeline (sorted launches):
+//   k_query_morton -> radix sort (sort.hip) -> the closest-point traversal reads query row perm[i] for slot
+//   i straight from the caller's array and stores its answer straight to the caller's row perm[i] (face,
+//   part, point: scattered 4 + 4 + 24-B stores); only the leader phases also write a 32-B slot-order
+//   record, because followers take their hints from them.  The ray, normals-metric and point-tree paths
+//   gather the rows into slot order (k_gather_rows) and restore the caller's order from slot-order records
+//   (k_unpermute).  Unsorted launches read and write the caller's arrays directly.
 //
 // Execution shape (gfx950):
 //   Pass 1 (k_knn): persistent grid; each WAVE dequeues 64-query tiles from one of 8 XCD-group
@@ -25,9 +26,11 @@
 //     A lane that exceeds `budget` node steps stops and appends its query (with its exact best so far)
 //     to a deferred list: queries near the centre of a closed surface are equidistant from most of it
 //     and would otherwise hold their whole wave for ~10^6 steps.
-//   Pass 2 (k_knn_coop): one WAVE per deferred query.  The wave expands the top of the tree
-//     breadth-first into <= 512 subtrees (LDS frontier), deals them to its 64 lanes, and every lane walks
-//     its subtrees depth-first while the wave shares the best bound after every step (wave min).
+//   Pass 2 (k_knn_coop): one WAVE per deferred query, dealt from an atomic counter.  The wave walks a
+//     last-in-first-out list of subtrees in LDS, 64 entries at a time (one per lane): children within the
+//     bound are pushed back (compacted by ballot), leaf children are tested on the spot, and the wave
+//     shares the best bound (wave min) after every round.  A list that would outgrow LDS is dealt to the
+//     lanes' own stacks for depth-first walks.
 // Ties: the lexicographic minimum of (squared distance, face index) — deterministic and independent of
 // traversal order or of how the work was split (every box within best*(1+2^-40) is visited).
 #include <algorithm>
@@ -242,9 +245,9 @@ struct Walker {
         }
         return false;
     }
-    // Visit `node`: bound its two children (max of the fp32 AABB and oriented-box lower bounds), test
-    // leaf children, descend into the nearer internal child and push the farther one.  Returns false
-    // when the traversal is complete.
+    // Visit `node`: bound its two children by their fp32 oriented boxes (node_child_bounds), test leaf
+    // children, descend into the nearer internal child and push the farther one.  Returns false when the
+    // traversal is complete.
     template <class Pol, bool STATS>
     __device__ inline bool step(const BNode* __restrict__ nodes, const QF& qf, Pol& pol, uint2* __restrict__ lds,
                                 uint2* __restrict__ spill, unsigned& n_nodes, unsigned& n_leaves) {

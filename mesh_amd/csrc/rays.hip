@@ -399,17 +399,18 @@ int launch_alongnormal(const msh_tree* tree, const QueryOrder& ord, size_t S, co
     return launch_rays<0, false>(t, a, S, s, "alongnormal");
 }
 
-// Morton order of the main-mesh vertices in the scene box (cached on the handle: visibility sources)
-__global__ __launch_bounds__(kBlock) void k_vertex_morton(const double* __restrict__ v, size_t P, float lx, float ly,
-                                                          float lz, float hx, float hy, float hz,
+// Morton order of main-mesh vertices [v0, v0 + n) in the scene box (visibility sources): keys of vertex
+// v0 + i and values v0 + i (global indices)
+__global__ __launch_bounds__(kBlock) void k_vertex_morton(const double* __restrict__ v, size_t v0, size_t n, float lx,
+                                                          float ly, float lz, float hx, float hy, float hz,
                                                           uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= P) return;
+    if (i >= n) return;
     const float e[3] = {hx - lx, hy - ly, hz - lz}, l[3] = {lx, ly, lz};
     uint32_t c[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-        float x = e[k] > 0.f ? ((float)v[3 * i + k] - l[k]) / e[k] : 0.5f;
+        float x = e[k] > 0.f ? ((float)v[3 * (v0 + i) + k] - l[k]) / e[k] : 0.5f;
         x = fminf(fmaxf(x * 1024.f, 0.f), 1023.f);
         uint32_t b = (uint32_t)x;
         b = (b * 0x00010001u) & 0xFF0000FFu;
@@ -419,23 +420,55 @@ __global__ __launch_bounds__(kBlock) void k_vertex_morton(const double* __restri
         c[k] = b;
     }
     keys[i] = (c[0] << 2) | (c[1] << 1) | c[2];
-    vals[i] = (uint32_t)i;
+    vals[i] = (uint32_t)(v0 + i);
 }
 
-static int vertex_order(msh_tree* t, hipStream_t s) {
-    if (t->d_vorder || t->P < 4096) return MSH_OK;
+// Morton order of the vertex range [v0, v0 + nv), cached on the handle: the whole mesh in d_vorder, the
+// last vertex shard asked for (visibility_sharded: one range per rank) in d_vorder_shard.  A shard's order
+// is the whole mesh's order restricted to the shard (the same keys, a stable sort), so a shard's rays run
+// as coherently as the whole mesh's.  The buffer is published on the handle only after the sort has been
+// enqueued successfully (a failed build leaves no half-initialised order behind).
+static int vertex_order(msh_tree* t, size_t v0, size_t nv, const uint32_t** order, hipStream_t s) {
+    *order = nullptr;
+    if (nv < 4096) return MSH_OK;  // small ranges: caller order
+    const bool whole = v0 == 0 && nv == t->P;
+    if (whole && t->d_vorder) { *order = t->d_vorder; return MSH_OK; }
+    if (!whole && t->d_vorder_shard && t->vshard_v0 == v0 && t->vshard_nv == nv) {
+        *order = t->d_vorder_shard;
+        return MSH_OK;
+    }
     Workspace& ws = t->ws;
-    const size_t P = t->P;
-    MSH_TRY(ws.keys.reserve(P * sizeof(uint32_t)));
-    MSH_TRY(ws.keys_alt.reserve(P * sizeof(uint32_t)));
-    MSH_TRY(ws.vals_alt.reserve(P * sizeof(uint32_t)));
-    MSH_HIP(hipMalloc(&t->d_vorder, P * sizeof(uint32_t)));
-    k_vertex_morton<<<(unsigned)((P + kBlock - 1) / kBlock), kBlock, 0, s>>>(
-        t->d_v, P, t->scene_lo[0], t->scene_lo[1], t->scene_lo[2], t->scene_hi[0], t->scene_hi[1], t->scene_hi[2],
-        ws.keys.as<uint32_t>(), t->d_vorder);
-    MSH_HIP(hipGetLastError());
-    return radix_sort_pairs(ws.keys.as<uint32_t>(), t->d_vorder, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(),
-                            P, 30, ws, s);
+    MSH_TRY(ws.keys.reserve(nv * sizeof(uint32_t)));
+    MSH_TRY(ws.keys_alt.reserve(nv * sizeof(uint32_t)));
+    MSH_TRY(ws.vals_alt.reserve(nv * sizeof(uint32_t)));
+    uint32_t* buf = nullptr;
+    MSH_HIP(hipMalloc(&buf, nv * sizeof(uint32_t)));
+    k_vertex_morton<<<(unsigned)((nv + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+        t->d_v, v0, nv, t->scene_lo[0], t->scene_lo[1], t->scene_lo[2], t->scene_hi[0], t->scene_hi[1],
+        t->scene_hi[2], ws.keys.as<uint32_t>(), buf);
+    int st = hipGetLastError() == hipSuccess ? MSH_OK : MSH_EDEVICE;
+    if (st == MSH_OK)
+        st = radix_sort_pairs(ws.keys.as<uint32_t>(), buf, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), nv,
+                              30, ws, s);
+    if (st != MSH_OK) {
+        if (st == MSH_EDEVICE) set_error("vertex Morton order: kernel launch failed");
+        (void)hipStreamSynchronize(s);  // the buffer may still be in use by enqueued work
+        (void)hipFree(buf);
+        return st;
+    }
+    if (whole) {
+        t->d_vorder = buf;
+    } else {
+        if (t->d_vorder_shard) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(t->d_vorder_shard);
+        }
+        t->d_vorder_shard = buf;
+        t->vshard_v0 = v0;
+        t->vshard_nv = nv;
+    }
+    *order = buf;
+    return MSH_OK;
 }
 
 int launch_visibility(const msh_tree* tree, const double* d_cams, size_t C, const double* d_normals,
@@ -448,10 +481,7 @@ int launch_visibility(const msh_tree* tree, const double* d_cams, size_t C, cons
     a.cams = d_cams; a.normals = d_normals; a.sensors = d_sensors;
     a.min_dist = min_dist; a.vis = d_vis; a.ndc = d_ndc;
     if (nv == 0 || C == 0) return MSH_OK;
-    if (v0 == 0 && nv == tree->P) {  // whole mesh: Morton-ordered sources
-        MSH_TRY(vertex_order(t, s));
-        a.vorder = t->d_vorder;
-    }
+    MSH_TRY(vertex_order(t, v0, nv, &a.vorder, s));  // Morton-ordered sources (whole mesh or shard)
     return launch_rays<1, false>(t, a, C * nv, s, "visibility");
 }
 
@@ -474,8 +504,7 @@ int launch_visibility_stats(const msh_tree* tree, const double* d_cams, size_t C
     a.cams = d_cams; a.min_dist = min_dist;
     a.stats = d_counts;
     if (C == 0 || tree->P == 0) return MSH_OK;
-    MSH_TRY(vertex_order(t, s));
-    a.vorder = t->d_vorder;
+    MSH_TRY(vertex_order(t, 0, tree->P, &a.vorder, s));
     return launch_rays<1, true>(t, a, C * tree->P, s, "visibility_stats");
 }
 

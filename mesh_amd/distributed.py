@@ -3,9 +3,11 @@ is RCCL on ROCm; xGMI between MI355X GPUs).
 
 The path partitions by query: every rank holds the same mesh + BVH and answers a contiguous shard of
 the queries.  The BVH is built once (on `src`) and replicated with ONE RCCL broadcast of its packed
-blob (mesh vertices + 128-B nodes + 80-B leaves), instead of every rank rebuilding it.  Results stay
-sharded in each rank's HBM; `gather_results` concatenates shards where a caller needs them in one
-place (one all_gather per output array, padded to the largest shard).
+blob (mesh vertices + the 64-B nodes + 80-B leaves; the sizes are in blob_info's node_bytes / leaf_bytes),
+instead of every rank rebuilding it.  Results stay sharded in each rank's HBM; `gather_results`
+concatenates shards where a caller needs them in one place (one all_gather per output array, padded to
+the largest shard); `gather_results_into` gathers equal shards straight into a preallocated tensor, and
+`ResultRing` overlaps each batch's gather with the next batch's traversal.
 """
 import numpy as np
 
@@ -94,6 +96,56 @@ def gather_results(local, total, group=None):
     bufs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(bufs, pad, group=group)
     return torch.cat([b[:c] for b, c in zip(bufs, counts)], 0)
+
+
+def gather_results_into(out, local, group=None, async_op=False):
+    """All-gather equal shards into a preallocated tensor: rank r's (n, ...) `local` lands in rows
+    [r n, (r + 1) n) of `out` (world n, ...) — one all_gather_into_tensor, no padding, no concatenation.
+    With async_op the work handle is returned: on RCCL the gather runs on the process group's stream after
+    the work already enqueued on the current stream, and handle.wait() makes the current stream wait for it."""
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    if out.shape[0] != world * local.shape[0] or tuple(out.shape[1:]) != tuple(local.shape[1:]):
+        raise ValueError("gather_results_into: out %s does not hold %d shards of %s"
+                         % (tuple(out.shape), world, tuple(local.shape)))
+    if out.dtype != local.dtype or not out.is_contiguous() or not local.is_contiguous():
+        raise ValueError("gather_results_into: dtype / contiguity mismatch")
+    return dist.all_gather_into_tensor(out, local, group=group, async_op=async_op)
+
+
+class ResultRing(object):
+    """Double-buffered result slabs of a stream of query batches on every rank, each batch's results
+    all-gathered into `gathered` (the whole answer on every rank, rank-major rows).  Batch k is answered into
+    slab k % 2 while the all-gather of batch k - 1 runs on the process group's stream (over xGMI on RCCL), so
+    the exchange overlaps the next traversal instead of following it; a slab is rewritten only after the
+    gather that read it has completed (its handle is waited on, on the current stream, first).
+
+    slabs: two tuples of local result tensors (e.g. face, part, point); gathered: a tuple of the matching
+    (world n, ...) tensors.  step(compute) calls compute(slab) to enqueue batch k's work on the current
+    stream, then starts its gathers; drain() waits for every gather still running."""
+
+    def __init__(self, slabs, gathered, group=None):
+        if len(slabs) != 2 or any(len(s) != len(gathered) for s in slabs):
+            raise ValueError("ResultRing: two slabs of %d tensors each" % len(gathered))
+        self.slabs, self.gathered, self.group = slabs, gathered, group
+        self.pending = [[], []]
+        self.k = 0
+
+    def step(self, compute):
+        b = self.k & 1
+        for w in self.pending[b]:
+            w.wait()
+        compute(self.slabs[b])
+        self.pending[b] = [gather_results_into(g, x, self.group, async_op=True)
+                           for g, x in zip(self.gathered, self.slabs[b])]
+        self.k += 1
+
+    def drain(self):
+        for b in (0, 1):
+            for w in self.pending[b]:
+                w.wait()
+            self.pending[b] = []
 
 
 def nearest_device(tree, q, face, part, pt, stream=None):

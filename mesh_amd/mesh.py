@@ -76,7 +76,7 @@ class Mesh(object):
         p = np.asarray(points, dtype=np.float64).reshape(-1, 3)
         n = np.cross(u, w)
         s = np.sum(n * n, axis=1)
-        s[s == 0] = 1e-16
+        s[s == 0] = np.spacing(1)  # barycentric_coordinates_of_projection.py:38-41
         oneOver4ASquared = 1.0 / s
         wp = p - a
         b2 = np.sum(np.cross(u, wp) * n, axis=1) * oneOver4ASquared
@@ -98,7 +98,8 @@ class Mesh(object):
         (a face's mean is (v0 + v1 + v2) / 3, as np.mean over its 3 rows), all centres go to the GPU in
         one closest-face query, and the faces are grouped per part with a stable sort (each part's
         list ascending, as the reference's sorted lists).  A face whose closest face of `mesh` is in no
-        part raises KeyError(''), as the reference's segm[''] lookup does."""
+        part belongs to the part named '' when `mesh` has one (parts_by_face maps such faces to ''), and
+        raises KeyError('') otherwise, as the reference's segm[''] lookup does."""
         self.segm = {}
         if not hasattr(mesh, 'segm'):
             return
@@ -112,7 +113,9 @@ class Mesh(object):
             part_of[np.asarray(mesh.segm[part], dtype=np.int64)] = k
         pid = part_of[np.asarray(closest_faces).ravel().astype(np.int64)]
         if (pid < 0).any():
-            raise KeyError('')
+            if '' not in names:
+                raise KeyError('')
+            pid[pid < 0] = names.index('')
         order = np.argsort(pid, kind='stable')
         bounds = np.searchsorted(pid[order], np.arange(len(names) + 1))
         self.segm = dict((part, order[bounds[k]:bounds[k + 1]].tolist()) for k, part in enumerate(names))

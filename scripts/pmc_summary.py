@@ -9,7 +9,10 @@ Reads gpurun_out/pmc/<pass>/**/*counter_collection.csv (one --pmc pass per count
                                L2 hit rate, and per-kernel counter means;
   profiles/<tag>_pmc.json    — every counter mean per kernel (all passes), for the record.
 
-    python scripts/pmc_summary.py --tag r02_c3_100M --code $(git rev-parse --short HEAD) [--queries 1e8]
+    python scripts/pmc_summary.py --tag r03_c3_100M --code $(git rev-parse --short HEAD) [--queries 1e8]
+
+The profiled library's build identity (msh_build_id, written to gpurun_out/pmc/build_id.txt on the box)
+is stored as build_id: bench.py reports roofline.traffic only for a library with that identity.
 """
 import argparse
 import csv
@@ -67,6 +70,9 @@ def main():
     ap.add_argument("--pmc", default=os.path.join(ROOT, "gpurun_out", "pmc"))
     ap.add_argument("--tag", required=True)
     ap.add_argument("--code", required=True, help="commit whose kernels were profiled")
+    ap.add_argument("--build-id", default=None,
+                    help="msh_build_id of the profiled library (default: gpurun_out/pmc/build_id.txt, written on "
+                         "the box by profile_pmc.sh)")
     ap.add_argument("--queries", type=float, default=1e8)
     ap.add_argument("--freq", type=int, default=224)
     args = ap.parse_args()
@@ -102,8 +108,23 @@ def main():
         tot_ns += ns
         kern[k] = {"counters_per_traversal": per, "hbm_bytes_per_traversal": b, "ms_per_traversal": ns / 1e6,
                    "hbm_GBps": (b / ns) if (b and ns) else None}
+    build_id = args.build_id
+    if build_id is None:
+        with open(os.path.join(args.pmc, "build_id.txt")) as fh:
+            build_id = fh.read().strip()
+    k0 = allc.get(TRAVERSAL[0], {})
+    per0 = {n: v / n_trav for n, v in k0.items() if not n.startswith("_")}
+
+    def ratio(a, b):
+        return per0[a] / per0[b] if per0.get(a) is not None and per0.get(b) else None
+
+    lanes = per0.get("SQ_THREAD_CYCLES_VALU"), per0.get("SQ_ACTIVE_INST_VALU")
     res = {
-        "workload": workload, "queries": S, "code": args.code,
+        "workload": workload, "queries": S, "code": args.code, "build_id": build_id,
+        # latency-side figures of the pass-1 kernel (k_knn<0,false>), same session
+        "lanes_active_valu": lanes[0] / (64.0 * lanes[1]) if all(lanes) else None,
+        "wave_cycles_waiting_frac": ratio("SQ_WAIT_ANY", "SQ_WAVE_CYCLES"),
+        "wave_cycles_valu_frac": ratio("SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES"),
         "units": "FETCH_SIZE / WRITE_SIZE in KB as rocprofv3 reports them; gfx950: bytes = "
                  "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md §HBM); TCC_HIT/MISS summed over "
                  "channels; every figure per traversal = pass-1 launches (leaders + followers) + pass 2",

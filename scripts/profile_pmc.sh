@@ -16,7 +16,9 @@ run() {
   [ $rc -eq 0 ] || exit $rc
 }
 : > "$OUT/status.txt"
-PASSES=${PASSES:-"stats fetch write tcc"}
+# identity of the library the passes measure (bench.py pairs profiles/pmc_traffic.json with it)
+(cd "$R" && python3 -c "from mesh_amd import _native; print(_native.build_id())") > "$OUT/build_id.txt" || exit 1
+PASSES=${PASSES:-"stats fetch write tcc sq"}
 for p in $PASSES; do
   case $p in
     stats) run stats --kernel-trace --stats ;;

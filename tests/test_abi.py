@@ -160,3 +160,11 @@ def test_batch_python_validation():
         AabbTreeBatch(np.zeros((4, 3)), f)
     with pytest.raises(ValueError, match="Tx3"):
         AabbTreeBatch(np.zeros((2, 4, 3)), np.zeros((2, 4), np.uint32))
+
+
+def test_build_id_matches_sources():
+    # the loaded library was built from the sources in the tree (profiles are keyed by this identity:
+    # profiles/pmc_traffic.json's build_id must equal it for bench.py to report roofline.traffic)
+    from mesh_amd import _native
+    bid = _native.build_id()
+    assert len(bid) == 16 and bid == _native.source_build_id()

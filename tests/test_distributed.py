@@ -154,3 +154,57 @@ def test_blob_and_shards_world2():
         wf[:, 0] = 0xFFFFFFFF
         assert r["face"].dtype == np.uint32 and (r["face"] == wf).all()
         assert (r["pt"] == np.arange(B, dtype=np.float64)[:, None, None]).all()
+
+
+# ---- the bench's N > 1 step: every batch's results all-gathered, overlapped with the next batch ----
+def _worker_ring(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mesh_amd.distributed import ResultRing, gather_results_into
+        n = 257
+        slabs = [(torch.empty(n, dtype=torch.int32), torch.empty((n, 3), dtype=torch.float64)) for _ in range(2)]
+        gathered = (torch.empty(world * n, dtype=torch.int32), torch.empty((world * n, 3), dtype=torch.float64))
+        ring = ResultRing(slabs, gathered)
+
+        def compute(k):
+            def run(slab):
+                face, pt = slab
+                face.copy_(torch.arange(n, dtype=torch.int32) + 1000 * rank + 100000 * k)
+                pt.copy_(face.to(torch.float64)[:, None] * torch.tensor([1.0, -1.0, 0.5], dtype=torch.float64))
+            return run
+
+        for k in range(5):  # batch k - 1's gather may still run while batch k is computed
+            ring.step(compute(k))
+        ring.drain()  # after draining, gathered holds the last batch
+        res = {"face": gathered[0].numpy().copy(), "pt": gathered[1].numpy().copy()}
+        # shape / dtype validation of the equal-shard gather
+        try:
+            gather_results_into(torch.empty(world * n + 1, dtype=torch.int32), slabs[0][0])
+            res["bad_shape_rejected"] = False
+        except ValueError:
+            res["bad_shape_rejected"] = True
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_result_ring_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_ring, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n, k = 257, 4
+    want = np.concatenate([np.arange(n) + 1000 * r + 100000 * k for r in range(world)]).astype(np.int32)
+    for _, r in res:
+        assert (r["face"] == want).all()
+        assert (r["pt"] == want[:, None].astype(np.float64) * np.array([1.0, -1.0, 0.5])).all()
+        assert r["bad_shape_rejected"]

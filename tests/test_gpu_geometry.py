@@ -24,7 +24,7 @@ def _device():
     _native.set_device(0)
 
 
-def _check_bary(oracle, v, f, q):
+def _check_bary(oracle, v, f, q, skip_faces=()):
     from mesh_amd import spatialsearch
     t = spatialsearch.aabbtree_compute(np.ascontiguousarray(v, np.float64), np.ascontiguousarray(f, np.uint32))
     face, pt, w = spatialsearch.aabbtree_nearest_barycentric(t, q)
@@ -36,10 +36,12 @@ def _check_bary(oracle, v, f, q):
     vi, bw = oracle.barycentric_coordinates_for_points(v, f, pt, face)
     assert np.array_equal(w, bw), np.abs(w - bw).max()
     # the point lies in its triangle: weights reconstruct it and are (nearly) a convex combination
-    rec = np.einsum("sk,skd->sd", w, v[vi.astype(np.int64)])
+    # (not for zero-area faces, whose Heidrich weights are (1, 0, 0) for any point)
+    keep = ~np.isin(face, np.asarray(skip_faces, np.uint32))
+    rec = np.einsum("sk,skd->sd", w[keep], v[vi[keep].astype(np.int64)])
     diag = float(np.linalg.norm(v.max(0) - v.min(0)))
-    assert np.abs(rec - pt).max() < 1e-9 * diag
-    assert w.min() > -1e-6 and abs(w.sum(1) - 1).max() < 1e-9
+    assert np.abs(rec - pt[keep]).max() < 1e-9 * diag
+    assert w[keep].min() > -1e-6 and abs(w[keep].sum(1) - 1).max() < 1e-9
     # the same faces/points as the plain nearest call
     f2, _, p2 = spatialsearch.aabbtree_nearest(t, q)
     assert np.array_equal(f2[0], face) and np.array_equal(p2, pt)
@@ -170,3 +172,75 @@ def test_transfer_segm(oracle, exclude):
     for k in want:
         assert tgt.segm[k] == want[k], k
     assert ("nothing" in tgt.segm) == (not exclude)
+
+
+def _degenerate_mesh():
+    # an icosphere plus zero-area faces: collinear vertices, a repeated vertex, and a tiny triangle whose
+    # n.n underflows to 0 although n != 0 (edges ~1e-85), so the s == 0 -> numpy.spacing(1) substitution
+    # of barycentric_coordinates_of_projection.py:38-41 decides the weights
+    v, f = W.geodesic_icosphere(6)
+    P = v.shape[0]
+    extra_v = np.array([[2.0, 0, 0], [2.5, 0, 0], [3.0, 0, 0],          # collinear
+                        [0, 2.0, 0], [0, 2.5, 0.5],                     # repeated vertex
+                        [0, 0, 2.0], [1e-85, 0, 2.0], [0, 1e-85, 2.0]])  # n.n underflows
+    extra_f = np.array([[P, P + 1, P + 2], [P + 3, P + 3, P + 4], [P + 5, P + 6, P + 7]], np.uint32)
+    return np.vstack([v, extra_v]), np.vstack([f, extra_f]).astype(np.uint32), P
+
+
+def test_barycentric_zero_area_faces(oracle):
+    from mesh_amd.mesh import Mesh
+    v, f, P = _degenerate_mesh()
+    T0 = f.shape[0] - 3
+    rng = np.random.default_rng(34)
+    q = np.vstack([rng.normal([2.5, 0, 0], 0.3, (3000, 3)), rng.normal([0, 2.2, 0.2], 0.2, (3000, 3)),
+                   rng.normal([0, 0, 2.0], 0.05, (3000, 3)), W.uniform_in_box([-1.1] * 3, [1.1] * 3, 3000, 35, 0)])
+    face, pt, w = _check_bary(oracle, v, f, q, skip_faces=[T0, T0 + 1, T0 + 2])
+    assert np.isin(face, [T0, T0 + 1, T0 + 2]).sum() > 1000  # the zero-area faces are really hit
+    # the facade (numpy) on the same faces and points, and on arbitrary points, where the tiny face's
+    # underflowed s matters (w = p - a is O(1), so (u x w).n does not underflow)
+    m = Mesh(v=v, f=f)
+    vi, coeff = m.barycentric_coordinates_for_points(pt, face)
+    assert np.array_equal(coeff, w)
+    faces = np.array([T0, T0 + 1, T0 + 2] * 5, np.uint32)
+    pts = rng.normal(0, 1, (faces.size, 3))
+    vi, coeff = m.barycentric_coordinates_for_points(pts, faces)
+    _, bw = oracle.barycentric_coordinates_for_points(v, f, pts, faces)
+    assert np.array_equal(coeff, bw)
+    assert np.abs(coeff[2::3, 1:]).max() > 0  # the tiny face's weights are not all zero
+
+
+def test_transfer_segm_empty_named_part(oracle):
+    # a part named '' (the OBJ reader makes one for a bare 'g' line): faces of `mesh` in no part map to it
+    # (parts_by_face gives them ''), as in the reference's loop (mesh.py:224-237); without it, KeyError('')
+    from mesh_amd.mesh import Mesh
+    v, f = W.geodesic_icosphere(8)
+    src = Mesh(v=v, f=f)
+    src.segm = {"a": list(range(0, 300)), "": list(range(300, 400))}  # faces >= 400 in no part
+    tv, tf = W.geodesic_icosphere(5)
+    tgt = Mesh(v=tv * 1.02, f=tf)
+    tgt.transfer_segm(src)
+    bf, _, _, _ = oracle.brute_nearest(v, f, oracle.face_centres(tv * 1.02, tf))
+    want = oracle.transfer_segm(tv * 1.02, tf, src.segm, bf)
+    assert tgt.segm == want and len(want[""]) > 0
+    del src.segm[""]
+    with pytest.raises(KeyError):
+        Mesh(v=tv * 1.02, f=tf).transfer_segm(src)
+
+
+def test_vertex_normals_device_bad_index():
+    # msh_vertex_normals_device gets device faces it cannot check on the host: an index >= P is found on the
+    # device and reported as MSH_EINVAL (no out-of-bounds read of v, no write past the range buffer)
+    import torch
+    from mesh_amd import _native as N
+    v, f = W.geodesic_icosphere(4)
+    f = f.copy()
+    f[5, 1] = v.shape[0] + 7
+    dv = torch.from_numpy(v).cuda()
+    df = torch.from_numpy(f.view(np.int32)).cuda()
+    dn = torch.empty_like(dv)
+    st = N.lib().msh_vertex_normals_device(dv.data_ptr(), v.shape[0], df.data_ptr(), f.shape[0], dn.data_ptr(), None)
+    assert st == N.MSH_EINVAL and b"out of range" in N.lib().msh_last_error()
+    f[5, 1] = 0  # a valid mesh on the same buffers still works
+    df.copy_(torch.from_numpy(f.view(np.int32)))
+    st = N.lib().msh_vertex_normals_device(dv.data_ptr(), v.shape[0], df.data_ptr(), f.shape[0], dn.data_ptr(), None)
+    assert st == 0

@@ -209,6 +209,24 @@ def test_ply_errors(tmp_path):
         plyutils.read(str(out_of_range))
 
 
+@pytest.mark.parametrize("count", [b"-1", b"99999999999", b"9223372036854775807", b"99999999999999999999", b"12x"])
+@pytest.mark.parametrize("fmt", ["ascii", "binary_little_endian"])
+def test_ply_bad_counts(tmp_path, fmt, count):
+    # element counts that are negative, unparsable or larger than the bytes after end_header can hold are
+    # refused with the module error before anything is allocated (no C++ exception escapes the C ABI)
+    body = _ply_file(fmt)
+    hdr, rest = body.split(b"end_header\n", 1)
+    lines = hdr.split(b"\n")
+    lines = [b"element vertex " + count if ln.startswith(b"element vertex") else ln for ln in lines]
+    p = tmp_path / "count.ply"
+    p.write_bytes(b"\n".join(lines) + b"end_header\n" + rest)
+    with pytest.raises(plyutils.error, match="Read failed|Bad raw header"):
+        plyutils.read(str(p))
+    ok = tmp_path / "ok.ply"  # the unmodified file still reads
+    ok.write_bytes(body)
+    plyutils.read(str(ok))
+
+
 @pytest.mark.parametrize("name", ["test_box.obj", "test_box.ply", "test_box_le.ply"])
 def test_mesh_from_file(ref_tests, name):
     # tests/test_mesh.py:35-47 through Mesh(filename=...)

@@ -264,3 +264,18 @@ def test_cgal_tree_visibility_vs_brute(oracle, ref_tests):
         return oracle.CgalVisibilityTree(v, f, extra_v, extra_f).visibility(cams, n=n, min_dist=min_dist)
 
     check_visibility_box(fn, t)
+
+
+def test_facade_barycentric_spacing_constant(oracle):
+    # Mesh.barycentric_coordinates_for_points (numpy facade) substitutes numpy.spacing(1) for s == 0, as
+    # barycentric_coordinates_of_projection.py:38-41 does: a triangle with edges ~1e-85 has n != 0 but
+    # n.n == 0, and its weights for an O(1) point depend on that constant
+    from mesh_amd.mesh import Mesh
+    v = np.array([[0, 0, 2.0], [1e-85, 0, 2.0], [0, 1e-85, 2.0], [1.0, 0, 0], [0, 1, 0], [0, 0, 1.0]])
+    f = np.array([[0, 1, 2], [3, 4, 5]], np.uint32)
+    pts = np.random.default_rng(36).normal(0, 1, (8, 3))
+    faces = np.array([0, 1] * 4, np.uint32)
+    vi, w = Mesh(v=v, f=f).barycentric_coordinates_for_points(pts, faces)
+    bvi, bw = oracle.barycentric_coordinates_for_points(v, f, pts, faces)
+    assert np.array_equal(vi, bvi) and np.array_equal(w, bw)
+    assert np.abs(w[0::2, 1:]).max() > 0
