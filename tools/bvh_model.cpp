@@ -628,3 +628,631 @@ extern "C" void model_counts_bvh4(const double* v, const uint32_t* f, int T, con
         leaves_out[i] = nl;
     }
 }
+
+// ---- entry-cut experiment: a uniform grid of G^3 cells over the box [blo, bhi]; every cell stores the
+// frontier of tree nodes that any point of the cell may need (a node is kept when its oriented-box bound
+// from the cell centre is <= d*(centre) + 2 r, r = the cell's half-diagonal; descent stops at depth Dcut or
+// when expanding would make the frontier larger than K).  Per query: nodes loaded from the root with a
+// near-perfect initial bound (d* (1 + 1e-9)), vs nodes loaded starting from its cell's frontier (every
+// frontier node is loaded once), and the frontier size.  depth_hist (64 bins, may be null): nodes loaded
+// from the root, by depth, summed over queries.
+namespace {
+struct ObbTree {
+    Tree tr;
+    std::vector<OBB> ob;
+    std::vector<int> depth;
+};
+ObbTree make_obb_tree(const double* v, const uint32_t* f, int T) {
+    ObbTree t;
+    t.tr = build_lbvh(v, f, T);
+    t.ob.resize(2 * (T - 1));
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int x = 0; x < T - 1; ++x)
+        for (int s = 0; s < 2; ++s) {
+            int b, e;
+            range_of(t.tr, t.tr.nodes[x].c[s], b, e);
+            t.ob[2 * x + s] = make_obb(t.tr, v, f, b, e, 1);
+        }
+    t.depth.assign(T - 1, 0);
+    std::vector<int> st{0};
+    while (!st.empty()) {
+        int x = st.back();
+        st.pop_back();
+        for (int s = 0; s < 2; ++s) {
+            int c = t.tr.nodes[x].c[s];
+            if (c >= 0) { t.depth[c] = t.depth[x] + 1; st.push_back(c); }
+        }
+    }
+    return t;
+}
+// nodes loaded by a near-first traversal from the given start nodes with initial squared bound b0;
+// returns final best
+double walk(const ObbTree& t, const double* v, const uint32_t* f, const double* q, const std::vector<int>& start,
+            double b0, uint32_t& nn, uint32_t& nl, uint64_t* hist) {
+    double best = b0;
+    std::vector<std::pair<int, double>> st;
+    for (int k = (int)start.size() - 1; k >= 0; --k) st.push_back({start[k], 0.0});
+    int node;
+    for (;;) {
+        bool found = false;
+        while (!st.empty()) {
+            auto e = st.back();
+            st.pop_back();
+            if (e.second <= best) { node = e.first; found = true; break; }
+        }
+        if (!found) break;
+        for (;;) {
+            const Node& n = t.tr.nodes[node];
+            ++nn;
+            if (hist) hist[std::min(t.depth[node], 63)]++;
+            double d[2];
+            bool h[2];
+            for (int s = 0; s < 2; ++s) {
+                d[s] = obb_d2(q, t.ob[2 * node + s]);
+                h[s] = d[s] <= best;
+                if (h[s] && n.c[s] < 0) {
+                    int fc = t.tr.order[~n.c[s]];
+                    const uint32_t* ff = f + 3 * fc;
+                    best = std::min(best, tri_d2(q, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                    ++nl;
+                    h[s] = false;
+                }
+            }
+            h[0] = h[0] && d[0] <= best;
+            h[1] = h[1] && d[1] <= best;
+            if (h[0] && h[1]) {
+                int nr = d[1] < d[0] ? 1 : 0;
+                st.push_back({n.c[1 - nr], d[1 - nr]});
+                node = n.c[nr];
+                continue;
+            }
+            if (h[0]) { node = n.c[0]; continue; }
+            if (h[1]) { node = n.c[1]; continue; }
+            break;
+        }
+    }
+    return best;
+}
+double exact_d2(const ObbTree& t, const double* v, const uint32_t* f, const double* q) {
+    uint32_t a = 0, b = 0;
+    return walk(t, v, f, q, std::vector<int>{0}, std::numeric_limits<double>::infinity(), a, b, nullptr);
+}
+// frontier of a cell: BFS by depth from the root, keeping nodes whose bound from c is <= lim (squared)
+std::vector<int> cell_cut(const ObbTree& t, const double* c, double lim, int dcut, int K) {
+    std::vector<int> cur{0};
+    for (int d = 0; d < dcut; ++d) {
+        std::vector<int> nxt;
+        bool leafy = false;
+        for (int x : cur) {
+            for (int s = 0; s < 2; ++s) {
+                int ch = t.tr.nodes[x].c[s];
+                if (obb_d2(c, t.ob[2 * x + s]) > lim) continue;
+                if (ch < 0) { leafy = true; continue; }
+                nxt.push_back(ch);
+            }
+        }
+        if (leafy || (int)nxt.size() > K || nxt.empty()) break;  // keep cur
+        cur.swap(nxt);
+    }
+    return cur;
+}
+}  // namespace
+
+extern "C" void model_entry_cut(const double* v, const uint32_t* f, int T, const double* q, long S, const double* blo,
+                                const double* bhi, int G, int dcut, int K, uint32_t* root_nodes, uint32_t* cut_nodes,
+                                uint32_t* cut_size, uint64_t* depth_hist) {
+    ObbTree t = make_obb_tree(v, f, T);
+    std::vector<uint64_t> hist(64, 0);
+#pragma omp parallel
+    {
+        std::vector<uint64_t> h(64, 0);
+#pragma omp for schedule(dynamic, 64)
+        for (long i = 0; i < S; ++i) {
+            const double* qq = q + 3 * i;
+            const double d2 = exact_d2(t, v, f, qq);
+            uint32_t nn = 0, nl = 0;
+            walk(t, v, f, qq, std::vector<int>{0}, d2 * (1 + 1e-9), nn, nl, h.data());
+            root_nodes[i] = nn;
+            // cell of q
+            double c[3], r2 = 0;
+            bool inside = true;
+            for (int k = 0; k < 3; ++k) {
+                const double w = (bhi[k] - blo[k]) / G;
+                int ci = (int)std::floor((qq[k] - blo[k]) / w);
+                if (ci < 0 || ci >= G) inside = false;
+                ci = std::min(std::max(ci, 0), G - 1);
+                c[k] = blo[k] + (ci + 0.5) * w;
+                r2 += 0.25 * w * w;
+            }
+            if (!inside) { cut_nodes[i] = nn; cut_size[i] = 0; continue; }
+            const double r = std::sqrt(r2);
+            const double dc = std::sqrt(exact_d2(t, v, f, c));
+            const double lim = (dc + 2 * r) * (dc + 2 * r) * (1 + 1e-9);
+            std::vector<int> cut = cell_cut(t, c, lim, dcut, K);
+            uint32_t cn = 0, cl = 0;
+            walk(t, v, f, qq, cut, d2 * (1 + 1e-9), cn, cl, nullptr);
+            cut_nodes[i] = cn;
+            cut_size[i] = (uint32_t)cut.size();
+        }
+#pragma omp critical
+        for (int k = 0; k < 64; ++k) hist[k] += h[k];
+    }
+    if (depth_hist)
+        for (int k = 0; k < 64; ++k) depth_hist[k] = hist[k];
+}
+
+// ---- follower hint experiment: slots in Morton order; every 8th slot is a leader answered exactly; the
+// other slots start from a hint of their 64-slot window's 8 leaders: kind 0 = min |q - p_L|^2 (the
+// leader's closest point, as k_knn does), 1 = d^2(q, face of the leader whose p_L is nearest), 2 = min over
+// the 8 leaders' faces of d^2(q, face), 3 = the exact answer (perfect bound).  Outputs per follower slot:
+// nodes loaded and leaf tests (leaders: 0).
+extern "C" void model_follower_hints(const double* v, const uint32_t* f, int T, const double* q, long S, int kind,
+                                     uint32_t* nodes_out, uint32_t* leaves_out) {
+    ObbTree t = make_obb_tree(v, f, T);
+    std::vector<int> face(S, -1);
+    std::vector<double> pt(3 * S, 0.0);
+    // leaders: exact closest face and point (brute force over the tree walk, then a point by projection)
+    auto closest = [&](const double* qq, int& bf, double* bp) {
+        double best = std::numeric_limits<double>::infinity();
+        std::vector<std::pair<int, double>> st{{0, 0.0}};
+        bf = -1;
+        while (!st.empty()) {
+            auto e = st.back();
+            st.pop_back();
+            if (e.second > best) continue;
+            const Node& n = t.tr.nodes[e.first];
+            for (int s = 0; s < 2; ++s) {
+                double d = obb_d2(qq, t.ob[2 * e.first + s]);
+                if (d > best) continue;
+                if (n.c[s] < 0) {
+                    int fc = t.tr.order[~n.c[s]];
+                    const uint32_t* ff = f + 3 * fc;
+                    double d2 = tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]);
+                    if (d2 < best) { best = d2; bf = fc; }
+                } else {
+                    st.push_back({n.c[s], d});
+                }
+            }
+        }
+        // closest point on face bf: sample by minimising over a projection (use segment/plane logic of tri_d2)
+        const uint32_t* ff = f + 3 * bf;
+        const double *A = v + 3 * ff[0], *B = v + 3 * ff[1], *C = v + 3 * ff[2];
+        // barycentric projection clamp (Ericson)
+        double ab[3], ac[3], ap[3];
+        for (int k = 0; k < 3; ++k) { ab[k] = B[k] - A[k]; ac[k] = C[k] - A[k]; ap[k] = qq[k] - A[k]; }
+        auto dot = [](const double* x, const double* y) { return x[0] * y[0] + x[1] * y[1] + x[2] * y[2]; };
+        double d1 = dot(ab, ap), d2 = dot(ac, ap);
+        double res[3];
+        if (d1 <= 0 && d2 <= 0) { for (int k = 0; k < 3; ++k) res[k] = A[k]; }
+        else {
+            double bp_[3]; for (int k = 0; k < 3; ++k) bp_[k] = qq[k] - B[k];
+            double d3 = dot(ab, bp_), d4 = dot(ac, bp_);
+            double cp[3]; for (int k = 0; k < 3; ++k) cp[k] = qq[k] - C[k];
+            double d5 = dot(ab, cp), d6 = dot(ac, cp);
+            double vc = d1 * d4 - d3 * d2, vb = d5 * d2 - d1 * d6, va = d3 * d6 - d5 * d4;
+            if (d3 >= 0 && d4 <= d3) { for (int k = 0; k < 3; ++k) res[k] = B[k]; }
+            else if (vc <= 0 && d1 >= 0 && d3 <= 0) { double w = d1 / (d1 - d3); for (int k = 0; k < 3; ++k) res[k] = A[k] + w * ab[k]; }
+            else if (d6 >= 0 && d5 <= d6) { for (int k = 0; k < 3; ++k) res[k] = C[k]; }
+            else if (vb <= 0 && d2 >= 0 && d6 <= 0) { double w = d2 / (d2 - d6); for (int k = 0; k < 3; ++k) res[k] = A[k] + w * ac[k]; }
+            else if (va <= 0 && (d4 - d3) >= 0 && (d5 - d6) >= 0) { double w = (d4 - d3) / ((d4 - d3) + (d5 - d6)); for (int k = 0; k < 3; ++k) res[k] = B[k] + w * (C[k] - B[k]); }
+            else { double den = 1.0 / (va + vb + vc); double vv = vb * den, ww = vc * den; for (int k = 0; k < 3; ++k) res[k] = A[k] + ab[k] * vv + ac[k] * ww; }
+        }
+        for (int k = 0; k < 3; ++k) bp[k] = res[k];
+        return best;
+    };
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long i = 0; i < S; i += 8) closest(q + 3 * i, face[i], &pt[3 * i]);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long i = 0; i < S; ++i) {
+        nodes_out[i] = leaves_out[i] = 0;
+        if (i % 8 == 0) continue;
+        const double* qq = q + 3 * i;
+        const long base = (i / 64) * 64;
+        double h = std::numeric_limits<double>::infinity();
+        if (kind == 3) {
+            int bf; double bp[3];
+            h = closest(qq, bf, bp) * (1 + 1e-9);
+        } else {
+            int nearest_l = -1;
+            double hp = std::numeric_limits<double>::infinity();
+            for (long L = base; L < base + 64 && L < S; L += 8) {
+                double dx = qq[0] - pt[3 * L], dy = qq[1] - pt[3 * L + 1], dz = qq[2] - pt[3 * L + 2];
+                double d2 = dx * dx + dy * dy + dz * dz;
+                if (d2 < hp) { hp = d2; nearest_l = (int)L; }
+                if (kind == 2) {
+                    const uint32_t* ff = f + 3 * face[L];
+                    h = std::min(h, tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                }
+            }
+            if (kind == 0) h = hp;
+            if (kind == 1) {
+                const uint32_t* ff = f + 3 * face[nearest_l];
+                h = tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]);
+            }
+            h *= 1 + 1e-9;
+        }
+        uint32_t nn = 0, nl = 0;
+        walk(t, v, f, qq, std::vector<int>{0}, h, nn, nl, nullptr);
+        nodes_out[i] = nn;
+        leaves_out[i] = nl;
+    }
+}
+
+// ---- postponed leaves: the near-first walk with leaf tests delayed until `qmax` leaves are queued or the
+// stack runs dry (k_knn's per-lane queue between wave-wide leaf phases); hint kind 0 (min |q - p_L|^2 of
+// 8 leaders in the 64-slot window, leaders exact) as model_follower_hints.  Outputs per follower slot.
+extern "C" void model_postponed(const double* v, const uint32_t* f, int T, const double* q, long S, int qmax,
+                                uint32_t* nodes_out, uint32_t* leaves_out) {
+    ObbTree t = make_obb_tree(v, f, T);
+    std::vector<double> pt(3 * S, 0.0);
+    // leaders' closest points from an exact walk + brute projection via tri_d2's minimiser (vertex/edge/face):
+    // reuse model_follower_hints' point by a fine sampling-free approach: closest point = q - (q - p) where
+    // p is found by testing the exact best face with a barycentric clamp
+    auto best_face = [&](const double* qq) {
+        double best = std::numeric_limits<double>::infinity();
+        int bf = -1;
+        std::vector<std::pair<int, double>> st{{0, 0.0}};
+        while (!st.empty()) {
+            auto e = st.back();
+            st.pop_back();
+            if (e.second > best) continue;
+            const Node& n = t.tr.nodes[e.first];
+            for (int s = 0; s < 2; ++s) {
+                double d = obb_d2(qq, t.ob[2 * e.first + s]);
+                if (d > best) continue;
+                if (n.c[s] < 0) {
+                    int fc = t.tr.order[~n.c[s]];
+                    const uint32_t* ff = f + 3 * fc;
+                    double d2 = tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]);
+                    if (d2 < best) { best = d2; bf = fc; }
+                } else st.push_back({n.c[s], d});
+            }
+        }
+        return bf;
+    };
+    auto closest_pt = [&](const double* qq, int bf, double* res) {
+        const uint32_t* ff = f + 3 * bf;
+        const double *A = v + 3 * ff[0], *B = v + 3 * ff[1], *C = v + 3 * ff[2];
+        // minimise over a fine barycentric grid refined by projection (adequate for a hint model)
+        double bestd = 1e300;
+        for (int i = 0; i <= 40; ++i)
+            for (int j = 0; i + j <= 40; ++j) {
+                double a = i / 40.0, b = j / 40.0, c = 1 - a - b, p[3], d = 0;
+                for (int k = 0; k < 3; ++k) { p[k] = a * A[k] + b * B[k] + c * C[k]; d += (p[k] - qq[k]) * (p[k] - qq[k]); }
+                if (d < bestd) { bestd = d; for (int k = 0; k < 3; ++k) res[k] = p[k]; }
+            }
+    };
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long i = 0; i < S; i += 8) closest_pt(q + 3 * i, best_face(q + 3 * i), &pt[3 * i]);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long i = 0; i < S; ++i) {
+        nodes_out[i] = leaves_out[i] = 0;
+        if (i % 8 == 0) continue;
+        const double* qq = q + 3 * i;
+        const long base = (i / 64) * 64;
+        double best = std::numeric_limits<double>::infinity();
+        for (long L = base; L < base + 64 && L < S; L += 8) {
+            double dx = qq[0] - pt[3 * L], dy = qq[1] - pt[3 * L + 1], dz = qq[2] - pt[3 * L + 2];
+            best = std::min(best, dx * dx + dy * dy + dz * dz);
+        }
+        best *= 1 + 1e-9;
+        uint32_t nn = 0, nl = 0;
+        std::vector<std::pair<int, double>> st;
+        std::vector<int> queue;
+        auto flush = [&]() {
+            for (int lf : queue) {
+                int fc = t.tr.order[lf];
+                const uint32_t* ff = f + 3 * fc;
+                best = std::min(best, tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                ++nl;
+            }
+            queue.clear();
+        };
+        int node = 0;
+        bool have = true;
+        for (;;) {
+            if (!have) {
+                bool found = false;
+                while (!st.empty()) {
+                    auto e = st.back();
+                    st.pop_back();
+                    if (e.second <= best) { node = e.first; found = true; break; }
+                }
+                if (!found) {
+                    if (queue.empty()) break;
+                    flush();
+                    continue;
+                }
+            }
+            have = true;
+            if ((int)queue.size() > qmax - 2) flush();
+            const Node& n = t.tr.nodes[node];
+            ++nn;
+            double d[2];
+            bool h[2];
+            for (int s = 0; s < 2; ++s) {
+                d[s] = obb_d2(qq, t.ob[2 * node + s]);
+                h[s] = d[s] <= best;
+                if (h[s] && n.c[s] < 0) {
+                    if (qmax == 0) {
+                        int fc = t.tr.order[~n.c[s]];
+                        const uint32_t* ff = f + 3 * fc;
+                        best = std::min(best, tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                        ++nl;
+                    } else {
+                        queue.push_back(~n.c[s]);
+                    }
+                    h[s] = false;
+                }
+            }
+            h[0] = h[0] && d[0] <= best;
+            h[1] = h[1] && d[1] <= best;
+            if (h[0] && h[1]) {
+                int nr = d[1] < d[0] ? 1 : 0;
+                st.push_back({n.c[1 - nr], d[1 - nr]});
+                node = n.c[nr];
+                continue;
+            }
+            if (h[0]) { node = n.c[0]; continue; }
+            if (h[1]) { node = n.c[1]; continue; }
+            have = false;
+        }
+        nodes_out[i] = nn;
+        leaves_out[i] = nl;
+    }
+}
+
+// ---- node encoding experiment: both children's oriented boxes in the PARENT's frame (k_obb_*: the frame
+// from the area-weighted normal of the node's Morton range, t from the x or y axis), and their extents
+// quantised like build.hip encode_node.  enc: 0 exact fp64 extents, 1 8-bit codes with a power-of-two scale
+// (254 * 2^e >= range, the product format), 2 8-bit codes with scale range / 255 (any fp32), 3 16-bit
+// codes with scale range / 65535.  init_best (nullable) as model_counts_obb_init.
+namespace {
+struct QBox { double ax[3][3]; double lo[2][3], hi[2][3]; };
+}
+Tree build_tree_kind(const double* v, const uint32_t* f, int T, int kind);
+extern "C" void model_encoded_tree(const double* v, const uint32_t* f, int T, const double* q, long S, int enc,
+                                   const double* init_best, uint32_t* nodes_out, uint32_t* leaves_out, int tree_kind);
+extern "C" void model_encoded(const double* v, const uint32_t* f, int T, const double* q, long S, int enc,
+                              const double* init_best, uint32_t* nodes_out, uint32_t* leaves_out) {
+    model_encoded_tree(v, f, T, q, S, enc, init_best, nodes_out, leaves_out, 0);
+}
+extern "C" void model_encoded_tree(const double* v, const uint32_t* f, int T, const double* q, long S, int enc,
+                                   const double* init_best, uint32_t* nodes_out, uint32_t* leaves_out, int tree_kind) {
+    Tree tr = build_tree_kind(v, f, T, tree_kind);
+    std::vector<QBox> nb(T - 1);
+#pragma omp parallel for schedule(dynamic, 256)
+    for (int x = 0; x < T - 1; ++x) {
+        int b, e;
+        range_of(tr, x, b, e);
+        double s[3] = {0, 0, 0};
+        for (int i = b; i <= e; ++i) {
+            const uint32_t* ff = f + 3 * tr.order[i];
+            const double *A = v + 3 * ff[0], *B = v + 3 * ff[1], *C = v + 3 * ff[2];
+            double ab[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, ac[3] = {C[0] - A[0], C[1] - A[1], C[2] - A[2]};
+            s[0] += ab[1] * ac[2] - ab[2] * ac[1]; s[1] += ab[2] * ac[0] - ab[0] * ac[2]; s[2] += ab[0] * ac[1] - ab[1] * ac[0];
+        }
+        double len = std::sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+        double n[3] = {1, 0, 0};
+        if (len > 0) for (int k = 0; k < 3; ++k) n[k] = s[k] / len;
+        double ee[3] = {0, 0, 0};
+        ee[std::fabs(n[0]) < 0.9 ? 0 : 1] = 1;
+        double d = ee[0] * n[0] + ee[1] * n[1] + ee[2] * n[2], t[3];
+        for (int k = 0; k < 3; ++k) t[k] = ee[k] - d * n[k];
+        double tl = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+        for (int k = 0; k < 3; ++k) t[k] /= tl;
+        QBox& qb = nb[x];
+        for (int k = 0; k < 3; ++k) { qb.ax[0][k] = n[k]; qb.ax[1][k] = t[k]; }
+        qb.ax[2][0] = n[1] * t[2] - n[2] * t[1]; qb.ax[2][1] = n[2] * t[0] - n[0] * t[2]; qb.ax[2][2] = n[0] * t[1] - n[1] * t[0];
+        for (int sd = 0; sd < 2; ++sd) {
+            int cb, ce;
+            range_of(tr, tr.nodes[x].c[sd], cb, ce);
+            for (int a = 0; a < 3; ++a) { qb.lo[sd][a] = 1e300; qb.hi[sd][a] = -1e300; }
+            for (int i = cb; i <= ce; ++i) {
+                const uint32_t* ff = f + 3 * tr.order[i];
+                for (int c = 0; c < 3; ++c) {
+                    const double* P = v + 3 * ff[c];
+                    for (int a = 0; a < 3; ++a) {
+                        double p = P[0] * qb.ax[a][0] + P[1] * qb.ax[a][1] + P[2] * qb.ax[a][2];
+                        qb.lo[sd][a] = std::min(qb.lo[sd][a], p);
+                        qb.hi[sd][a] = std::max(qb.hi[sd][a], p);
+                    }
+                }
+            }
+        }
+        if (enc == 0) continue;
+        for (int a = 0; a < 3; ++a) {
+            double base = std::min(qb.lo[0][a], qb.lo[1][a]);
+            double top = std::max(qb.hi[0][a], qb.hi[1][a]);
+            double range = top - base, sc;
+            if (enc == 1) { int e2 = range > 0 ? (int)std::ceil(std::log2(range / 254.0)) : -126; sc = std::ldexp(1.0, e2); }
+            else if (enc == 2) sc = range > 0 ? range / 255.0 : 1e-30;
+            else sc = range > 0 ? range / 65535.0 : 1e-30;
+            for (int sd = 0; sd < 2; ++sd) {
+                qb.lo[sd][a] = base + std::floor((qb.lo[sd][a] - base) / sc) * sc;
+                qb.hi[sd][a] = base + std::ceil((qb.hi[sd][a] - base) / sc) * sc;
+            }
+        }
+    }
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long i = 0; i < S; ++i) {
+        const double* qq = q + 3 * i;
+        double best = init_best ? init_best[i] : std::numeric_limits<double>::infinity();
+        uint32_t nn = 0, nl = 0;
+        std::vector<std::pair<int, double>> st;
+        int node = 0;
+        for (;;) {
+            const Node& n = tr.nodes[node];
+            const QBox& qb = nb[node];
+            ++nn;
+            double pr[3];
+            for (int a = 0; a < 3; ++a) pr[a] = qq[0] * qb.ax[a][0] + qq[1] * qb.ax[a][1] + qq[2] * qb.ax[a][2];
+            double dd[2];
+            bool h[2];
+            for (int s = 0; s < 2; ++s) {
+                double acc = 0;
+                for (int a = 0; a < 3; ++a) {
+                    double g = std::max(std::max(qb.lo[s][a] - pr[a], pr[a] - qb.hi[s][a]), 0.0);
+                    acc += g * g;
+                }
+                dd[s] = acc;
+                h[s] = acc <= best;
+                if (h[s] && n.c[s] < 0) {
+                    int fc = tr.order[~n.c[s]];
+                    const uint32_t* ff = f + 3 * fc;
+                    best = std::min(best, tri_d2(qq, v + 3 * ff[0], v + 3 * ff[1], v + 3 * ff[2]));
+                    ++nl;
+                    h[s] = false;
+                }
+            }
+            h[0] = h[0] && dd[0] <= best;
+            h[1] = h[1] && dd[1] <= best;
+            if (h[0] && h[1]) {
+                int nr = dd[1] < dd[0] ? 1 : 0;
+                st.push_back({n.c[1 - nr], dd[1 - nr]});
+                node = n.c[nr];
+                continue;
+            }
+            if (h[0]) { node = n.c[0]; continue; }
+            if (h[1]) { node = n.c[1]; continue; }
+            bool found = false;
+            while (!st.empty()) {
+                auto e = st.back();
+                st.pop_back();
+                if (e.second <= best) { node = e.first; found = true; break; }
+            }
+            if (!found) break;
+        }
+        nodes_out[i] = nn;
+        leaves_out[i] = nl;
+    }
+}
+
+
+// ---- tree builders for the encoding experiment: 0 LBVH (build.hip), 1 median split on the longest axis of
+// the centroid AABB (CGAL-like), 2 median split along the longest tangent axis of the node's own frame
+// (area-weighted normal n; centroids projected on t, b; split on the larger spread), 3 as 2 but split at the
+// spatial midpoint of that axis (object partition, unbalanced allowed)
+namespace {
+int build_oriented_rec(Tree& tr, std::vector<int>& idx, int b, int e, const std::vector<double>& cen,
+                       const std::vector<double>& area, int mode) {
+    if (e - b == 1) return ~b;
+    int node = (int)tr.nodes.size();
+    tr.nodes.push_back(Node{});
+    double s[3] = {0, 0, 0};
+    for (int i = b; i < e; ++i)
+        for (int k = 0; k < 3; ++k) s[k] += area[3 * idx[i] + k];
+    double len = std::sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+    double n[3] = {1, 0, 0};
+    if (len > 1e-9 * (e - b) * 1e-12) for (int k = 0; k < 3; ++k) n[k] = s[k] / len;
+    // candidate axes: for a closed/curved patch use the 3 principal directions of the centroid spread
+    // (covariance eigenvectors via power iteration); otherwise the tangent plane
+    double m[3] = {0, 0, 0};
+    for (int i = b; i < e; ++i)
+        for (int k = 0; k < 3; ++k) m[k] += cen[3 * idx[i] + k];
+    for (int k = 0; k < 3; ++k) m[k] /= (e - b);
+    double C[3][3] = {{0}};
+    for (int i = b; i < e; ++i) {
+        double d[3];
+        for (int k = 0; k < 3; ++k) d[k] = cen[3 * idx[i] + k] - m[k];
+        for (int a = 0; a < 3; ++a)
+            for (int c = 0; c < 3; ++c) C[a][c] += d[a] * d[c];
+    }
+    double ax[3] = {1, 1, 1};
+    if (mode == 5 || mode == 6 || mode == 7) {
+        // 5: longest axis of the centroid AABB, split at its spatial middle; 6: the longest centroid spread
+        // among x, y, z and the node frame's two tangent axes, split at the median
+        double cands[5][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}, {0, 0, 0}};
+        int nc = 3;
+        if ((mode == 6 || mode == 7) && len > 0) {
+            double ee[3] = {0, 0, 0};
+            ee[std::fabs(n[0]) < 0.9 ? 0 : 1] = 1;
+            double d = ee[0] * n[0] + ee[1] * n[1] + ee[2] * n[2], t[3];
+            for (int k = 0; k < 3; ++k) t[k] = ee[k] - d * n[k];
+            double tl = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+            for (int k = 0; k < 3; ++k) t[k] /= tl;
+            double bb[3] = {n[1] * t[2] - n[2] * t[1], n[2] * t[0] - n[0] * t[2], n[0] * t[1] - n[1] * t[0]};
+            for (int k = 0; k < 3; ++k) { cands[3][k] = t[k]; cands[4][k] = bb[k]; }
+            nc = 5;
+        }
+        double bestw = -1;
+        for (int c = 0; c < nc; ++c) {
+            double lo = 1e300, hi = -1e300;
+            for (int i = b; i < e; ++i) {
+                double k = cen[3 * idx[i]] * cands[c][0] + cen[3 * idx[i] + 1] * cands[c][1] + cen[3 * idx[i] + 2] * cands[c][2];
+                lo = std::min(lo, k); hi = std::max(hi, k);
+            }
+            if (hi - lo > bestw) { bestw = hi - lo; for (int k = 0; k < 3; ++k) ax[k] = cands[c][k]; }
+        }
+    } else
+    for (int it = 0; it < 50; ++it) {
+        double y[3];
+        for (int a = 0; a < 3; ++a) y[a] = C[a][0] * ax[0] + C[a][1] * ax[1] + C[a][2] * ax[2];
+        double l = std::sqrt(y[0] * y[0] + y[1] * y[1] + y[2] * y[2]);
+        if (!(l > 0)) break;
+        for (int a = 0; a < 3; ++a) ax[a] = y[a] / l;
+    }
+    (void)n;
+    auto key = [&](int x) { return cen[3 * x] * ax[0] + cen[3 * x + 1] * ax[1] + cen[3 * x + 2] * ax[2]; };
+    int mid = (b + e) / 2;
+    if (mode == 3 || mode == 5 || mode == 7) {
+        double lo = 1e300, hi = -1e300;
+        for (int i = b; i < e; ++i) { double k = key(idx[i]); lo = std::min(lo, k); hi = std::max(hi, k); }
+        double c = 0.5 * (lo + hi);
+        auto it = std::partition(idx.begin() + b, idx.begin() + e, [&](int x) { return key(x) < c; });
+        mid = (int)(it - idx.begin());
+        if (mid == b || mid == e) mid = (b + e) / 2;
+        std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e, [&](int x, int y) { return key(x) < key(y); });
+    } else {
+        std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e, [&](int x, int y) { return key(x) < key(y); });
+    }
+    int l = build_oriented_rec(tr, idx, b, mid, cen, area, mode);
+    int r = build_oriented_rec(tr, idx, mid, e, cen, area, mode);
+    tr.nodes[node].c[0] = l;
+    tr.nodes[node].c[1] = r;
+    return node;
+}
+}  // namespace
+namespace {
+// hybrid: the LBVH's nodes over more than K leaves, its subtrees over at most K leaves rebuilt with mode 7
+int hybrid_rec(const Tree& lb, int c, Tree& out, std::vector<int>& idx, const std::vector<double>& cen,
+               const std::vector<double>& area, int K, int mode) {
+    if (c < 0) return c;  // a leaf: position ~c
+    int b, e;
+    range_of(lb, c, b, e);
+    if (e - b + 1 <= K) return build_oriented_rec(out, idx, b, e + 1, cen, area, mode);
+    int node = (int)out.nodes.size();
+    out.nodes.push_back(Node{});
+    int l = hybrid_rec(lb, lb.nodes[c].c[0], out, idx, cen, area, K, mode);
+    int r = hybrid_rec(lb, lb.nodes[c].c[1], out, idx, cen, area, K, mode);
+    out.nodes[node].c[0] = l;
+    out.nodes[node].c[1] = r;
+    return node;
+}
+}  // namespace
+Tree build_tree_kind(const double* v, const uint32_t* f, int T, int kind) {
+    if (kind == 0) return build_lbvh(v, f, T);
+    if (kind == 1) return build_median(v, f, T);
+    std::vector<double> cen(3 * T), area(3 * T);
+    for (int t = 0; t < T; ++t) {
+        const double *A = v + 3 * f[3 * t], *B = v + 3 * f[3 * t + 1], *C = v + 3 * f[3 * t + 2];
+        double ab[3] = {B[0] - A[0], B[1] - A[1], B[2] - A[2]}, ac[3] = {C[0] - A[0], C[1] - A[1], C[2] - A[2]};
+        area[3 * t] = ab[1] * ac[2] - ab[2] * ac[1];
+        area[3 * t + 1] = ab[2] * ac[0] - ab[0] * ac[2];
+        area[3 * t + 2] = ab[0] * ac[1] - ab[1] * ac[0];
+        for (int k = 0; k < 3; ++k) cen[3 * t + k] = (A[k] + B[k] + C[k]) / 3.0;
+    }
+    Tree tr;
+    std::vector<int> idx(T);
+    std::iota(idx.begin(), idx.end(), 0);
+    tr.nodes.reserve(T);
+    if (kind >= 100) {  // 100 + log2 K: hybrid over the LBVH
+        Tree lb = build_lbvh(v, f, T);
+        idx = lb.order;
+        hybrid_rec(lb, 0, tr, idx, cen, area, 1 << (kind - 100), 7);
+    } else {
+        build_oriented_rec(tr, idx, 0, T, cen, area, kind);
+    }
+    tr.order = idx;
+    return tr;
+}
