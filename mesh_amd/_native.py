@@ -199,7 +199,7 @@ def source_build_id(extra=""):
     import hashlib
     import os
     csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
-    names = sorted(["sort.hip", "build.hip", "nearest.hip", "rays.hip", "tritri.hip", "geometry.hip", "api.cpp",
+    names = sorted(["sort.hip", "build.hip", "refine.hip", "nearest.hip", "rays.hip", "tritri.hip", "geometry.hip", "api.cpp",
                     "loaders.cpp", "common.h", "internal.h"])
     h = hashlib.sha256()
     for p in [os.path.join(csrc, n) for n in names] + [os.path.join(csrc, "..", "..", "include", "meshsearch.h")]:

@@ -208,6 +208,13 @@ struct WsOrder {
 };
 
 // Triangle tree over v (P rows) and f (T rows, indices into v).
+// Subtrees of the LBVH over at most 2^kResplitLog2 leaves are rebuilt top down along the surface (refine.hip);
+// 0 keeps the plain Karras tree
+#ifndef MSH_RESPLIT
+#define MSH_RESPLIT 16
+#endif
+constexpr int kResplitLog2 = MSH_RESPLIT;
+
 static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint32_t* f, size_t T) {
     hipStream_t s = t->stream;
     hipEvent_t e0, e1;
@@ -231,6 +238,7 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
         (void)hipEventRecord(e0, s);
         if ((st = tri_bounds(t->d_v, dF.as<uint32_t>(), T, dLo.as<double>(), dHi.as<double>(), s)) != MSH_OK) break;
         if ((st = build_lbvh(t, dLo.as<double>(), dHi.as<double>(), T, dOrder.as<uint32_t>())) != MSH_OK) break;
+        if ((st = resplit_tree(t, t->d_v, dF.as<uint32_t>(), T, dOrder.as<uint32_t>(), kResplitLog2)) != MSH_OK) break;
         if ((st = pack_tri_leaves(t->d_v, dF.as<uint32_t>(), dOrder.as<uint32_t>(), T, 0u,
                                   static_cast<TriRec*>(t->d_leaves), s)) != MSH_OK)
             break;

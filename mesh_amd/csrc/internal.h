@@ -151,6 +151,9 @@ int mesh_keys(const uint32_t* vals, size_t n, size_t per, uint32_t* keys, hipStr
 double half_diagonal(const double* box, const double* origin);
 // device copy of tree->origin (single-mesh trees; blob unpack)
 int upload_origin(msh_tree* tree, hipStream_t s);
+// Top-down re-split of every LBVH subtree over at most 2^log2K leaves (refine.hip): the same node ids,
+// ranges and leaf-order conventions as build_lbvh, which it must follow (triangle trees; before leaf packing).
+int resplit_tree(msh_tree* tree, const double* d_v, const uint32_t* d_f, size_t T, uint32_t* d_order, int log2K);
 // Oriented-box pass over the packed leaves (needs the node ranges recorded by build_lbvh).
 int build_obb(msh_tree* tree, bool triangles);
 int tri_bounds(const double* d_v, const uint32_t* d_f, size_t T, double* d_lo, double* d_hi, hipStream_t s);
