@@ -93,6 +93,9 @@ struct KnnArgs {
     // direct: the sorted path writes each answer straight to the caller's row perm[i] (no k_unpermute);
     // slot-order records are kept only for the leader phases, whose records are the followers' hints
     bool direct;
+    // rec_leaf: slot-order records are hints only (direct stores, or instrumented launches), so their part
+    // field carries the winner's leaf index instead of its part code (leader_leaf)
+    bool rec_leaf;
     size_t nunits;  // work units of this phase (slots it covers)
     DeferRec* deferred;
     unsigned* n_deferred;
@@ -282,11 +285,19 @@ struct Walker {
         return pop(pol, lds, spill);
     }
     // As step(), but leaf children that survive the bound are handed back in p0/p1 instead of being
-    // tested here, so the caller can run leaf tests for many lanes of the wave at once.
+    // tested here, so the caller can run leaf tests for many lanes of the wave at once.  `room` = leaves the
+    // caller can still queue (>= 1): when a node has two leaf children and there is room for one, the farther
+    // leaf is parked on the stack as an entry (~leaf, bound); a parked leaf popped later becomes `node`
+    // (negative) and is handed back by the next step without a node load.  So a lane keeps traversing while
+    // its queue has room for one leaf, instead of stopping as soon as a node could add two.
     template <class Pol, bool STATS>
     __device__ inline bool step_collect(const BNode* __restrict__ nodes, const QF& qf, const Pol& pol,
                                         uint2* __restrict__ lds, uint2* __restrict__ spill, unsigned& n_nodes, int& p0,
-                                        int& p1) {
+                                        int& p1, int room = 2) {
+        if (node < 0) {
+            p0 = ~node;
+            return pop(pol, lds, spill);
+        }
         const NodeV nd = load_node(nodes, node);
         if (STATS) ++n_nodes;
         float d0, d1;
@@ -294,6 +305,12 @@ struct Walker {
         const int c0 = nd.child(0), c1 = nd.child(1);
         const float lim = pol.limf;
         bool h0 = d0 <= lim, h1 = d1 <= lim;
+        if (room < 2 && h0 && h1 && c0 < 0 && c1 < 0) {  // two leaves, room for one: park the farther
+            const bool far0 = d0 > d1;
+            p0 = far0 ? ~c1 : ~c0;
+            push(make_uint2((unsigned)(far0 ? c0 : c1), __float_as_uint(far0 ? d0 : d1)), lds, spill);
+            return pop(pol, lds, spill);
+        }
         if (h0 && c0 < 0) {
             p0 = ~c0;
             h0 = false;
@@ -358,7 +375,7 @@ __device__ inline void write_result(const KnnArgs& a, size_t i, const D3& q, con
         if (MODE == 3) w = heidrich_bary(o, ta, tb, tc);
     }
     if (rec) {
-        store_qres(a.res + i, face, (uint32_t)part, o.x, o.y, o.z);
+        store_qres(a.res + i, face, a.rec_leaf ? (uint32_t)pol.best_leaf : (uint32_t)part, o.x, o.y, o.z);
         if (MODE == 3 && !a.direct) {
             a.res_w[3 * i] = w.x;
             a.res_w[3 * i + 1] = w.y;
@@ -419,7 +436,7 @@ __device__ inline D3 load_q(const KnnArgs& a, size_t i) {
 #endif
 constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: leader ordering off)
 #ifndef MSH_LEAF_K
-#define MSH_LEAF_K 2
+#define MSH_LEAF_K 3
 #endif
 constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= traversing lanes / kLeafK
 #ifndef MSH_LEAF_Q
@@ -427,6 +444,10 @@ constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= t
 #endif
 constexpr int kLeafQ = MSH_LEAF_Q;  // leaves a lane may hold before it stops traversing (2..4)
 static_assert(kLeafQ >= 2 && kLeafQ <= 4, "kLeafQ must be 2, 3 or 4");
+#ifndef MSH_LEAF_PARK
+#define MSH_LEAF_PARK 1
+#endif
+constexpr bool kLeafPark = MSH_LEAF_PARK;  // lanes traverse while their queue has room for one leaf (step_collect)
 
 #ifndef MSH_LEAD2
 #define MSH_LEAD2 256
@@ -486,6 +507,39 @@ __device__ inline double hint_from_leaders(const KnnArgs& a, size_t i, const D3&
     return h * (1.0 + 9.313225746154785e-10) + e * e;  // 1 + 2^-30
 }
 
+// The leaf holding the closest point of the leader (at base, base + stride, ... < base + window, as
+// hint_from_leaders) nearest to q, or -1: with kHintFace a slot starts by testing that leaf exactly, as if
+// the traversal had reached it first — a real candidate (d^2, face, leaf), so no hint can be too tight and
+// nothing re-runs, and the exact distance to the leader's face is at most |q - p_L|.  Neighbouring queries
+// mostly share their closest face: the first bound is usually the answer (host model: 14 % fewer leaf tests
+// than the |q - p_L| hint).
+#ifndef MSH_HINT_FACE
+#define MSH_HINT_FACE 1
+#endif
+constexpr bool kHintFace = MSH_HINT_FACE;
+__device__ inline int leader_leaf(const KnnArgs& a, size_t i, const D3& q, size_t window, size_t stride) {
+    const size_t base = (i / window) * window;
+    const size_t mesh = a.orgs ? i / a.qper : 0;
+    double h = INFINITY;
+    int leaf = -1;
+    for (size_t L = 0; L < window; L += stride) {
+        const size_t li = base + L;
+        if (li >= a.S) break;
+        if (a.orgs && li / a.qper != mesh) continue;
+        const uint4 r0 = reinterpret_cast<const uint4*>(a.res + li)[0];
+        if (r0.x == MSH_NO_FACE) continue;
+        const double2 r1 = reinterpret_cast<const double2*>(a.res + li)[1];
+        const double x = __longlong_as_double((long long)(((unsigned long long)r0.w << 32) | r0.z));
+        const double dx = q.x - x, dy = q.y - r1.x, dz = q.z - r1.y;
+        const double d2 = dx * dx + dy * dy + dz * dz;
+        if (d2 < h) {
+            h = d2;
+            leaf = (int)r0.y;
+        }
+    }
+    return leaf;
+}
+
 // Pass 1 runs 4 waves per SIMD: the register budget drops from 139 to 128 VGPRs at the cost of a few
 // spills of loop-invariant values outside the node step (C3: +10 % over the compiler's 3 waves).
 #ifndef MSH_WAVES
@@ -521,9 +575,19 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         double hint = INFINITY;
         if constexpr (MODE == 0 || MODE == 3) {
             if (a.phase == 2 || (a.phase == 1 && kLead2 > 0)) {
-                hint = a.phase == 2 ? hint_from_leaders(a, i, q, MSH_FWIN, kLead) : hint_from_leaders(a, i, q, MSH_LWIN * kLead2, kLead2);
-                pol.shared = hint;
-                pol.relim();
+                if constexpr (kHintFace) {
+                    const int lf = a.phase == 2 ? leader_leaf(a, i, q, MSH_FWIN, kLead)
+                                                : leader_leaf(a, i, q, MSH_LWIN * kLead2, kLead2);
+                    if (lf >= 0) {
+                        pol.test(lf);
+                        if (STATS) ++n_leaves;
+                    }
+                } else {
+                    hint = a.phase == 2 ? hint_from_leaders(a, i, q, MSH_FWIN, kLead)
+                                        : hint_from_leaders(a, i, q, MSH_LWIN * kLead2, kLead2);
+                    pol.shared = hint;
+                    pol.relim();
+                }
             }
         }
         if (a.T == 1) {
@@ -572,7 +636,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     steps = 0;
                     active = true;
                 }
-                const bool can = active && nq <= kLeafQ - 2;
+                const bool can = active && nq <= kLeafQ - (kLeafPark ? 1 : 2);
                 const bool has = nq > 0;
                 const unsigned long long bl = __ballot(has);
                 const unsigned long long bt = __ballot(can);
@@ -595,7 +659,8 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 }
                 if (can) {
                     int l0 = -1, l1 = -1;
-                    active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, l0, l1);
+                    active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, l0, l1,
+                                                                  kLeafQ - nq);
                     enqueue(l0);
                     enqueue(l1);
                     ++steps;
@@ -619,7 +684,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                                         load_tri(static_cast<const TriRec*>(a.leaves), pol.best_leaf, ta, tb, tc, f);
                                         closest_on_triangle(q, ta, tb, tc, o, part);
                                     }
-                                    store_qres(a.res + i, f, 0u, o.x, o.y, o.z);
+                                    store_qres(a.res + i, f, (uint32_t)pol.best_leaf, o.x, o.y, o.z);
                                 } else {
                                     store_qres(a.res + i, MSH_NO_FACE, 0u, NAN, NAN, NAN);
                                 }
@@ -1064,6 +1129,7 @@ static int run_knn(msh_tree* tree, KnnArgs a, const QueryOrder& ord, const SlotO
         MSH_TRY(ws.res.reserve(a.S * sizeof(QRes)));
         a.res = ws.res.as<QRes>();
         a.direct = kDirectOut && !STATS && (MODE == 0 || MODE == 3);
+        a.rec_leaf = a.direct || STATS;
         if (nw && !a.direct) {
             MSH_TRY(ws.res_w.reserve(a.S * (size_t)nw * sizeof(double)));
             a.res_w = ws.res_w.as<double>();
