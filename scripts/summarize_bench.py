@@ -13,6 +13,6 @@ for path in sys.argv[1:]:
         continue
     b = d["breakdown_ms_per_step"]
     r = d["roofline"]
-    print("%-40s %7.1f M q/s %7.2f ms  p1 %6.2f (sl %5.2f lead %5.2f fol %6.2f) p2 %5.2f sort %4.2f  nodes %5.1f leaves %5.2f"
+    print("%-34s %7.1f M q/s %6.2f ms  p1 %6.2f (sl %4.2f lead %5.2f fol %6.2f) p2 %4.2f sort %4.2f  nodes %5.1f leaves %5.2f"
           % (path, d["value"] / 1e6, d["ms_per_step"], b["pass1"], b["pass1_superleaders"], b["pass1_leaders"],
              b["pass1_followers"], b["pass2"], b["sort"], r["nodes_per_query"], r["leaves_per_query"]))
