@@ -13,6 +13,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -375,21 +378,89 @@ static int host_threads() {
     return std::max(1, std::min(n, 32));
 }
 
-static void par_copy(void* dst, const void* src, size_t bytes) {
-    const int nt = bytes < ((size_t)8 << 20) ? 1 : host_threads();
-    if (nt <= 1) {
-        std::memcpy(dst, src, bytes);
-        return;
+// Persistent host copy workers (created on first use, one pool per process): run(tasks) splits a list of
+// memcpys into ~2 MB pieces and executes them on all workers plus the caller, so the pageable <-> pinned
+// staging copies of one pipeline step (inputs of chunk k and outputs of chunk k - 2) move together at the
+// host's memory bandwidth instead of one after the other, without creating threads per copy.
+struct CopyTask {
+    void* dst;
+    const void* src;
+    size_t bytes;
+};
+class CopyPool {
+  public:
+    explicit CopyPool(int n) {
+        for (int i = 0; i < n; ++i) th_.emplace_back([this] { loop(); });
     }
-    std::vector<std::thread> th;
-    const size_t per = (bytes + nt - 1) / nt;
-    for (int k = 0; k < nt; ++k) {
-        const size_t o = (size_t)k * per;
-        if (o >= bytes) break;
-        const size_t n = std::min(per, bytes - o);
-        th.emplace_back([=] { std::memcpy(static_cast<char*>(dst) + o, static_cast<const char*>(src) + o, n); });
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
     }
-    for (auto& x : th) x.join();
+    void run(const std::vector<CopyTask>& tasks) {
+        constexpr size_t kPiece = (size_t)2 << 20;
+        std::vector<CopyTask> pieces;
+        for (const CopyTask& t : tasks)
+            for (size_t o = 0; o < t.bytes; o += kPiece)
+                pieces.push_back({static_cast<char*>(t.dst) + o, static_cast<const char*>(t.src) + o,
+                                  std::min(kPiece, t.bytes - o)});
+        if (pieces.empty()) return;
+        std::lock_guard<std::mutex> job(job_mu_);  // one job at a time
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            pieces_ = &pieces;
+            next_.store(0);
+            ++gen_;
+        }
+        cv_.notify_all();
+        work(&pieces);
+        // every worker that took this job has left it before `pieces` goes away
+        std::unique_lock<std::mutex> g(mu_);
+        done_cv_.wait(g, [&] { return busy_ == 0; });
+        pieces_ = nullptr;
+    }
+
+  private:
+    void work(std::vector<CopyTask>* p) {
+        for (;;) {
+            const size_t i = next_.fetch_add(1);
+            if (i >= p->size()) return;
+            std::memcpy((*p)[i].dst, (*p)[i].src, (*p)[i].bytes);
+        }
+    }
+    void loop() {
+        size_t seen = 0;
+        for (;;) {
+            std::vector<CopyTask>* p = nullptr;
+            {
+                std::unique_lock<std::mutex> g(mu_);
+                cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                p = pieces_;
+                if (p) ++busy_;
+            }
+            if (!p) continue;
+            work(p);
+            std::lock_guard<std::mutex> g(mu_);
+            if (--busy_ == 0) done_cv_.notify_all();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_, job_mu_;
+    std::condition_variable cv_, done_cv_;
+    std::vector<CopyTask>* pieces_ = nullptr;
+    std::atomic<size_t> next_{0};
+    int busy_ = 0;
+    size_t gen_ = 0;
+    bool stop_ = false;
+};
+static CopyPool& copy_pool() {
+    static CopyPool pool(host_threads() - 1);
+    return pool;
 }
 
 // One pipelined host call: rows [0, S) in chunks; inputs (ni arrays of in_w doubles per row) are staged
@@ -429,6 +500,69 @@ static int stage_setup(msh_tree* t, size_t bytes) {
     return MSH_OK;
 }
 
+// MESH_AMD_HOST_REGISTER=1: page-lock the caller's arrays in place instead of staging.  Off by default:
+// registering C3's 5.6 GB of rows per call cost more than the staging copies (C3 numpy path 395 vs 280 ms).
+static bool host_register_enabled() {
+    const char* e = getenv("MESH_AMD_HOST_REGISTER");
+    return e && atoi(e) != 0;
+}
+
+// pipelined() over caller arrays that are page-locked in place: per chunk an H2D copy of the input rows into a
+// device slab (copy stream `up`), the kernels (handle stream), a D2H copy of the output rows straight into
+// the caller's arrays (stream `down`); two device slabs alternate, so chunk k uploads while k - 1 computes and
+// k - 2 downloads.
+template <class Run>
+static int pipelined_registered(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, size_t chunk, Run run) {
+    size_t row = 0;
+    for (const HostArr& a : arrs) row += a.row_bytes;
+    MSH_TRY(stage_setup(t, chunk * row));
+    hipStream_t sc = t->stream, up = t->s_up, down = t->s_down;
+    int st = MSH_OK;
+    hipError_t e = hipSuccess;
+    const size_t nch = (S + chunk - 1) / chunk;
+    for (size_t k = 0; k < nch && st == MSH_OK && e == hipSuccess; ++k) {
+        const int b = (int)(k & 1);
+        const size_t r0 = k * chunk, n = std::min(chunk, S - r0);
+        char* dev = static_cast<char*>(t->d_stage[b]);
+        // the slab's previous chunk (k - 2) must have been downloaded before it is overwritten
+        if (k >= 2 && (e = hipStreamWaitEvent(up, t->e_down[b], 0)) != hipSuccess) break;
+        size_t off = 0;
+        for (const HostArr& a : arrs) {
+            if (a.in && (e = hipMemcpyAsync(dev + off * chunk, static_cast<const char*>(a.in) + r0 * a.row_bytes,
+                                            n * a.row_bytes, hipMemcpyHostToDevice, up)) != hipSuccess)
+                break;
+            off += a.row_bytes;
+        }
+        if (e != hipSuccess || (e = hipEventRecord(t->e_up[b], up)) != hipSuccess ||
+            (e = hipStreamWaitEvent(sc, t->e_up[b], 0)) != hipSuccess)
+            break;
+        std::vector<char*> slabs;
+        off = 0;
+        for (const HostArr& a : arrs) {
+            slabs.push_back(dev + off * chunk);
+            off += a.row_bytes;
+        }
+        if ((st = run(r0, n, slabs)) != MSH_OK) break;
+        if ((e = hipEventRecord(t->e_run[b], sc)) != hipSuccess || (e = hipStreamWaitEvent(down, t->e_run[b], 0)) != hipSuccess)
+            break;
+        off = 0;
+        for (const HostArr& a : arrs) {
+            if (a.out && (e = hipMemcpyAsync(static_cast<char*>(a.out) + r0 * a.row_bytes, dev + off * chunk,
+                                             n * a.row_bytes, hipMemcpyDeviceToHost, down)) != hipSuccess)
+                break;
+            off += a.row_bytes;
+        }
+        if (e == hipSuccess) e = hipEventRecord(t->e_down[b], down);
+    }
+    const hipError_t e1 = hipStreamSynchronize(up), e2 = hipStreamSynchronize(sc), e3 = hipStreamSynchronize(down);
+    if (e == hipSuccess) e = e1 != hipSuccess ? e1 : (e2 != hipSuccess ? e2 : e3);
+    if (st == MSH_OK && e != hipSuccess) {
+        set_error("host call (registered): %s", hipGetErrorString(e));
+        st = e == hipErrorOutOfMemory ? MSH_ENOMEM : MSH_EDEVICE;
+    }
+    return st;
+}
+
 template <class Run>
 static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, size_t chunk, Run run) {
     size_t row = 0;
@@ -464,6 +598,26 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, si
         return st;
     }
     const size_t nch = (S + chunk - 1) / chunk;
+    // Optionally (host_register_enabled) page-lock the caller's arrays in place (hipHostRegister): the copy
+    // engines then move the rows straight between the caller's memory and HBM, with no pageable <-> pinned
+    // staging copies on the host.  Any registration failure falls back to staging.
+    if (host_register_enabled()) {
+        std::vector<std::pair<void*, size_t>> reg;
+        bool ok = true;
+        for (const HostArr& a : arrs) {
+            void* p = a.in ? const_cast<void*>(a.in) : a.out;
+            if (!p) continue;
+            if (hipHostRegister(p, S * a.row_bytes, hipHostRegisterDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                ok = false;
+                break;
+            }
+            reg.emplace_back(p, S * a.row_bytes);
+        }
+        if (ok) st = pipelined_registered(t, S, arrs, chunk, run);
+        for (auto& r : reg) (void)hipHostUnregister(r.first);
+        if (ok) return st;
+    }
     MSH_TRY(stage_setup(t, chunk * row));
     hipStream_t up = t->s_up, down = t->s_down;
     hipEvent_t* e_up = t->e_up;
@@ -475,67 +629,75 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, si
         set_error("%s: %s", what, hipGetErrorString(e));
         st = e == hipErrorOutOfMemory ? MSH_ENOMEM : MSH_EDEVICE;
     };
+    // Step k (slab b = k & 1; a slab holds one chunk's input rows and, after them, its output rows):
+    //   wait for chunk k - 2's download, then copy chunk k - 2's outputs out of slab b AND chunk k's inputs into
+    //   it, on all copy workers at once, while the GPU works on chunk k - 1 in the other slab; then enqueue
+    //   chunk k's upload (copy stream), kernels (handle stream) and download (second copy stream).
+    auto outs_of = [&](size_t kk, std::vector<CopyTask>& tasks) {
+        const int b = (int)(kk & 1);
+        const size_t r0 = kk * chunk, n = std::min(chunk, S - r0);
+        size_t off = 0;
+        for (const HostArr& a : arrs) {
+            if (a.out)
+                tasks.push_back({static_cast<char*>(a.out) + r0 * a.row_bytes, static_cast<char*>(host[b]) + off * chunk,
+                                 n * a.row_bytes});
+            off += a.row_bytes;
+        }
+    };
     do {
         hipError_t e = hipSuccess;
-        for (size_t k = 0; k <= nch && st == MSH_OK; ++k) {
-            if (k < nch) {
-                const int b = (int)(k & 1);
-                const size_t r0 = k * chunk, n = std::min(chunk, S - r0);
-                if (k >= 2 && (e = hipEventSynchronize(e_up[b])) != hipSuccess) { fail(e, "staging"); break; }
-                // inputs: pinned slab of this buffer, array by array
+        for (size_t k = 0; k < nch + 2 && st == MSH_OK; ++k) {
+            const int b = (int)(k & 1);
+            std::vector<CopyTask> tasks;
+            if (k >= 2) {
+                if ((e = hipEventSynchronize(e_down[b])) != hipSuccess) { fail(e, "kernels / download"); break; }
+                outs_of(k - 2, tasks);
+            }
+            const bool have = k < nch;
+            const size_t r0 = k * chunk, n = have ? std::min(chunk, S - r0) : 0;
+            if (have) {
                 size_t off = 0;
                 for (const HostArr& a : arrs) {
                     if (a.in)
-                        par_copy(static_cast<char*>(host[b]) + off * chunk, static_cast<const char*>(a.in) + r0 * a.row_bytes,
-                                 n * a.row_bytes);
+                        tasks.push_back({static_cast<char*>(host[b]) + off * chunk,
+                                         static_cast<const char*>(a.in) + r0 * a.row_bytes, n * a.row_bytes});
                     off += a.row_bytes;
                 }
-                off = 0;
-                for (const HostArr& a : arrs) {
-                    if (a.in && (e = hipMemcpyAsync(static_cast<char*>(dev[b]) + off * chunk,
-                                                    static_cast<char*>(host[b]) + off * chunk, n * a.row_bytes,
-                                                    hipMemcpyHostToDevice, up)) != hipSuccess)
-                        break;
-                    off += a.row_bytes;
-                }
-                if (e == hipSuccess) e = hipEventRecord(e_up[b], up);
-                if (e == hipSuccess) e = hipStreamWaitEvent(sc, e_up[b], 0);
-                if (e == hipSuccess && k >= 2) e = hipStreamWaitEvent(sc, e_down[b], 0);
-                if (e != hipSuccess) { fail(e, "upload"); break; }
-                std::vector<char*> slabs;
-                off = 0;
-                for (const HostArr& a : arrs) {
-                    slabs.push_back(static_cast<char*>(dev[b]) + off * chunk);
-                    off += a.row_bytes;
-                }
-                if ((st = run(r0, n, slabs)) != MSH_OK) break;
-                if ((e = hipEventRecord(e_run[b], sc)) != hipSuccess || (e = hipStreamWaitEvent(down, e_run[b], 0)) != hipSuccess) {
-                    fail(e, "launch");
+            }
+            copy_pool().run(tasks);
+            if (!have) continue;
+            size_t off = 0;
+            for (const HostArr& a : arrs) {
+                if (a.in && (e = hipMemcpyAsync(static_cast<char*>(dev[b]) + off * chunk,
+                                                static_cast<char*>(host[b]) + off * chunk, n * a.row_bytes,
+                                                hipMemcpyHostToDevice, up)) != hipSuccess)
                     break;
-                }
-                off = 0;
-                for (const HostArr& a : arrs) {
-                    if (a.out && (e = hipMemcpyAsync(static_cast<char*>(host[b]) + off * chunk,
-                                                     static_cast<char*>(dev[b]) + off * chunk, n * a.row_bytes,
-                                                     hipMemcpyDeviceToHost, down)) != hipSuccess)
-                        break;
-                    off += a.row_bytes;
-                }
-                if (e == hipSuccess) e = hipEventRecord(e_down[b], down);
-                if (e != hipSuccess) { fail(e, "download"); break; }
+                off += a.row_bytes;
             }
-            if (k >= 1) {  // drain chunk k - 1
-                const int b = (int)((k - 1) & 1);
-                const size_t r0 = (k - 1) * chunk, n = std::min(chunk, S - r0);
-                if ((e = hipEventSynchronize(e_down[b])) != hipSuccess) { fail(e, "kernels / download"); break; }
-                size_t off = 0;
-                for (const HostArr& a : arrs) {
-                    if (a.out)
-                        par_copy(static_cast<char*>(a.out) + r0 * a.row_bytes, static_cast<char*>(host[b]) + off * chunk,
-                                 n * a.row_bytes);
-                    off += a.row_bytes;
-                }
+            if (e == hipSuccess) e = hipEventRecord(e_up[b], up);
+            if (e == hipSuccess) e = hipStreamWaitEvent(sc, e_up[b], 0);
+            if (e != hipSuccess) { fail(e, "upload"); break; }
+            std::vector<char*> slabs;
+            off = 0;
+            for (const HostArr& a : arrs) {
+                slabs.push_back(static_cast<char*>(dev[b]) + off * chunk);
+                off += a.row_bytes;
             }
+            if ((st = run(r0, n, slabs)) != MSH_OK) break;
+            if ((e = hipEventRecord(e_run[b], sc)) != hipSuccess || (e = hipStreamWaitEvent(down, e_run[b], 0)) != hipSuccess) {
+                fail(e, "launch");
+                break;
+            }
+            off = 0;
+            for (const HostArr& a : arrs) {
+                if (a.out && (e = hipMemcpyAsync(static_cast<char*>(host[b]) + off * chunk,
+                                                 static_cast<char*>(dev[b]) + off * chunk, n * a.row_bytes,
+                                                 hipMemcpyDeviceToHost, down)) != hipSuccess)
+                    break;
+                off += a.row_bytes;
+            }
+            if (e == hipSuccess) e = hipEventRecord(e_down[b], down);
+            if (e != hipSuccess) { fail(e, "download"); break; }
         }
     } while (0);
     (void)hipStreamSynchronize(up);

@@ -132,16 +132,28 @@ def c2(reps):
 
 def c3np(reps):
     """C3 through the reference's entry point (the secondary metric of SURVEY §8(d)): 100M host queries in,
-    host arrays out — H2D + sort + traversal + D2H, pipelined through pinned slabs by the library."""
+    host arrays out — H2D + sort + traversal + D2H.  Two host paths of the library, timed on the same call:
+    pageable -> pinned staging slabs copied by the library's host workers (the default) and the caller's arrays
+    page-locked in place (hipHostRegister, MESH_AMD_HOST_REGISTER=1); both must give identical arrays."""
     from mesh_amd import spatialsearch
     import workloads as W
     v, f = W.c3_mesh()
     q = np.random.default_rng(3).uniform(-1.1, 1.1, (100_000_000, 3))
     tree = spatialsearch.aabbtree_compute(v, f)
-    _, wall = timed(lambda: spatialsearch.aabbtree_nearest(tree, q), reps)
+    res = {}
+    outs = {}
+    for mode in ("0", "1"):
+        os.environ["MESH_AMD_HOST_REGISTER"] = mode
+        outs[mode], wall = timed(lambda: spatialsearch.aabbtree_nearest(tree, q), reps)
+        res[mode] = (wall, kernel_ms("nearest"))
+    os.environ.pop("MESH_AMD_HOST_REGISTER", None)
+    same = all(np.array_equal(a, b) for a, b in zip(outs["1"], outs["0"]))
     return {"config": "C3 icosphere (1,003,520 faces), 100M uniform host queries, aabbtree_nearest (numpy API)",
-            "queries_per_s_numpy_api": q.shape[0] / wall, "ms_numpy_api": wall * 1e3,
-            "ms_traversal_kernel": kernel_ms("nearest"), "pcie_bytes_per_query": 56}
+            "queries_per_s_numpy_api": q.shape[0] / res["0"][0], "ms_numpy_api": res["0"][0] * 1e3,
+            "host_path": "pinned staging slabs (4M-row chunks), host copies on the library's copy workers",
+            "queries_per_s_numpy_api_registered": q.shape[0] / res["1"][0], "ms_numpy_api_registered": res["1"][0] * 1e3,
+            "registered_equals_staged": bool(same),
+            "ms_traversal_kernel": res["0"][1], "pcie_bytes_per_query": 56}
 
 
 def c4(reps):

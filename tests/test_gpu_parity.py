@@ -430,6 +430,32 @@ def test_device_api_matches_host_api():
     assert np.array_equal(dpt.cpu().numpy(), pt)
 
 
+def test_host_api_registered_and_staged_agree(monkeypatch):
+    # calls above 16 MB of rows run chunked: the caller's arrays page-locked in place (hipHostRegister) or,
+    # with MESH_AMD_HOST_REGISTER=0, through pinned staging slabs; both equal the device entry point's answer
+    import torch
+    from mesh_amd import spatialsearch
+    from mesh_amd.distributed import nearest_device
+    v, f = W.c2_mesh()
+    q = W.uniform_in_box(v.min(0), v.max(0), 700000, seed=25)  # 39 MB of rows (56 B each): the chunked path
+    monkeypatch.setenv("MESH_AMD_HOST_CHUNK", "262144")      # 3 chunks: both slabs reused
+    t = spatialsearch.aabbtree_compute(v, f)
+    monkeypatch.setenv("MESH_AMD_HOST_REGISTER", "1")
+    reg = spatialsearch.aabbtree_nearest(t, q)
+    monkeypatch.setenv("MESH_AMD_HOST_REGISTER", "0")
+    stg = spatialsearch.aabbtree_nearest(t, q)
+    for a, b in zip(reg, stg):
+        assert np.array_equal(a, b)
+    dq = torch.from_numpy(q).cuda()
+    df = torch.empty(q.shape[0], dtype=torch.int32, device="cuda")
+    dp = torch.empty(q.shape[0], dtype=torch.int32, device="cuda")
+    dpt = torch.empty((q.shape[0], 3), dtype=torch.float64, device="cuda")
+    nearest_device(t, dq, df, dp, dpt)
+    torch.cuda.synchronize()
+    assert np.array_equal(df.cpu().numpy().view(np.uint32), reg[0][0])
+    assert np.array_equal(dpt.cpu().numpy(), reg[2])
+
+
 @pytest.mark.parametrize("name", ["ico", "ico60", "c2", "offset"])
 def test_tree_bounds_contain_primitives(name):
     # every child's quantised oriented box (frame n, t, n x t) contains all vertices below it
