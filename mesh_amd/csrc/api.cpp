@@ -1288,7 +1288,7 @@ struct BlobHeader {
     double origin[3];
     uint32_t node_bytes, leaf_bytes;
 };
-static const uint64_t kBlobMagic = 0x4d53484c42564834ull;  // "MSHLBVH4" (interleaved node frame)
+static const uint64_t kBlobMagic = 0x4d53484c42564835ull;  // "MSHLBVH5" (interleaved node frame, bf16 scales)
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 

@@ -14,7 +14,7 @@
 //                                      its Morton leaf range: area-weighted
 //                                      normal -> node frame (n, t, b = n x t), then both children's vertex
 //                                      extents along the frame (oriented boxes, thin along the surface),
-//                                      quantised to 8 bits against a per-node base and power-of-two scale
+//                                      quantised to 8 bits against a per-node base and bf16 scale
 // All bounds are rounded outward (fp32 round-down lo / round-up hi plus one ulp, then the quantised code
 // rounds down / up, checked against the decoder), so every fp64 primitive lies inside the bounds of
 // every ancestor.  Round 1 also stored an fp32 AABB per child (128-B nodes, filled by a bottom-up refit);
@@ -318,31 +318,19 @@ __device__ inline void leaf_extent(const void* leaves, int i, const ObbFrame& f,
     }
 }
 
-// smallest e in [-126, 127] with 254 * 2^e >= range (127 for a non-finite range)
-__device__ inline int scale_exponent(double range) {
-    if (!(range < 1e38)) return 127;
-    int e = range > 0.0 ? ilogb(range / 254.0) : -126;
-    e = max(-126, min(127, e));
-    while (e < 127 && 254.0 * (double)exp2_scale(e) < range) ++e;
-    while (e > -126 && 254.0 * (double)exp2_scale(e - 1) >= range) --e;
-    return e;
-}
-
 // Write node: frame, and both children's fp32 extents ext[side][lo n t b, hi n t b] quantised against
-// base = min lower bound with scale 2^e per axis (254 * 2^e >= range); lower codes round down and upper
-// codes up, checked with the decoder's own expression, so the decoded box contains the fp32 one.
+// base = min lower bound with a bf16 scale per axis (bf16_scale_up: >= range / 254); lower codes round down
+// and upper codes up, checked with the decoder's own expression, so the decoded box contains the fp32 one.
 __device__ inline void encode_node(BNode* node, const ObbFrame& fr, const float (*ext)[6]) {
     float* f = node->f;
-    float base[3];
-    int ex[3];
+    float base[3], scs[3];
     uint32_t u[12];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         base[k] = fminf(ext[0][k], ext[1][k]);
         const double top = fmax((double)ext[0][3 + k], (double)ext[1][3 + k]);
-        const int e = scale_exponent(top - (double)base[k]);
-        ex[k] = e;
-        const float sc = exp2_scale(e);
+        const float sc = bf16_scale_up(top - (double)base[k]);
+        scs[k] = sc;
 #pragma unroll
         for (int side = 0; side < 2; ++side) {
             const float lo = ext[side][k], hi = ext[side][3 + k];
@@ -360,7 +348,7 @@ __device__ inline void encode_node(BNode* node, const ObbFrame& fr, const float 
     for (int j = 0; j < 3; ++j) w[j] = u[4 * j] | (u[4 * j + 1] << 8) | (u[4 * j + 2] << 16) | (u[4 * j + 3] << 24);
     float h[16];
     encode_frame(h, fr.n, fr.t);
-    encode_scales(h, ex);
+    encode_scales(h, scs);
     *reinterpret_cast<float4*>(f) = make_float4(h[0], h[1], h[2], h[3]);
     *reinterpret_cast<float2*>(f + 4) = make_float2(h[4], h[5]);
     *reinterpret_cast<float4*>(f + 8) = make_float4(base[0], base[1], base[2], __uint_as_float(w[0]));

@@ -37,12 +37,12 @@ def check_mesh(v, f):
     child = fl[:, 6:8].copy().view(np.int32)
     base = fl[:, 8:11]
     u = nodes[:, 44:56].reshape(T - 1, 2, 6).astype(np.float32)
-    # biased exponents (common.h encode_scales): float 14 = E0 << 23 | E2, float 15 = E1 << 23
-    w14 = nodes[:, 56:60].copy().view(np.uint32)[:, 0].astype(np.int64)
-    w15 = nodes[:, 60:64].copy().view(np.uint32)[:, 0].astype(np.int64)
-    ex = np.stack([(w14 >> 23) & 0xff, (w15 >> 23) & 0xff, w14 & 0xff], axis=1).astype(np.int32) - 127
-    scale = np.ldexp(np.float32(1.0), ex).astype(np.float32)  # (T-1, 3)
-    # base + u * 2^e in fp32: the product is exact, the sum rounds once (as fmaf in the kernels)
+    # bf16 scales (common.h encode_scales): float 14 = S0 << 16 | S2, float 15 = S1 << 16
+    w14 = nodes[:, 56:60].copy().view(np.uint32)[:, 0]
+    w15 = nodes[:, 60:64].copy().view(np.uint32)[:, 0]
+    sb = np.stack([w14 & np.uint32(0xFFFF0000), w15 & np.uint32(0xFFFF0000), (w14 << np.uint32(16))], axis=1)
+    scale = np.ascontiguousarray(sb, dtype=np.uint32).view(np.float32)  # (T-1, 3)
+    # base + u * s in fp32: the product is exact, the sum rounds once (as fmaf in the kernels)
     dec = (np.tile(base, 2)[:, None, :] + u * np.tile(scale, 2)[:, None, :]).astype(np.float32)  # (T-1, 2, 6)
     tri = leaves[:, :9].reshape(T, 3, 3) - origin
     llo, lhi = tri.min(1), tri.max(1)

@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
                 mn[ch][k] = lo;
                 mx[ch][k] = hi;
             }
-        // node encoding: fp32 base below both children, power-of-two scale, tightest codes
+        // node encoding: fp32 base below both children, bf16 scale (build.hip encode_node), tightest codes
         BNode bn;
         std::memset(&bn, 0, sizeof(bn));
         float* f = bn.f;
@@ -117,23 +117,21 @@ int main(int argc, char** argv) {
         f[6] = u2f(~0u);
         f[7] = u2f(~1u);
         uint32_t u[12];
-        int ex[3];
+        float scs[3];
         for (int k = 0; k < 3; ++k) {
             float base = (float)std::fmin(mn[0][k], mn[1][k]);
             if ((double)base > std::fmin(mn[0][k], mn[1][k])) base = nextafterf(base, -INFINITY);
             const double range = std::fmax(mx[0][k], mx[1][k]) - (double)base;
-            int e = -126;
-            while (e < 127 && 254.0 * (double)exp2_scale(e) < range) ++e;
-            const float sc = exp2_scale(e);
+            const float sc = bf16_scale_up(range);
             f[kBase + k] = base;
-            ex[k] = e;
+            scs[k] = sc;
             for (int ch = 0; ch < 2; ++ch) {
                 u[6 * ch + k] = code_lo(mn[ch][k], base, sc);
                 u[6 * ch + 3 + k] = code_hi(mx[ch][k], base, sc);
             }
         }
         for (int j = 0; j < 3; ++j) f[11 + j] = u2f(u[4 * j] | (u[4 * j + 1] << 8) | (u[4 * j + 2] << 16) | (u[4 * j + 3] << 24));
-        encode_scales(f, ex);
+        encode_scales(f, scs);
         NodeV nd;
         std::memcpy(&nd, &bn, sizeof(bn));
         // the decoded boxes must contain the points (what the build guarantees); skip codes that cannot

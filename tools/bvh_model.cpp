@@ -1134,6 +1134,9 @@ extern "C" void model_encoded_tree(const double* v, const uint32_t* f, int T, co
 // (area-weighted normal n; centroids projected on t, b; split on the larger spread), 3 as 2 but split at the
 // spatial midpoint of that axis (object partition, unbalanced allowed)
 namespace {
+const double* g_v = nullptr;
+const uint32_t* g_f = nullptr;
+int g_bins = 16;
 int build_oriented_rec(Tree& tr, std::vector<int>& idx, int b, int e, const std::vector<double>& cen,
                        const std::vector<double>& area, int mode) {
     if (e - b == 1) return ~b;
@@ -1159,6 +1162,87 @@ int build_oriented_rec(Tree& tr, std::vector<int>& idx, int b, int e, const std:
             for (int c = 0; c < 3; ++c) C[a][c] += d[a] * d[c];
     }
     double ax[3] = {1, 1, 1};
+    if (mode == 10 || mode == 11) {
+        // binned SAH over the candidate axes x, y, z, t, b: cost N_L * SA_L + N_R * SA_R of the children's boxes
+        // in the node frame (n, t, b) (mode 11: lateral area t-extent * b-extent only)
+        double fr[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+        if (len > 0) {
+            double ee[3] = {0, 0, 0};
+            ee[std::fabs(n[0]) < 0.9 ? 0 : 1] = 1;
+            double d = ee[0] * n[0] + ee[1] * n[1] + ee[2] * n[2], t[3];
+            for (int k = 0; k < 3; ++k) t[k] = ee[k] - d * n[k];
+            double tl = std::sqrt(t[0] * t[0] + t[1] * t[1] + t[2] * t[2]);
+            for (int k = 0; k < 3; ++k) t[k] /= tl;
+            double bb[3] = {n[1] * t[2] - n[2] * t[1], n[2] * t[0] - n[0] * t[2], n[0] * t[1] - n[1] * t[0]};
+            for (int k = 0; k < 3; ++k) { fr[0][k] = n[k]; fr[1][k] = t[k]; fr[2][k] = bb[k]; }
+        }
+        double cands[5][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {fr[1][0], fr[1][1], fr[1][2]}, {fr[2][0], fr[2][1], fr[2][2]}};
+        const int NB = g_bins;
+        double best_cost = 1e300; int best_axis = -1; double best_split = 0;
+        for (int c = 0; c < 5; ++c) {
+            double lo = 1e300, hi = -1e300;
+            for (int i = b; i < e; ++i) {
+                double k = cen[3 * idx[i]] * cands[c][0] + cen[3 * idx[i] + 1] * cands[c][1] + cen[3 * idx[i] + 2] * cands[c][2];
+                lo = std::min(lo, k); hi = std::max(hi, k);
+            }
+            if (!(hi > lo)) continue;
+            std::vector<double> bmin(NB * 3, 1e300), bmax(NB * 3, -1e300);
+            std::vector<int> bcnt(NB, 0);
+            for (int i = b; i < e; ++i) {
+                int t = idx[i];
+                double k = cen[3 * t] * cands[c][0] + cen[3 * t + 1] * cands[c][1] + cen[3 * t + 2] * cands[c][2];
+                int bi = std::min(NB - 1, (int)((k - lo) / (hi - lo) * NB));
+                bcnt[bi]++;
+                for (int vv = 0; vv < 3; ++vv) {
+                    const double* P = g_v + 3 * g_f[3 * t + vv];
+                    for (int a = 0; a < 3; ++a) {
+                        double pr = P[0] * fr[a][0] + P[1] * fr[a][1] + P[2] * fr[a][2];
+                        bmin[3 * bi + a] = std::min(bmin[3 * bi + a], pr);
+                        bmax[3 * bi + a] = std::max(bmax[3 * bi + a], pr);
+                    }
+                }
+            }
+            auto sa = [&](const double* mn, const double* mx) {
+                double x = mx[0] - mn[0], y = mx[1] - mn[1], z = mx[2] - mn[2];
+                return mode == 11 ? y * z : 2 * (x * y + y * z + z * x);
+            };
+            std::vector<double> lcost(NB, 0);
+            double mn[3] = {1e300, 1e300, 1e300}, mx[3] = {-1e300, -1e300, -1e300};
+            int cntL = 0;
+            for (int sp = 1; sp < NB; ++sp) {
+                for (int a = 0; a < 3; ++a) { mn[a] = std::min(mn[a], bmin[3 * (sp - 1) + a]); mx[a] = std::max(mx[a], bmax[3 * (sp - 1) + a]); }
+                cntL += bcnt[sp - 1];
+                lcost[sp] = cntL ? cntL * sa(mn, mx) : -1;
+            }
+            double mn2[3] = {1e300, 1e300, 1e300}, mx2[3] = {-1e300, -1e300, -1e300};
+            int cntR = 0;
+            for (int sp = NB - 1; sp >= 1; --sp) {
+                for (int a = 0; a < 3; ++a) { mn2[a] = std::min(mn2[a], bmin[3 * sp + a]); mx2[a] = std::max(mx2[a], bmax[3 * sp + a]); }
+                cntR += bcnt[sp];
+                if (cntR == 0 || lcost[sp] < 0) continue;
+                double cst = lcost[sp] + cntR * sa(mn2, mx2);
+                if (cst < best_cost) { best_cost = cst; best_axis = c; best_split = lo + (hi - lo) * sp / NB; }
+            }
+        }
+        if (best_axis >= 0) {
+            for (int k = 0; k < 3; ++k) ax[k] = cands[best_axis][k];
+            auto key2 = [&](int x) { return cen[3 * x] * ax[0] + cen[3 * x + 1] * ax[1] + cen[3 * x + 2] * ax[2]; };
+            auto it = std::partition(idx.begin() + b, idx.begin() + e, [&](int x) { return key2(x) < best_split; });
+            int mid = (int)(it - idx.begin());
+            if (mid == b || mid == e) { mid = (b + e) / 2; std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e, [&](int x, int y) { return key2(x) < key2(y); }); }
+            int l = build_oriented_rec(tr, idx, b, mid, cen, area, mode);
+            int r = build_oriented_rec(tr, idx, mid, e, cen, area, mode);
+            tr.nodes[node].c[0] = l;
+            tr.nodes[node].c[1] = r;
+            return node;
+        }
+        int mid = (b + e) / 2;
+        int l = build_oriented_rec(tr, idx, b, mid, cen, area, mode);
+        int r = build_oriented_rec(tr, idx, mid, e, cen, area, mode);
+        tr.nodes[node].c[0] = l;
+        tr.nodes[node].c[1] = r;
+        return node;
+    }
     if (mode == 5 || mode == 6 || mode == 7) {
         // 5: longest axis of the centroid AABB, split at its spatial middle; 6: the longest centroid spread
         // among x, y, z and the node frame's two tangent axes, split at the median
@@ -1246,10 +1330,13 @@ Tree build_tree_kind(const double* v, const uint32_t* f, int T, int kind) {
     std::vector<int> idx(T);
     std::iota(idx.begin(), idx.end(), 0);
     tr.nodes.reserve(T);
-    if (kind >= 100) {  // 100 + log2 K: hybrid over the LBVH
+    g_v = v;
+    g_f = f;
+    if (kind >= 100) {  // 100 + log2 K: hybrid over the LBVH (split mode 7); 200 + log2 K: mode 10; 300: mode 11
         Tree lb = build_lbvh(v, f, T);
         idx = lb.order;
-        hybrid_rec(lb, 0, tr, idx, cen, area, 1 << (kind - 100), 7);
+        const int m = kind >= 300 ? 11 : (kind >= 200 ? 10 : 7);
+        hybrid_rec(lb, 0, tr, idx, cen, area, 1 << (kind % 100), m);
     } else {
         build_oriented_rec(tr, idx, 0, T, cen, area, kind);
     }
