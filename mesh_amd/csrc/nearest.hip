@@ -436,7 +436,7 @@ __device__ inline D3 load_q(const KnnArgs& a, size_t i) {
 #endif
 constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: leader ordering off)
 #ifndef MSH_LEAF_K
-#define MSH_LEAF_K 3
+#define MSH_LEAF_K 4
 #endif
 constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= traversing lanes / kLeafK
 #ifndef MSH_LEAF_Q
@@ -998,7 +998,7 @@ static int device_cus(int dev) {
 }
 
 #ifndef MSH_BUDGET
-#define MSH_BUDGET 1024
+#define MSH_BUDGET 512
 #endif
 constexpr unsigned kBudget = MSH_BUDGET;  // pass-1 node steps per lane before a query is deferred
 #ifndef MSH_BUDGET3

@@ -1343,3 +1343,83 @@ Tree build_tree_kind(const double* v, const uint32_t* f, int T, int kind) {
     tr.order = idx;
     return tr;
 }
+
+
+// ---- leaf screen experiment: lower bound of the triangle distance from the plane distance and the three
+// edge half-planes (max of the in-plane signed edge distances), exact arithmetic; counts, over the leaf
+// tests of a walk with initial bound b0, how many the screen would reject against the best at that moment.
+namespace {
+double tri_lb2(const double* q, const double* A, const double* B, const double* C) {
+    double a[3], b[3], c[3];
+    for (int k = 0; k < 3; ++k) { a[k] = A[k] - q[k]; b[k] = B[k] - q[k]; c[k] = C[k] - q[k]; }
+    double ab[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]}, ac[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+    double n[3] = {ab[1] * ac[2] - ab[2] * ac[1], ab[2] * ac[0] - ab[0] * ac[2], ab[0] * ac[1] - ab[1] * ac[0]};
+    double nl = std::sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+    if (!(nl > 0)) return 0;
+    double h = (n[0] * a[0] + n[1] * a[1] + n[2] * a[2]) / nl;
+    const double* P[3] = {a, b, c};
+    double smax = 0;
+    for (int e = 0; e < 3; ++e) {
+        const double* p1 = P[e];
+        const double* p2 = P[(e + 1) % 3];
+        double d[3] = {p2[0] - p1[0], p2[1] - p1[1], p2[2] - p1[2]};
+        double m[3] = {d[1] * n[2] - d[2] * n[1], d[2] * n[0] - d[0] * n[2], d[0] * n[1] - d[1] * n[0]};
+        double ml = std::sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+        if (!(ml > 0)) continue;
+        double sd = -(m[0] * p1[0] + m[1] * p1[1] + m[2] * p1[2]) / ml;
+        smax = std::max(smax, sd);
+    }
+    return h * h + smax * smax;
+}
+}  // namespace
+extern "C" void model_leaf_screen(const double* v, const uint32_t* f, int T, const double* q, long S, const double* b0,
+                                  uint32_t* tests_out, uint32_t* rejects_out, uint32_t* improves_out) {
+    ObbTree t = make_obb_tree(v, f, T);
+#pragma omp parallel for schedule(dynamic, 64)
+    for (long i = 0; i < S; ++i) {
+        const double* qq = q + 3 * i;
+        double best = b0 ? b0[i] : std::numeric_limits<double>::infinity();
+        uint32_t nt = 0, nr = 0, ni = 0;
+        std::vector<std::pair<int, double>> st{{0, 0.0}};
+        while (!st.empty()) {
+            auto e = st.back();
+            st.pop_back();
+            if (e.second > best) continue;
+            int node = e.first;
+            for (;;) {
+                const Node& n = t.tr.nodes[node];
+                double d[2];
+                bool h[2];
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    d[s2] = obb_d2(qq, t.ob[2 * node + s2]);
+                    h[s2] = d[s2] <= best;
+                    if (h[s2] && n.c[s2] < 0) {
+                        int fc = t.tr.order[~n.c[s2]];
+                        const uint32_t* ff = f + 3 * fc;
+                        const double* A = v + 3 * ff[0]; const double* B = v + 3 * ff[1]; const double* C = v + 3 * ff[2];
+                        double lb = tri_lb2(qq, A, B, C);
+                        double dd = tri_d2(qq, A, B, C);
+                        ++nt;
+                        if (lb > best * (1 + 1e-6)) ++nr;
+                        if (dd < best) { ++ni; best = dd; }
+                        h[s2] = false;
+                    }
+                }
+                h[0] = h[0] && d[0] <= best;
+                h[1] = h[1] && d[1] <= best;
+                if (h[0] && h[1]) {
+                    int nr2 = d[1] < d[0] ? 1 : 0;
+                    st.push_back({n.c[1 - nr2], d[1 - nr2]});
+                    node = n.c[nr2];
+                    continue;
+                }
+                if (h[0]) { node = n.c[0]; continue; }
+                if (h[1]) { node = n.c[1]; continue; }
+                break;
+            }
+        }
+        tests_out[i] = nt;
+        rejects_out[i] = nr;
+        improves_out[i] = ni;
+    }
+}
