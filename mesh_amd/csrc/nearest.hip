@@ -439,6 +439,12 @@ constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: lea
 #define MSH_LEAF_K 4
 #endif
 constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= traversing lanes / kLeafK
+#ifndef MSH_LEAF_ROUND
+#define MSH_LEAF_ROUND 2
+#endif
+// leaves a lane tests per leaf phase: fewer rounds per phase keep more of the wave's lanes busy in each (the
+// rounds of a phase run until its fullest queue is empty)
+constexpr int kLeafRound = MSH_LEAF_ROUND;
 #ifndef MSH_LEAF_Q
 #define MSH_LEAF_Q 3
 #endif
@@ -609,15 +615,17 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 q0 = x;
                 ++nq;
             };
-            auto test_queue = [&]() {
-                // one copy of the fp64 construction in the code (a loop over the queue), not one per entry
+            // tests up to `most` queued leaves, newest first (one copy of the fp64 construction in the code: a
+            // loop over the queue, not one per entry)
+            auto test_queue = [&](int most) {
+                const int n = min(nq, most);
 #pragma nounroll
-                for (int k = 0; k < nq; ++k) {
+                for (int k = 0; k < n; ++k) {
                     pol.test(q0);
                     q0 = q1;
                     q1 = q2;
                 }
-                nq = 0;
+                nq -= n;
             };
             size_t steps = 0;
             unsigned tot = 0;  // STATS: node steps of this lane, restarts included
@@ -648,8 +656,8 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         u_leaf_lanes += __popcll(bl);
                     }
                     if (has) {
-                        if (STATS) n_leaves += nq;
-                        test_queue();
+                        if (STATS) n_leaves += min(nq, kLeafRound);
+                        test_queue(kLeafRound);
                     }
                     continue;
                 }
@@ -670,7 +678,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
                         if (slot < a.max_deferred) {
                             if (STATS) n_leaves += nq;
-                            test_queue();
+                            test_queue(kLeafQ);
                             if ((a.phase == 1 || a.phase == 3) && a.res) {
                                 // later phases take hints from this slot before pass 2 answers it: publish the
                                 // closest point of the best face so far (a point on the mesh, so a valid upper
