@@ -198,20 +198,6 @@ __device__ inline D3 project_line(const D3& p1, const D3& p2, const D3& q) {
     return D3{p1.x + lambda * ldx, p1.y + lambda * ldy, p1.z + lambda * ldz};
 }
 
-// edge test of the reference's is_inside_triangle_3_aux (nearest_point_triangle_3.h:22-60)
-__device__ inline bool edge_test(const D3& w, const D3& p1, const D3& p2, const D3& q, D3& result, bool& outside) {
-    const D3 e = vsub(p2, p1), pq = vsub(q, p1);
-    const D3 v = vcross(e, pq);
-    if (vdot(v, w) < 0.0) {
-        if (vdot(pq, e) >= 0.0 && vdot(vsub(q, p2), vsub(p1, p2)) >= 0.0) {
-            result = project_line(p1, p2, q);
-            return true;
-        }
-        outside = true;
-    }
-    return false;
-}
-
 __device__ inline D3 seg_closest(const D3& a, const D3& b, const D3& p) {
     const D3 ab = vsub(b, a);
     const double den = vdot(ab, ab);
@@ -244,12 +230,26 @@ __device__ inline double closest_on_triangle(const D3& o, const D3& t0, const D3
     const double lambda = num / den;
     const D3 p = D3{o.x - lambda * a, o.y - lambda * b, o.z - lambda * c};
     const D3 w = vcross(vsub(t1, t0), vsub(t2, t1));
-    bool outside = false;
-    D3 r;
-    if (edge_test(w, t0, t1, p, r, outside)) { out = r; part = 1; }
-    else if (edge_test(w, t1, t2, p, r, outside)) { out = r; part = 2; }
-    else if (edge_test(w, t2, t0, p, r, outside)) { out = r; part = 3; }
-    else if (outside) {
+    // is_inside_triangle_3_aux (nearest_point_triangle_3.h:22-60) for the edges (t0, t1), (t1, t2), (t2, t0)
+    // in that order: the first edge whose side test is negative and whose two projections are >= 0 gives
+    // the answer (projection onto its line); else any negative side test means a vertex, else p.  All three
+    // tests are evaluated without branches (lanes of a leaf phase test different triangles, and a divergent
+    // block per edge would run once per edge for the wave), with CGAL's operand order:
+    // (q - p2) . (p1 - p2) is -((q - p2) . e) exactly (negation commutes with rounding), so the second
+    // projection test of edge k is pq[k + 1] . e[k] <= 0.
+    const D3 e0 = vsub(t1, t0), e1 = vsub(t2, t1), e2 = vsub(t0, t2);
+    const D3 q0 = vsub(p, t0), q1 = vsub(p, t1), q2 = vsub(p, t2);
+    const bool n0 = vdot(vcross(e0, q0), w) < 0.0, n1 = vdot(vcross(e1, q1), w) < 0.0,
+               n2 = vdot(vcross(e2, q2), w) < 0.0;
+    const bool k0 = n0 && vdot(q0, e0) >= 0.0 && vdot(q1, e0) <= 0.0;
+    const bool k1 = n1 && vdot(q1, e1) >= 0.0 && vdot(q2, e1) <= 0.0;
+    const bool k2 = n2 && vdot(q2, e2) >= 0.0 && vdot(q0, e2) <= 0.0;
+    if (k0 || k1 || k2) {
+        const D3& p1 = k0 ? t0 : (k1 ? t1 : t2);
+        const D3& p2 = k0 ? t1 : (k1 ? t2 : t0);
+        out = project_line(p1, p2, p);
+        part = k0 ? 1 : (k1 ? 2 : 3);
+    } else if (n0 || n1 || n2) {
         const double d0 = sqdist(p, t0), d1 = sqdist(p, t1), d2 = sqdist(p, t2);
         if (d1 >= d0 && d2 >= d0) { out = t0; part = 4; }
         else if (d2 >= d1) { out = t1; part = 5; }

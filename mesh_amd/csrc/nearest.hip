@@ -290,46 +290,47 @@ struct Walker {
     // leaf is parked on the stack as an entry (~leaf, bound); a parked leaf popped later becomes `node`
     // (negative) and is handed back by the next step without a node load.  So a lane keeps traversing while
     // its queue has room for one leaf, instead of stopping as soon as a node could add two.
+    // One push site and one pop site (each is a divergent loop or branch in the wave-synchronous caller, so
+    // every extra copy runs serially for the lanes that take it); a parked leaf goes straight to `node`,
+    // since the stack entry it would get is the one the following pop returns.
     template <class Pol, bool STATS>
     __device__ inline bool step_collect(const BNode* __restrict__ nodes, const QF& qf, const Pol& pol,
                                         uint2* __restrict__ lds, uint2* __restrict__ spill, unsigned& n_nodes, int& p0,
                                         int& p1, int room = 2) {
+        bool more = false;  // `node` holds the next entry; otherwise pop
         if (node < 0) {
             p0 = ~node;
-            return pop(pol, lds, spill);
+        } else {
+            const NodeV nd = load_node(nodes, node);
+            if (STATS) ++n_nodes;
+            float d0, d1;
+            node_child_bounds(nd, qf, d0, d1);
+            const int c0 = nd.child(0), c1 = nd.child(1);
+            const float lim = pol.limf;
+            const bool h0 = d0 <= lim, h1 = d1 <= lim;
+            const bool l0 = h0 && c0 < 0, l1 = h1 && c1 < 0;  // leaf children within the bound
+            const bool i0 = h0 && c0 >= 0, i1 = h1 && c1 >= 0;  // internal children within the bound
+            const bool first1 = d1 < d0;                         // child 1 is the nearer
+            if (l0 && l1) {
+                if (room < 2) {  // two leaves, room for one: queue the nearer, park the farther
+                    p0 = first1 ? ~c1 : ~c0;
+                    node = first1 ? c0 : c1;
+                    more = true;
+                } else {
+                    p0 = ~c0;
+                    p1 = ~c1;
+                }
+            } else {
+                if (l0) p0 = ~c0;
+                if (l1) p0 = ~c1;
+                if (i0 && i1) push(make_uint2((unsigned)(first1 ? c0 : c1), __float_as_uint(first1 ? d0 : d1)), lds, spill);
+                if (i0 || i1) {
+                    node = (i0 && i1) ? (first1 ? c1 : c0) : (i0 ? c0 : c1);
+                    more = true;
+                }
+            }
         }
-        const NodeV nd = load_node(nodes, node);
-        if (STATS) ++n_nodes;
-        float d0, d1;
-        node_child_bounds(nd, qf, d0, d1);
-        const int c0 = nd.child(0), c1 = nd.child(1);
-        const float lim = pol.limf;
-        bool h0 = d0 <= lim, h1 = d1 <= lim;
-        if (room < 2 && h0 && h1 && c0 < 0 && c1 < 0) {  // two leaves, room for one: park the farther
-            const bool far0 = d0 > d1;
-            p0 = far0 ? ~c1 : ~c0;
-            push(make_uint2((unsigned)(far0 ? c0 : c1), __float_as_uint(far0 ? d0 : d1)), lds, spill);
-            return pop(pol, lds, spill);
-        }
-        if (h0 && c0 < 0) {
-            p0 = ~c0;
-            h0 = false;
-        }
-        if (h1 && c1 < 0) {
-            if (p0 < 0) p0 = ~c1;
-            else p1 = ~c1;
-            h1 = false;
-        }
-        if (h0 && h1) {
-            int nearc = c0, farc = c1;
-            float dfar = d1;
-            if (d1 < d0) { nearc = c1; farc = c0; dfar = d0; }
-            push(make_uint2((unsigned)farc, __float_as_uint(dfar)), lds, spill);
-            node = nearc;
-            return true;
-        }
-        if (h0) { node = c0; return true; }
-        if (h1) { node = c1; return true; }
+        if (more) return true;
         return pop(pol, lds, spill);
     }
 };
@@ -627,7 +628,8 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 }
                 nq -= n;
             };
-            size_t steps = 0;
+            unsigned steps = 0;
+            const unsigned max_steps = (unsigned)min(a.T, (size_t)UINT_MAX);
             unsigned tot = 0;  // STATS: node steps of this lane, restarts included
             // Wave-synchronous loop.  Lanes that reach leaves queue them; a lane keeps traversing while
             // its queue has room for a node's two children.  Leaf tests run when the blocked lanes are
@@ -673,7 +675,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     enqueue(l1);
                     ++steps;
                     if (STATS) ++tot;
-                    if (active && steps >= a.T) active = false;  // each node is entered once: corrupt tree
+                    if (active && steps >= max_steps) active = false;  // each node is entered once: corrupt tree
                     if (active && steps == a.budget) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
                         if (slot < a.max_deferred) {
