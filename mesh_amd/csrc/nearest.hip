@@ -149,18 +149,27 @@ struct TriPol {
     // Ericson pretest before it, tri_d2_lo, rejected some leaves early but cost more than it saved: C3
     // pass 1 137 -> 117 ms without it.)
     __device__ void test(int leaf) {
-        D3 a, b, c;
         uint32_t face;
+        const double d2 = eval(leaf, q, face);
+        if (offer(d2, face, leaf)) relim();
+    }
+    // exact squared distance from x (this lane's query or another lane's) to the leaf's triangle
+    __device__ double eval(int leaf, const D3& x, uint32_t& face) const {
+        D3 a, b, c;
         load_tri(tris, leaf, a, b, c, face);
         D3 o;
         int part;
-        const double d2 = closest_on_triangle(q, a, b, c, o, part);
+        return closest_on_triangle(x, a, b, c, o, part);
+    }
+    // lexicographic (d2, face) update; the caller refreshes limf
+    __device__ bool offer(double d2, uint32_t face, int leaf) {
         if (d2 < best || (d2 == best && face < best_face)) {
             best = d2;
             best_face = face;
             best_leaf = leaf;
-            relim();
+            return true;
         }
+        return false;
     }
 };
 
@@ -552,13 +561,19 @@ __device__ inline int leader_leaf(const KnnArgs& a, size_t i, const D3& q, size_
 #ifndef MSH_WAVES
 #define MSH_WAVES 4
 #endif
+#ifndef MSH_COMPACT
+#define MSH_COMPACT 1
+#endif
 // (not for the normals metric, MODE 1, whose larger live set would spill in the node step)
 #define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 1 : MSH_WAVES)))
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
+    constexpr bool kCompact = (MODE == 0 || MODE == 3) && MSH_COMPACT;
+    __shared__ uint2 lent[kCompact ? kBlock * kLeafQ : 1];  // compacted leaf phases: kLeafQ entries per lane
     const int tid = threadIdx.x, lane = tid & 63;
     uint2* lds = stk + tid;
+    uint2* ent = lent + (kCompact ? (tid >> 6) * 64 * kLeafQ : 0);
     uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
     const unsigned group = blockIdx.x & 7u;
     unsigned long long u_trav_it = 0, u_trav_lanes = 0, u_leaf_it = 0, u_leaf_lanes = 0;  // STATS: wave iterations
@@ -568,20 +583,25 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         if (lane == 0) tile = dequeue_tile(a.counters, a.ntiles, group);
         tile = __shfl(tile, 0);
         if (tile >= a.ntiles) break;
+        // every lane of the wave stays in the tile's loops (compacted leaf phases deal entries to all 64 lanes);
+        // a lane without a query (past the phase's units, or a non-finite row) only helps
         const size_t k = (size_t)tile * 64 + lane;
-        if (k >= a.nunits) continue;
-        const size_t i = slot_of(a, k);
-        if (i >= a.S) continue;
-        const D3 q = load_q(a, i);
-        if (a.inv_w && !a.direct) a.inv_w[a.qperm[i]] = (uint32_t)i;
+        size_t i = 0;
+        bool live = k < a.nunits;
+        if (live) {
+            i = slot_of(a, k);
+            live = i < a.S;
+        }
+        const D3 q = live ? load_q(a, i) : D3{0.0, 0.0, 0.0};
+        if (live && a.inv_w && !a.direct) a.inv_w[a.qperm[i]] = (uint32_t)i;
         auto pol = make_pol<MODE>(a, i, q);
-        if (!finite3(q)) {  // no distance is defined: NO_FACE / NaN, no traversal
+        const bool fin = live && finite3(q);
+        if (live && !fin) {  // no distance is defined: NO_FACE / NaN, no traversal
             if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
-            continue;
         }
         double hint = INFINITY;
         if constexpr (MODE == 0 || MODE == 3) {
-            if (a.phase == 2 || (a.phase == 1 && kLead2 > 0)) {
+            if (fin && (a.phase == 2 || (a.phase == 1 && kLead2 > 0))) {
                 if constexpr (kHintFace) {
                     const int lf = a.phase == 2 ? leader_leaf(a, i, q, MSH_FWIN, kLead)
                                                 : leader_leaf(a, i, q, MSH_LWIN * kLead2, kLead2);
@@ -598,13 +618,18 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             }
         }
         if (a.T == 1) {
-            pol.test(0);
-            if (STATS) ++n_leaves;
-        } else {
+            if (fin) {
+                pol.test(0);
+                if (STATS) ++n_leaves;
+                if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
+            }
+            continue;
+        }
+        {
             QF qf;
             const int root = query_root(a, i, q, qf);
             Walker w{root, 0};
-            bool active = true, deferred = false;
+            bool active = fin, deferred = false;
             // leaf children waiting for a wave-wide leaf phase: a per-lane queue of up to kLeafQ leaves
             int q0 = -1, q1 = -1, q2 = -1, nq = 0;
             static_assert(kLeafQ >= 2 && kLeafQ <= 3, "leaf queue: 2 or 3 entries");
@@ -653,13 +678,54 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 if ((bl | bt) == 0ull) break;
                 const int nb = __popcll(__ballot(has && !can)), nt = __popcll(bt);
                 if (bl != 0ull && (nt == 0 || kLeafK * nb >= nt)) {
-                    if (STATS && lane == 0) {
-                        ++u_leaf_it;
-                        u_leaf_lanes += __popcll(bl);
-                    }
-                    if (has) {
-                        if (STATS) n_leaves += min(nq, kLeafRound);
-                        test_queue(kLeafRound);
+                    if constexpr (kCompact) {
+                        // Compacted leaf phase: the wave's queued leaves (newest first per lane) are dealt to
+                        // its 64 lanes, one (leaf, owner) entry each; a lane tests its entry against the
+                        // owner's query (ds_bpermute) and each owner takes its entries' (d2, face) back.  The
+                        // fp64 construction then runs with (nearly) every lane busy instead of only the
+                        // lanes that hold leaves.
+                        const unsigned long long lt = (1ull << lane) - 1ull;
+                        const unsigned long long m1 = bl, m2 = __ballot(nq >= 2), m3 = __ballot(nq >= 3);
+                        const int pos = __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
+                        const int E = __popcll(m1) + __popcll(m2) + __popcll(m3);
+                        if (nq >= 1) ent[pos] = make_uint2((unsigned)q0, (unsigned)lane);
+                        if (nq >= 2) ent[pos + 1] = make_uint2((unsigned)q1, (unsigned)lane);
+                        if (nq >= 3) ent[pos + 2] = make_uint2((unsigned)q2, (unsigned)lane);
+                        asm volatile("" ::: "memory");  // the wave's LDS accesses run in order
+                        bool better = false;
+                        for (int base = 0; base < E; base += 64) {
+                            const uint2 en = ent[min(base + lane, E - 1)];  // lanes past E repeat the last entry
+                            const int src = (int)en.y;
+                            const D3 x = D3{__shfl(pol.q.x, src), __shfl(pol.q.y, src), __shfl(pol.q.z, src)};
+                            uint32_t f;
+                            const double d2 = pol.eval((int)en.x, x, f);
+                            if (STATS && base + lane < E) ++n_leaves;
+#pragma unroll
+                            for (int e = 0; e < 3; ++e) {
+                                const int at = pos + e - base;
+                                const bool mine = e < nq && at >= 0 && at < 64;
+                                const int from = mine ? at : lane;
+                                const double dk = __shfl(d2, from);
+                                const uint32_t fk = (uint32_t)__shfl((int)f, from);
+                                if (mine) better |= pol.offer(dk, fk, e == 0 ? q0 : (e == 1 ? q1 : q2));
+                            }
+                        }
+                        asm volatile("" ::: "memory");
+                        if (better) pol.relim();
+                        if (STATS && lane == 0) {
+                            u_leaf_it += (unsigned long long)((E + 63) / 64);
+                            u_leaf_lanes += (unsigned long long)E;
+                        }
+                        nq = 0;
+                    } else {
+                        if (STATS && lane == 0) {
+                            ++u_leaf_it;
+                            u_leaf_lanes += __popcll(bl);
+                        }
+                        if (has) {
+                            if (STATS) n_leaves += min(nq, kLeafRound);
+                            test_queue(kLeafRound);
+                        }
                     }
                     continue;
                 }
@@ -735,7 +801,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             }
             if (deferred) continue;
         }
-        if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
+        if (fin && (!STATS || a.res)) write_result<MODE>(a, i, q, pol);
     }
     if (STATS) {
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
