@@ -446,7 +446,7 @@ __device__ inline D3 load_q(const KnnArgs& a, size_t i) {
 #endif
 constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: leader ordering off)
 #ifndef MSH_LEAF_K
-#define MSH_LEAF_K 4
+#define MSH_LEAF_K 64
 #endif
 constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= traversing lanes / kLeafK
 #ifndef MSH_LEAF_ROUND
@@ -455,11 +455,15 @@ constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= t
 // leaves a lane tests per leaf phase: fewer rounds per phase keep more of the wave's lanes busy in each (the
 // rounds of a phase run until its fullest queue is empty)
 constexpr int kLeafRound = MSH_LEAF_ROUND;
+#ifndef MSH_LEAF_FULL
+#define MSH_LEAF_FULL 0
+#endif
+constexpr int kLeafFull = MSH_LEAF_FULL;  // compacted phases: also flush once the wave holds this many leaves
 #ifndef MSH_LEAF_Q
-#define MSH_LEAF_Q 3
+#define MSH_LEAF_Q 4
 #endif
 constexpr int kLeafQ = MSH_LEAF_Q;  // leaves a lane may hold before it stops traversing (2..4)
-static_assert(kLeafQ >= 2 && kLeafQ <= 4, "kLeafQ must be 2, 3 or 4");
+static_assert(kLeafQ >= 2 && kLeafQ <= 8, "kLeafQ: 2..8");
 #ifndef MSH_LEAF_PARK
 #define MSH_LEAF_PARK 1
 #endif
@@ -631,11 +635,11 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             Walker w{root, 0};
             bool active = fin, deferred = false;
             // leaf children waiting for a wave-wide leaf phase: a per-lane queue of up to kLeafQ leaves
-            int q0 = -1, q1 = -1, q2 = -1, nq = 0;
-            static_assert(kLeafQ >= 2 && kLeafQ <= 3, "leaf queue: 2 or 3 entries");
+            int q0 = -1, q1 = -1, q2 = -1, q3 = -1, nq = 0;
             // a shift register (no dynamic index, so the queue stays in VGPRs, not in scratch)
             auto enqueue = [&](int x) {
                 if (x < 0) return;
+                if (kLeafQ > 3) q3 = q2;
                 q2 = q1;
                 q1 = q0;
                 q0 = x;
@@ -650,6 +654,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     pol.test(q0);
                     q0 = q1;
                     q1 = q2;
+                    if (kLeafQ > 3) q2 = q3;
                 }
                 nq -= n;
             };
@@ -677,7 +682,12 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 const unsigned long long bt = __ballot(can);
                 if ((bl | bt) == 0ull) break;
                 const int nb = __popcll(__ballot(has && !can)), nt = __popcll(bt);
-                if (bl != 0ull && (nt == 0 || kLeafK * nb >= nt)) {
+                bool flush = nt == 0 || kLeafK * nb >= nt;
+                if constexpr (kCompact && kLeafFull > 0) {
+                    if (!flush && bl != 0ull)
+                        flush = __popcll(bl) + __popcll(__ballot(nq >= 2)) + __popcll(__ballot(nq >= 3)) >= kLeafFull;
+                }
+                if (bl != 0ull && flush) {
                     if constexpr (kCompact) {
                         // Compacted leaf phase: the wave's queued leaves (newest first per lane) are dealt to
                         // its 64 lanes, one (leaf, owner) entry each; a lane tests its entry against the
@@ -685,12 +695,14 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         // fp64 construction then runs with (nearly) every lane busy instead of only the
                         // lanes that hold leaves.
                         const unsigned long long lt = (1ull << lane) - 1ull;
-                        const unsigned long long m1 = bl, m2 = __ballot(nq >= 2), m3 = __ballot(nq >= 3);
-                        const int pos = __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt);
-                        const int E = __popcll(m1) + __popcll(m2) + __popcll(m3);
+                        const unsigned long long m1 = bl, m2 = __ballot(nq >= 2), m3 = __ballot(nq >= 3),
+                                                 m4 = kLeafQ > 3 ? __ballot(nq >= 4) : 0ull;
+                        const int pos = __popcll(m1 & lt) + __popcll(m2 & lt) + __popcll(m3 & lt) + __popcll(m4 & lt);
+                        const int E = __popcll(m1) + __popcll(m2) + __popcll(m3) + __popcll(m4);
                         if (nq >= 1) ent[pos] = make_uint2((unsigned)q0, (unsigned)lane);
                         if (nq >= 2) ent[pos + 1] = make_uint2((unsigned)q1, (unsigned)lane);
                         if (nq >= 3) ent[pos + 2] = make_uint2((unsigned)q2, (unsigned)lane);
+                        if (kLeafQ > 3 && nq >= 4) ent[pos + 3] = make_uint2((unsigned)q3, (unsigned)lane);
                         asm volatile("" ::: "memory");  // the wave's LDS accesses run in order
                         bool better = false;
                         for (int base = 0; base < E; base += 64) {
@@ -701,13 +713,13 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                             const double d2 = pol.eval((int)en.x, x, f);
                             if (STATS && base + lane < E) ++n_leaves;
 #pragma unroll
-                            for (int e = 0; e < 3; ++e) {
+                            for (int e = 0; e < kLeafQ; ++e) {
                                 const int at = pos + e - base;
                                 const bool mine = e < nq && at >= 0 && at < 64;
                                 const int from = mine ? at : lane;
                                 const double dk = __shfl(d2, from);
                                 const uint32_t fk = (uint32_t)__shfl((int)f, from);
-                                if (mine) better |= pol.offer(dk, fk, e == 0 ? q0 : (e == 1 ? q1 : q2));
+                                if (mine) better |= pol.offer(dk, fk, e == 0 ? q0 : (e == 1 ? q1 : (e == 2 ? q2 : q3)));
                             }
                         }
                         asm volatile("" ::: "memory");
