@@ -232,6 +232,25 @@ int msh_timing_enable(int on);
 int msh_timing_get(const char* name, double* ms, int64_t* count);
 int msh_timing_reset(void);
 
+/* ---- page-locked result pool (host-buffer entry points) ----
+ * Replaces nothing in the reference: its methods return fresh numpy arrays (PyArray_SimpleNew,
+ * spatialsearchmodule.cpp:196-206), which the shims keep doing for small calls.  For large calls the
+ * shims carve the result arrays out of one block of this pool instead, so the host-buffer entry points
+ * copy results from HBM straight into them (no pinned staging copy, and no first-touch page faults of
+ * fresh pages: on C3, 3.2 GB of results per call).  A block returns to the pool when the last array
+ * over it dies.
+ *  - msh_host_alloc: a block of >= bytes (2 MB granules), reusing a free block of at most 5/4 the
+ *    size; blocks are page-locked with hipHostMalloc.  MSH_ENOMEM when the pool would outgrow its
+ *    cap (MESH_AMD_PINNED_POOL_MB, default 16384; 0 disables the pool) even after releasing its free
+ *    blocks: the caller then allocates ordinary pageable arrays.
+ *  - msh_host_free: returns a block (any pointer msh_host_alloc gave) to the pool; NULL is ignored.
+ *  - msh_host_pool_trim: releases every free block; msh_host_pool_bytes: bytes held (live + free).
+ * Host-buffer entry points recognise output arrays that lie inside one live block. */
+int msh_host_alloc(size_t bytes, void** out);
+void msh_host_free(void* p);
+int msh_host_pool_trim(void);
+size_t msh_host_pool_bytes(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -17,6 +17,7 @@
 #include <condition_variable>
 #include <functional>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -473,16 +474,20 @@ struct HostArr {
     size_t row_bytes;
 };
 
-static void release_stage(msh_tree* t) {
+static void release_stage(msh_tree* t, bool host, bool dev) {
     for (int b = 0; b < 2; ++b) {
-        if (t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
-        if (t->d_stage[b]) (void)hipFree(t->d_stage[b]);
-        t->h_stage[b] = t->d_stage[b] = nullptr;
+        if (host && t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
+        if (dev && t->d_stage[b]) (void)hipFree(t->d_stage[b]);
+        if (host) t->h_stage[b] = nullptr;
+        if (dev) t->d_stage[b] = nullptr;
     }
-    t->stage_bytes = 0;
+    if (host) t->hstage_bytes = 0;
+    if (dev) t->stage_bytes = 0;
 }
+static void release_stage(msh_tree* t) { release_stage(t, true, true); }
 
-static int stage_setup(msh_tree* t, size_t bytes) {
+// copy streams, events, and two host slabs of >= host_bytes and two device slabs of >= dev_bytes (grow-only)
+static int stage_setup(msh_tree* t, size_t host_bytes, size_t dev_bytes) {
     if (!t->s_up) MSH_HIP(hipStreamCreateWithFlags(&t->s_up, hipStreamNonBlocking));
     if (!t->s_down) MSH_HIP(hipStreamCreateWithFlags(&t->s_down, hipStreamNonBlocking));
     for (int b = 0; b < 2; ++b) {
@@ -490,13 +495,16 @@ static int stage_setup(msh_tree* t, size_t bytes) {
         if (!t->e_run[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_run[b], hipEventDisableTiming));
         if (!t->e_down[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_down[b], hipEventDisableTiming));
     }
-    if (t->stage_bytes >= bytes) return MSH_OK;
-    release_stage(t);
-    for (int b = 0; b < 2; ++b) {
-        MSH_HIP(hipHostMalloc(&t->h_stage[b], bytes, hipHostMallocDefault));
-        MSH_HIP(hipMalloc(&t->d_stage[b], bytes));
+    if (t->hstage_bytes < host_bytes) {
+        release_stage(t, true, false);
+        for (int b = 0; b < 2; ++b) MSH_HIP(hipHostMalloc(&t->h_stage[b], host_bytes, hipHostMallocDefault));
+        t->hstage_bytes = host_bytes;
     }
-    t->stage_bytes = bytes;
+    if (t->stage_bytes < dev_bytes) {
+        release_stage(t, false, true);
+        for (int b = 0; b < 2; ++b) MSH_HIP(hipMalloc(&t->d_stage[b], dev_bytes));
+        t->stage_bytes = dev_bytes;
+    }
     return MSH_OK;
 }
 
@@ -507,6 +515,105 @@ static bool host_register_enabled() {
     return e && atoi(e) != 0;
 }
 
+// Rows per pipelined chunk (MESH_AMD_HOST_CHUNK overrides).  Larger chunks keep the sorted traversal coherent
+// and cut per-chunk launch tails; measured on C3 (100M queries): staging 4M 155 ms, 8M 137, 16M 134, 32M 150;
+// results in pinned pool arrays 4M 197 ms, 16M 145, 32M 125.
+static size_t host_chunk(bool direct_out) {
+    const char* e = getenv("MESH_AMD_HOST_CHUNK");
+    const long long c = e ? atoll(e) : 0;
+    if (c > 0) return (size_t)c;
+    return direct_out ? ((size_t)32 << 20) : ((size_t)16 << 20);
+}
+
+// Page-locked result pool (msh_host_alloc / msh_host_free, meshsearch.h).  Blocks are hipHostMalloc'd in 2-MB
+// granules and kept after release for the next call of similar size, up to a cap; the host-buffer entry points
+// download results straight into output arrays that lie inside a live block (pinned_range).
+class PinnedPool {
+  public:
+    int alloc(size_t bytes, void** out) {
+        constexpr size_t kGran = (size_t)2 << 20;
+        const size_t want = (std::max<size_t>(bytes, 1) + kGran - 1) / kGran * kGran;
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = free_.lower_bound(want);  // best fit, at most 5/4 of the request
+        if (it != free_.end() && it->first <= want + want / 4) {
+            *out = it->second;
+            live_.insert(it->second);
+            free_.erase(it);
+            return MSH_OK;
+        }
+        const size_t cap = cap_bytes();
+        // make room: release free blocks, largest first, until the new block fits under the cap
+        while (total_ + want > cap && !free_.empty()) release_locked(std::prev(free_.end()));
+        if (total_ + want > cap) {
+            set_error("msh_host_alloc: pinned pool cap %zu MB reached", cap >> 20);
+            return MSH_ENOMEM;
+        }
+        void* p = nullptr;
+        if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            while (!free_.empty()) release_locked(std::prev(free_.end()));
+            if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                set_error("msh_host_alloc: hipHostMalloc of %zu bytes failed", want);
+                return MSH_ENOMEM;
+            }
+        }
+        blocks_[p] = want;
+        live_.insert(p);
+        total_ += want;
+        *out = p;
+        return MSH_OK;
+    }
+    void release(void* p) {
+        std::lock_guard<std::mutex> g(mu_);
+        auto b = blocks_.find(p);
+        if (b == blocks_.end() || !live_.erase(p)) return;
+        free_.emplace(b->second, p);
+    }
+    int trim() {
+        std::lock_guard<std::mutex> g(mu_);
+        while (!free_.empty()) release_locked(std::prev(free_.end()));
+        return MSH_OK;
+    }
+    size_t bytes() {
+        std::lock_guard<std::mutex> g(mu_);
+        return total_;
+    }
+    // [p, p + n) lies inside one live block
+    bool contains(const void* p, size_t n) {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = blocks_.upper_bound(const_cast<void*>(p));
+        if (it == blocks_.begin()) return false;
+        --it;
+        const char* b = static_cast<const char*>(it->first);
+        const char* c = static_cast<const char*>(p);
+        return live_.count(it->first) && c >= b && c + n <= b + it->second;
+    }
+
+  private:
+    static size_t cap_bytes() {
+        const char* e = getenv("MESH_AMD_PINNED_POOL_MB");
+        const long long mb = e ? atoll(e) : 16384;
+        return mb > 0 ? (size_t)mb << 20 : 0;
+    }
+    void release_locked(std::multimap<size_t, void*>::iterator it) {
+        void* p = it->second;
+        (void)hipHostFree(p);
+        total_ -= it->first;
+        blocks_.erase(p);
+        free_.erase(it);
+    }
+    std::mutex mu_;
+    std::map<void*, size_t> blocks_;       // every block: base -> bytes
+    std::set<void*> live_;                 // blocks handed out
+    std::multimap<size_t, void*> free_;    // released blocks by size
+    size_t total_ = 0;
+};
+static PinnedPool& pinned_pool() {
+    static PinnedPool* p = new PinnedPool;  // never destroyed: live arrays may outlive static destructors
+    return *p;
+}
+
 // pipelined() over caller arrays that are page-locked in place: per chunk an H2D copy of the input rows into a
 // device slab (copy stream `up`), the kernels (handle stream), a D2H copy of the output rows straight into
 // the caller's arrays (stream `down`); two device slabs alternate, so chunk k uploads while k - 1 computes and
@@ -515,7 +622,7 @@ template <class Run>
 static int pipelined_registered(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, size_t chunk, Run run) {
     size_t row = 0;
     for (const HostArr& a : arrs) row += a.row_bytes;
-    MSH_TRY(stage_setup(t, chunk * row));
+    MSH_TRY(stage_setup(t, 0, chunk * row));
     hipStream_t sc = t->stream, up = t->s_up, down = t->s_down;
     int st = MSH_OK;
     hipError_t e = hipSuccess;
@@ -564,9 +671,18 @@ static int pipelined_registered(msh_tree* t, size_t S, const std::vector<HostArr
 }
 
 template <class Run>
-static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, size_t chunk, Run run) {
-    size_t row = 0;
-    for (const HostArr& a : arrs) row += a.row_bytes;
+static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Run run) {
+    size_t row = 0, in_end = 0;  // in_end: the inputs' share of a slab row (they come first)
+    for (const HostArr& a : arrs) {
+        row += a.row_bytes;
+        if (a.in) in_end = row;
+    }
+    // outputs inside the pinned result pool (msh_host_alloc) are downloaded straight into place: no staging
+    // copy, and the host only waits for a slab's previous upload before refilling it
+    bool direct_out = true;
+    for (const HostArr& a : arrs)
+        if (a.out && !pinned_pool().contains(a.out, S * a.row_bytes)) direct_out = false;
+    const size_t chunk = std::min(S, host_chunk(direct_out));
     hipStream_t sc = t->stream;
     int st = MSH_OK;
     if (S * row <= ((size_t)16 << 20)) {  // small call: one pageable round trip through device scratch
@@ -618,7 +734,7 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, si
         for (auto& r : reg) (void)hipHostUnregister(r.first);
         if (ok) return st;
     }
-    MSH_TRY(stage_setup(t, chunk * row));
+    MSH_TRY(stage_setup(t, chunk * (direct_out ? in_end : row), chunk * row));
     hipStream_t up = t->s_up, down = t->s_down;
     hipEvent_t* e_up = t->e_up;
     hipEvent_t* e_run = t->e_run;
@@ -650,8 +766,12 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, si
             const int b = (int)(k & 1);
             std::vector<CopyTask> tasks;
             if (k >= 2) {
-                if ((e = hipEventSynchronize(e_down[b])) != hipSuccess) { fail(e, "kernels / download"); break; }
-                outs_of(k - 2, tasks);
+                if (direct_out) {
+                    if ((e = hipEventSynchronize(e_up[b])) != hipSuccess) { fail(e, "upload"); break; }
+                } else {
+                    if ((e = hipEventSynchronize(e_down[b])) != hipSuccess) { fail(e, "kernels / download"); break; }
+                    outs_of(k - 2, tasks);
+                }
             }
             const bool have = k < nch;
             const size_t r0 = k * chunk, n = have ? std::min(chunk, S - r0) : 0;
@@ -666,6 +786,8 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, si
             }
             copy_pool().run(tasks);
             if (!have) continue;
+            // the device slab's previous chunk (k - 2) must have been downloaded before it is overwritten
+            if (direct_out && k >= 2 && (e = hipStreamWaitEvent(up, e_down[b], 0)) != hipSuccess) { fail(e, "upload"); break; }
             size_t off = 0;
             for (const HostArr& a : arrs) {
                 if (a.in && (e = hipMemcpyAsync(static_cast<char*>(dev[b]) + off * chunk,
@@ -690,10 +812,13 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, si
             }
             off = 0;
             for (const HostArr& a : arrs) {
-                if (a.out && (e = hipMemcpyAsync(static_cast<char*>(host[b]) + off * chunk,
-                                                 static_cast<char*>(dev[b]) + off * chunk, n * a.row_bytes,
-                                                 hipMemcpyDeviceToHost, down)) != hipSuccess)
-                    break;
+                if (a.out) {
+                    char* dst = direct_out ? static_cast<char*>(a.out) + r0 * a.row_bytes
+                                           : static_cast<char*>(host[b]) + off * chunk;
+                    if ((e = hipMemcpyAsync(dst, static_cast<char*>(dev[b]) + off * chunk, n * a.row_bytes,
+                                            hipMemcpyDeviceToHost, down)) != hipSuccess)
+                        break;
+                }
                 off += a.row_bytes;
             }
             if (e == hipSuccess) e = hipEventRecord(e_down[b], down);
@@ -706,11 +831,6 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, si
     return st;
 }
 
-static size_t host_chunk() {
-    const char* e = getenv("MESH_AMD_HOST_CHUNK");
-    const long long c = e ? atoll(e) : 0;
-    return c > 0 ? (size_t)c : ((size_t)4 << 20);  // 4M rows per chunk
-}
 
 }  // namespace msh
 
@@ -902,7 +1022,7 @@ int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uin
     if (!q || !face || !pt) { set_error("msh_tree_nearest: null argument"); return MSH_EINVAL; }
     // rows: q (24 B in) | face (4 B out) | part (4 B out) | point (24 B out)
     const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, part, 4}, {nullptr, pt, 24}};
-    return pipelined(t, S, arrs, std::min(S, host_chunk()), [&](size_t, size_t n, const std::vector<char*>& d) {
+    return pipelined(t, S, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
         return msh_tree_nearest_device(t, reinterpret_cast<const double*>(d[0]), n, reinterpret_cast<uint32_t*>(d[1]),
                                        part ? reinterpret_cast<uint32_t*>(d[2]) : nullptr,
                                        reinterpret_cast<double*>(d[3]), t->stream);
@@ -915,7 +1035,7 @@ int msh_tree_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face
     if (S == 0) return MSH_OK;
     if (!q || !face || !pt || !w) { set_error("msh_tree_nearest_bary: null argument"); return MSH_EINVAL; }
     const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, pt, 24}, {nullptr, w, 24}};
-    return pipelined(t, S, arrs, std::min(S, host_chunk()), [&](size_t, size_t n, const std::vector<char*>& d) {
+    return pipelined(t, S, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
         return msh_tree_nearest_bary_device(t, reinterpret_cast<const double*>(d[0]), n, reinterpret_cast<uint32_t*>(d[1]),
                                             reinterpret_cast<double*>(d[2]), reinterpret_cast<double*>(d[3]), t->stream);
     });
@@ -1023,7 +1143,7 @@ int msh_tree_nearest_alongnormal(msh_tree* t, const double* p, const double* n, 
     if (!p || !n || !dist || !face || !pt) { set_error("msh_tree_nearest_alongnormal: null argument"); return MSH_EINVAL; }
     const std::vector<HostArr> arrs = {{p, nullptr, 24}, {n, nullptr, 24}, {nullptr, dist, 8}, {nullptr, face, 4},
                                        {nullptr, pt, 24}};
-    return pipelined(t, S, arrs, std::min(S, host_chunk()), [&](size_t, size_t c, const std::vector<char*>& d) {
+    return pipelined(t, S, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
         return msh_tree_nearest_alongnormal_device(t, reinterpret_cast<const double*>(d[0]),
                                                    reinterpret_cast<const double*>(d[1]), c,
                                                    reinterpret_cast<double*>(d[2]), reinterpret_cast<uint32_t*>(d[3]),
@@ -1487,6 +1607,20 @@ int msh_timing_get(const char* name, double* ms, int64_t* count) {
     *count = it == g_times.end() ? 0 : it->second.second;
     return MSH_OK;
 }
+
+int msh_host_alloc(size_t bytes, void** out) {
+    if (!out) { set_error("msh_host_alloc: null argument"); return MSH_EINVAL; }
+    *out = nullptr;
+    return pinned_pool().alloc(bytes, out);
+}
+
+void msh_host_free(void* p) {
+    if (p) pinned_pool().release(p);
+}
+
+int msh_host_pool_trim(void) { return pinned_pool().trim(); }
+
+size_t msh_host_pool_bytes(void) { return pinned_pool().bytes(); }
 
 int msh_timing_reset(void) {
     resolve_pending();

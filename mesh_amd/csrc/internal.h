@@ -112,7 +112,8 @@ struct msh_tree {
     // streams and their events (api.cpp pipelined())
     void* h_stage[2] = {nullptr, nullptr};
     void* d_stage[2] = {nullptr, nullptr};
-    size_t stage_bytes = 0;
+    size_t stage_bytes = 0;   // device slabs
+    size_t hstage_bytes = 0;  // host slabs (inputs only when results go straight into pinned arrays)
     hipStream_t s_up = nullptr, s_down = nullptr;
     hipEvent_t e_up[2] = {nullptr, nullptr}, e_run[2] = {nullptr, nullptr}, e_down[2] = {nullptr, nullptr};
     double build_ms = 0.0;

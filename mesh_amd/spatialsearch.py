@@ -55,9 +55,7 @@ def aabbtree_nearest(tree, q):
         raise ValueError("Input must be Nx3")
     q = np.ascontiguousarray(q, dtype=np.float64)
     S = q.shape[0]
-    face = np.empty((1, S), dtype=np.uint32)
-    part = np.empty((1, S), dtype=np.uint32)
-    pt = np.empty((S, 3), dtype=np.float64)
+    face, part, pt = N.empty_results(((1, S), np.uint32), ((1, S), np.uint32), ((S, 3), np.float64))
     N.check(N.lib().msh_tree_nearest(tree.ptr, N.dptr(q), S, N.uptr(face), N.uptr(part), N.dptr(pt)))
     return face, part, pt
 
@@ -79,9 +77,7 @@ def aabbtree_nearest_barycentric(tree, q):
         raise TypeError("aabbtree_nearest_barycentric: handle is not a triangle tree")
     q = np.ascontiguousarray(q, dtype=np.float64)
     S = q.shape[0]
-    face = np.empty(S, dtype=np.uint32)
-    pt = np.empty((S, 3), dtype=np.float64)
-    w = np.empty((S, 3), dtype=np.float64)
+    face, pt, w = N.empty_results(((S,), np.uint32), ((S, 3), np.float64), ((S, 3), np.float64))
     N.check(N.lib().msh_tree_nearest_bary(tree.ptr, N.dptr(q), S, N.uptr(face), N.dptr(pt), N.dptr(w)))
     return face, pt, w
 
@@ -96,9 +92,7 @@ def aabbtree_nearest_alongnormal(tree, p, n):
     p = np.ascontiguousarray(p, dtype=np.float64)
     n = np.ascontiguousarray(n, dtype=np.float64)
     S = p.shape[0]
-    dist = np.empty(S, dtype=np.float64)
-    face = np.empty(S, dtype=np.uint32)
-    pt = np.empty((S, 3), dtype=np.float64)
+    dist, face, pt = N.empty_results(((S,), np.float64), ((S,), np.uint32), ((S, 3), np.float64))
     N.check(N.lib().msh_tree_nearest_alongnormal(tree.ptr, N.dptr(p), N.dptr(n), S, N.dptr(dist), N.uptr(face),
                                                   N.dptr(pt)))
     return dist, face, pt

@@ -456,6 +456,46 @@ def test_host_api_registered_and_staged_agree(monkeypatch):
     assert np.array_equal(dpt.cpu().numpy(), reg[2])
 
 
+def test_host_api_pinned_results(monkeypatch):
+    # large host calls carve their results from the page-locked pool (msh_host_alloc) and download straight
+    # into them; the arrays equal the pageable path's (pool disabled) for all three pipelined entry points, the
+    # block returns to the pool when its arrays die and is reused by the next call, and an in-place
+    # registration attempt on pool memory falls back to staging with the same answer
+    from mesh_amd import _native as N, spatialsearch
+    v, f = W.c2_mesh()
+    q = W.uniform_in_box(v.min(0), v.max(0), 700000, seed=26)
+    nrm = np.random.default_rng(27).normal(size=q.shape)
+    monkeypatch.setenv("MESH_AMD_HOST_CHUNK", "262144")  # 3 chunks: both slabs reused
+    monkeypatch.setattr(N, "PINNED_MIN_BYTES", 1 << 20)
+    t = spatialsearch.aabbtree_compute(v, f)
+    calls = [lambda: spatialsearch.aabbtree_nearest(t, q), lambda: spatialsearch.aabbtree_nearest_barycentric(t, q),
+             lambda: spatialsearch.aabbtree_nearest_alongnormal(t, q, nrm)]
+    monkeypatch.setenv("MESH_AMD_PINNED_POOL_MB", "0")
+    ref = [c() for c in calls]
+    assert all(r[0].base is None for r in ref)  # pool disabled: plain np.empty arrays
+    monkeypatch.setenv("MESH_AMD_PINNED_POOL_MB", "1024")
+    for c, r in zip(calls, ref):
+        got = c()
+        for a, b in zip(got, r):
+            assert a.shape == b.shape and a.dtype == b.dtype and a.flags.c_contiguous
+            assert np.array_equal(a, b, equal_nan=a.dtype.kind == "f")
+        owner = got[0]
+        while isinstance(owner, np.ndarray):
+            owner = owner.base
+        assert isinstance(owner, N._PinnedBlock)
+        del got, owner
+    held = N.lib().msh_host_pool_bytes()
+    assert held > 0
+    for _ in range(3):  # steady state: blocks come back and are reused
+        out = spatialsearch.aabbtree_nearest(t, q)
+        del out
+    assert N.lib().msh_host_pool_bytes() == held
+    monkeypatch.setenv("MESH_AMD_HOST_REGISTER", "1")
+    for a, b in zip(spatialsearch.aabbtree_nearest(t, q), ref[0]):
+        assert np.array_equal(a, b)
+    assert N.lib().msh_host_pool_trim() == 0
+
+
 @pytest.mark.parametrize("name", ["ico", "ico60", "c2", "offset"])
 def test_tree_bounds_contain_primitives(name):
     # every child's quantised oriented box (frame n, t, n x t) contains all vertices below it
