@@ -1075,6 +1075,7 @@ int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* n
         }
         fprintf(stderr, "[msh pass2] waves=%llu items=%llu visits_sum=%llu visits_max_item=%llu\n", h[6], h[46], h[44],
                 h[45]);
+        fprintf(stderr, "[msh leaves] improving_phase_tests=%llu hinted=%llu hint_leaf_won=%llu\n", h[36], h[37], h[38]);
     }
     return MSH_OK;
 }

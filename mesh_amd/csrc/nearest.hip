@@ -96,6 +96,7 @@ struct KnnArgs {
     // rec_leaf: slot-order records are hints only (direct stores, or instrumented launches), so their part
     // field carries the winner's leaf index instead of its part code (leader_leaf)
     bool rec_leaf;
+    bool list;      // closest-point modes: wave leaf list (trees of < 2^26 leaves) instead of per-lane queues
     size_t nunits;  // work units of this phase (slots it covers)
     DeferRec* deferred;
     unsigned* n_deferred;
@@ -568,13 +569,34 @@ __device__ inline int leader_leaf(const KnnArgs& a, size_t i, const D3& q, size_
 #ifndef MSH_COMPACT
 #define MSH_COMPACT 1
 #endif
+// Wave leaf list (closest-point modes): lanes append the leaf children that survive their node's bound to a
+// ring of (leaf << 6 | owner lane) entries in LDS shared by the wave, and the wave evaluates them in rounds of
+// 64 — one entry per lane, every round full except when nobody can move — instead of per-lane queues flushed
+// part-empty.  A lane stops traversing while kPend of its leaves wait (its bound is stale).  Each round's
+// results reach their owners through LDS: an atomic min of the squared distance's bits per owner, then an
+// atomic min of (face << 32 | leaf) among the entries that reached it: the lexicographic (d2, face) rule.
+#ifndef MSH_LIST
+#define MSH_LIST 1
+#endif
+#ifndef MSH_PEND
+#define MSH_PEND 32
+#endif
+constexpr int kPend = MSH_PEND;     // unevaluated leaves a lane may hold before it stops traversing
+constexpr unsigned kRing = 256;     // ring entries per wave: < 64 left after full rounds + <= 128 per step
+constexpr size_t kListMaxLeaves = (size_t)1 << 26;  // leaf index bits of a ring entry
+
 // (not for the normals metric, MODE 1, whose larger live set would spill in the node step)
 #define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 1 : MSH_WAVES)))
-template <int MODE, bool STATS>
+template <int MODE, bool STATS, bool LIST>
 __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
     constexpr bool kCompact = (MODE == 0 || MODE == 3) && MSH_COMPACT;
-    __shared__ uint2 lent[kCompact ? kBlock * kLeafQ : 1];  // compacted leaf phases: kLeafQ entries per lane
+    constexpr bool kList = (MODE == 0 || MODE == 3) && LIST;  // a separate instantiation: its own registers
+    // compacted leaf phases: kLeafQ entries per lane; the wave leaf list shares this space (a.list)
+    constexpr size_t kEntWords = kCompact && !kList ? (size_t)kBlock * kLeafQ * 2 : 1;
+    constexpr size_t kListWords = kList ? 4 * (kRing + 64 * 4) : 1;  // per wave: ring + bd/bfl (u64 per lane each)
+    __shared__ uint32_t lsh[kEntWords > kListWords ? kEntWords : kListWords];
+    uint2* lent = reinterpret_cast<uint2*>(lsh);
     const int tid = threadIdx.x, lane = tid & 63;
     uint2* lds = stk + tid;
     uint2* ent = lent + (kCompact ? (tid >> 6) * 64 * kLeafQ : 0);
@@ -582,6 +604,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     const unsigned group = blockIdx.x & 7u;
     unsigned long long u_trav_it = 0, u_trav_lanes = 0, u_leaf_it = 0, u_leaf_lanes = 0;  // STATS: wave iterations
     unsigned n_nodes = 0, n_leaves = 0;
+    unsigned n_impr = 0, n_hinted = 0, n_hint_won = 0;  // STATS: improving leaf tests, hinted queries, hint = answer
     for (;;) {
         unsigned tile = 0;
         if (lane == 0) tile = dequeue_tile(a.counters, a.ntiles, group);
@@ -604,14 +627,19 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
         }
         double hint = INFINITY;
+        int hint_leaf = -1;  // STATS
         if constexpr (MODE == 0 || MODE == 3) {
             if (fin && (a.phase == 2 || (a.phase == 1 && kLead2 > 0))) {
                 if constexpr (kHintFace) {
                     const int lf = a.phase == 2 ? leader_leaf(a, i, q, MSH_FWIN, kLead)
                                                 : leader_leaf(a, i, q, MSH_LWIN * kLead2, kLead2);
+                    if (STATS) hint_leaf = lf;
                     if (lf >= 0) {
                         pol.test(lf);
-                        if (STATS) ++n_leaves;
+                        if (STATS) {
+                            ++n_leaves;
+                            ++n_hinted;
+                        }
                     }
                 } else {
                     hint = a.phase == 2 ? hint_from_leaders(a, i, q, MSH_FWIN, kLead)
@@ -629,6 +657,162 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             }
             continue;
         }
+        if constexpr (kList) {
+          {
+            QF qf;
+            const int root = query_root(a, i, q, qf);
+            Walker w{root, 0};
+            uint32_t* ring = lsh + (tid >> 6) * (kRing + 64 * 4);
+            unsigned long long* bd = reinterpret_cast<unsigned long long*>(ring + kRing);  // per owner: d2 bits
+            unsigned long long* bfl = bd + 64;                                              // (face << 32 | leaf)
+            const unsigned long long lt = (1ull << lane) - 1ull;
+            bool active = fin, want_defer = false, deferred = false;
+            int nq = 0;              // this lane's leaves appended since all of them were last evaluated (a bound)
+            unsigned last_pos = 0;   // ring counter of this lane's newest entry
+            unsigned head = 0, tail = 0;  // wave-uniform ring counters: entries [head, tail) wait
+            unsigned steps = 0;
+            const unsigned max_steps = (unsigned)min(a.T, (size_t)UINT_MAX);
+            unsigned tot = 0;  // STATS: node steps of this lane, restarts included
+            // Evaluate ring entries [head, upto) in rounds of 64, one per lane: each lane tests its entry's leaf
+            // against its owner's query (ds_bpermute); the owners publish their best before each round and take
+            // the round's lexicographic (d2, face) minimum back from LDS.
+            auto run_rounds = [&](unsigned upto) {
+                while (head != upto) {
+                    const unsigned n = min(64u, upto - head);
+                    bd[lane] = (unsigned long long)__double_as_longlong(pol.best);
+                    bfl[lane] = ~0ull;
+                    const bool valid = (unsigned)lane < n;
+                    const uint32_t en = ring[(head + (valid ? (unsigned)lane : 0u)) & (kRing - 1)];
+                    const int src = (int)(en & 63u);
+                    const int leaf = (int)(en >> 6);
+                    const D3 x = D3{__shfl(pol.q.x, src), __shfl(pol.q.y, src), __shfl(pol.q.z, src)};
+                    uint32_t f;
+                    const double d2 = pol.eval(leaf, x, f);
+                    const unsigned long long kb = (unsigned long long)__double_as_longlong(d2);
+                    asm volatile("" ::: "memory");
+                    if (valid) atomicMin(&bd[src], kb);
+                    asm volatile("" ::: "memory");
+                    if (valid && bd[src] == kb) atomicMin(&bfl[src], ((unsigned long long)f << 32) | (unsigned)leaf);
+                    asm volatile("" ::: "memory");
+                    const unsigned long long nb = bd[lane], nf = bfl[lane];
+                    const double nd = __longlong_as_double((long long)nb);
+                    const uint32_t nface = (uint32_t)(nf >> 32);
+                    if (nf != ~0ull && (nd < pol.best || (nd == pol.best && nface < pol.best_face))) {
+                        pol.best = nd;
+                        pol.best_face = nface;
+                        pol.best_leaf = (int)(uint32_t)nf;
+                        pol.relim();
+                        if (STATS) ++n_impr;
+                    }
+                    asm volatile("" ::: "memory");
+                    if (STATS) {
+                        if (valid) ++n_leaves;
+                        if (lane == 0) {
+                            ++u_leaf_it;
+                            u_leaf_lanes += n;
+                        }
+                    }
+                    head += n;
+                }
+                if ((int)(last_pos - head) < 0) nq = 0;  // every entry of this lane is evaluated
+            };
+            for (;;) {
+                // a lane past its budget defers once its own leaves are evaluated (pass 2 then owns the query)
+                if (want_defer && nq == 0) {
+                    want_defer = false;
+                    const unsigned slot = atomicAdd(a.n_deferred, 1u);
+                    if (slot < a.max_deferred) {
+                        if ((a.phase == 1 || a.phase == 3) && a.res) {
+                            // later phases take hints from this slot before pass 2 answers it: publish the closest
+                            // point of the best face so far (a point on the mesh), or NO_FACE when it has none yet
+                            D3 o = D3{NAN, NAN, NAN};
+                            uint32_t f = MSH_NO_FACE;
+                            if (pol.best_leaf >= 0) {
+                                D3 ta, tb, tc;
+                                int part;
+                                load_tri(static_cast<const TriRec*>(a.leaves), pol.best_leaf, ta, tb, tc, f);
+                                closest_on_triangle(q, ta, tb, tc, o, part);
+                            }
+                            store_qres(a.res + i, f, (uint32_t)pol.best_leaf, o.x, o.y, o.z);
+                        }
+                        DeferRec r;
+                        r.slot = (uint32_t)i;
+                        r.face = pol.best_face;
+                        r.leaf = pol.best_leaf;
+                        r.pad = 0;
+                        r.best = pol.best;
+                        r.pad2 = 0;
+                        a.deferred[slot] = r;
+                        active = false;
+                        deferred = true;
+                    }
+                    // deferred list full: finish here without a budget
+                }
+                const bool can = active && !want_defer && nq < kPend;
+                if (__ballot(can) == 0ull) {
+                    if (tail == head) break;  // nothing queued and nobody can move: the tile is done
+                    run_rounds(tail);
+                    continue;
+                }
+                if (STATS && lane == 0) {
+                    ++u_trav_it;
+                    u_trav_lanes += __popcll(__ballot(can));
+                }
+                int l0 = -1, l1 = -1;
+                if (can) {
+                    active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, l0, l1,
+                                                                  kPend - nq);
+                    ++steps;
+                    if (STATS) ++tot;
+                    if (active && steps >= max_steps) active = false;  // each node is entered once: corrupt tree
+                    if (active && steps == a.budget) want_defer = true;
+                }
+                // append this step's leaves (at most two per lane) to the ring, in lane order
+                if (l0 < 0) {
+                    l0 = l1;
+                    l1 = -1;
+                }
+                const unsigned long long m1 = __ballot(l0 >= 0), m2 = __ballot(l1 >= 0);
+                const unsigned pos = tail + (unsigned)(__popcll(m1 & lt) + __popcll(m2 & lt));
+                if (l0 >= 0) {
+                    ring[pos & (kRing - 1)] = ((uint32_t)l0 << 6) | (uint32_t)lane;
+                    last_pos = pos;
+                    ++nq;
+                }
+                if (l1 >= 0) {
+                    ring[(pos + 1) & (kRing - 1)] = ((uint32_t)l1 << 6) | (uint32_t)lane;
+                    last_pos = pos + 1;
+                    ++nq;
+                }
+                tail += (unsigned)(__popcll(m1) + __popcll(m2));
+                if (tail - head >= 64u) run_rounds(head + ((tail - head) & ~63u));
+            }
+            if (STATS) {  // per-tile step profile of this phase (stats[8 + 9 * phase slot ...])
+                unsigned mx = tot, sm = tot;
+                for (int o = 32; o > 0; o >>= 1) {
+                    mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
+                    sm += (unsigned)__shfl_xor((int)sm, o);
+                }
+                unsigned long long* h = a.stats + 8 + 9 * (a.phase == 3 ? 0 : (a.phase == 1 ? 1 : 2));
+                if (lane == 0) {
+                    atomicAdd(h + 0, 1ull);
+                    atomicAdd(h + 1, (unsigned long long)mx);
+                    atomicAdd(h + 2, (unsigned long long)sm);
+                    atomicAdd(h + 3, (unsigned long long)min(mx, 128u));
+                    atomicAdd(h + 4, (unsigned long long)min(mx, 256u));
+                    atomicAdd(h + 5, (unsigned long long)min(mx, 512u));
+                }
+                if (tot > 128) atomicAdd(h + 6, 1ull);
+                if (tot > 256) atomicAdd(h + 7, 1ull);
+                if (tot > 512) atomicAdd(h + 8, 1ull);
+            }
+            if (STATS && fin && hint_leaf >= 0 && pol.best_leaf == hint_leaf) ++n_hint_won;
+            if (deferred) continue;
+            if (fin && (!STATS || a.res)) write_result<MODE>(a, i, q, pol);
+            continue;
+          }
+        }
+        if constexpr (!kList) {
         {
             QF qf;
             const int root = query_root(a, i, q, qf);
@@ -719,7 +903,11 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                                 const int from = mine ? at : lane;
                                 const double dk = __shfl(d2, from);
                                 const uint32_t fk = (uint32_t)__shfl((int)f, from);
-                                if (mine) better |= pol.offer(dk, fk, e == 0 ? q0 : (e == 1 ? q1 : (e == 2 ? q2 : q3)));
+                                if (mine) {
+                                    const bool b = pol.offer(dk, fk, e == 0 ? q0 : (e == 1 ? q1 : (e == 2 ? q2 : q3)));
+                                    better |= b;
+                                    if (STATS && b) ++n_impr;
+                                }
                             }
                         }
                         asm volatile("" ::: "memory");
@@ -813,11 +1001,16 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             }
             if (deferred) continue;
         }
+        if (STATS && fin && hint_leaf >= 0 && pol.best_leaf == hint_leaf) ++n_hint_won;
         if (fin && (!STATS || a.res)) write_result<MODE>(a, i, q, pol);
+        }
     }
     if (STATS) {
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
         atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
+        atomicAdd(&a.stats[36], (unsigned long long)n_impr);
+        atomicAdd(&a.stats[37], (unsigned long long)n_hinted);
+        atomicAdd(&a.stats[38], (unsigned long long)n_hint_won);
         if (lane == 0) {
             atomicAdd(&a.stats[2], u_trav_it);
             atomicAdd(&a.stats[3], u_trav_lanes);
@@ -1143,6 +1336,10 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         a.spill = ws.spill.as<uint2>();
     }
     a.budget = kBudget;
+    {
+        const char* e = getenv("MESH_AMD_LEAF_LIST");  // 0: per-lane leaf queues (the path of larger trees)
+        a.list = (MODE == 0 || MODE == 3) && MSH_LIST && !(e && atoi(e) == 0) && tree->B * tree->T < kListMaxLeaves;
+    }
     a.max_deferred = (unsigned)std::min<size_t>(a.S, (a.S / 16) + 65536);
     DevBuf& dbuf = ws.flags;
     MSH_TRY(dbuf.reserve((size_t)a.max_deferred * sizeof(DeferRec)));
@@ -1162,7 +1359,10 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, ncu * kKnnBlocksPerCU);
         if (nblk == 0) return MSH_OK;
         TimedLaunch t1(name, s);
-        k_knn<MODE, STATS><<<nblk, kBlock, 0, s>>>(a);
+        if (a.list)
+            k_knn<MODE, STATS, (MODE == 0 || MODE == 3)><<<nblk, kBlock, 0, s>>>(a);
+        else
+            k_knn<MODE, STATS, false><<<nblk, kBlock, 0, s>>>(a);
         MSH_HIP(hipGetLastError());
         return MSH_OK;
     };

@@ -31,7 +31,7 @@ def compile_asm(flags):
 
 
 def report(s, mode):
-    name = f"_ZN3msh5k_knnILi{mode}ELb0EEEvNS_7KnnArgsE"
+    name = f"_ZN3msh5k_knnILi{mode}ELb0ELb{int(LIST)}EEEvNS_7KnnArgsE"
     meta = s[re.search(r"\.name:\s+" + name + r"\n", s).start():][:1500]
     vgpr = int(re.search(r"\.vgpr_count:\s+(\d+)", meta).group(1))
     spill = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", meta).group(1))
@@ -51,11 +51,16 @@ def report(s, mode):
     return dict(mode=mode, vgpr=vgpr, vgpr_spill=spill, scratch_ops=total, scratch_in_loop=in_loop, lds=lds)
 
 
+LIST = True  # the wave-leaf-list instantiation k_knn<MODE, false, true> (the closest-point path)
+
+
 def main():
+    global LIST
     flags = sys.argv[1:]
     s = compile_asm(flags)
-    for mode in (0, 3):
-        print(report(s, mode))
+    for LIST in (True, False):
+        for mode in (0, 3):
+            print(dict(report(s, mode), list=LIST))
 
 
 if __name__ == "__main__":
