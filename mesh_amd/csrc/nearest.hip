@@ -581,6 +581,9 @@ __device__ inline int leader_leaf(const KnnArgs& a, size_t i, const D3& q, size_
 #ifndef MSH_PEND
 #define MSH_PEND 32
 #endif
+#ifndef MSH_ROUND_AT
+#define MSH_ROUND_AT 64
+#endif
 constexpr int kPend = MSH_PEND;     // unevaluated leaves a lane may hold before it stops traversing
 constexpr unsigned kRing = 256;     // ring entries per wave: < 64 left after full rounds + <= 128 per step
 constexpr size_t kListMaxLeaves = (size_t)1 << 26;  // leaf index bits of a ring entry
@@ -754,9 +757,12 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     run_rounds(tail);
                     continue;
                 }
-                if (STATS && lane == 0) {
-                    ++u_trav_it;
-                    u_trav_lanes += __popcll(__ballot(can));
+                if (STATS) {
+                    const int nt = __popcll(__ballot(can));
+                    if (lane == 0) {
+                        ++u_trav_it;
+                        u_trav_lanes += nt;
+                    }
                 }
                 int l0 = -1, l1 = -1;
                 if (can) {
@@ -785,7 +791,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     ++nq;
                 }
                 tail += (unsigned)(__popcll(m1) + __popcll(m2));
-                if (tail - head >= 64u) run_rounds(head + ((tail - head) & ~63u));
+                if (tail - head >= (unsigned)MSH_ROUND_AT) run_rounds(head + ((tail - head) & ~63u));
             }
             if (STATS) {  // per-tile step profile of this phase (stats[8 + 9 * phase slot ...])
                 unsigned mx = tot, sm = tot;
