@@ -212,12 +212,9 @@ struct WsOrder {
 };
 
 // Triangle tree over v (P rows) and f (T rows, indices into v).
-// Subtrees of the LBVH over at most 2^kResplitLog2 leaves are rebuilt top down along the surface (refine.hip);
-// 0 keeps the plain Karras tree
-#ifndef MSH_RESPLIT
-#define MSH_RESPLIT 16
-#endif
-constexpr int kResplitLog2 = MSH_RESPLIT;
+// Subtrees of the LBVH over at most 2^kResplitLog2 leaves are rebuilt top down along the surface (refine.hip;
+// C3: 2^12 and 2^17 measured slower, profiles/r03_c3_resplit_ab.jsonl)
+constexpr int kResplitLog2 = 16;
 
 static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint32_t* f, size_t T) {
     hipStream_t s = t->stream;
@@ -268,18 +265,11 @@ static const size_t kSortMin = 4096;  // below this the query Morton sort costs 
 // otherwise Morton codes + radix sort give the permutation (ws.vals).  With allow_lazy (closest-point
 // launches without normals) the traversal reads row perm[i] itself and writes the inverse permutation
 // (ws.inv); otherwise the rows (and normals, when given) are gathered once into slot order
-// (ws.qs / ws.ns) with the inverse permutation.  MSH_SLOT_GATHER=1 gathers always (A/B switch: the
-// gather is 3 % slower on C3).
-#ifndef MSH_SLOT_GATHER
-#define MSH_SLOT_GATHER 0
-#endif
+// (ws.qs / ws.ns) with the inverse permutation (gathering the closest-point rows too measured 3 % slower on C3).
 // Queries are ordered by the top 24 bits of their 30-bit Morton code (256 cells per axis, 3 radix passes):
 // C3's 100M queries put ~6 in a cell, and the traversal runs the same node counts as with the full code
 // (sort 3.44 -> 3.08 ms, traversal unchanged).  The order within a cell is the caller's (stable sort).
-#ifndef MSH_QSORT_LO
-#define MSH_QSORT_LO 6
-#endif
-constexpr int kQuerySortLo = MSH_QSORT_LO;
+constexpr int kQuerySortLo = 6;
 static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_t S, hipStream_t s,
                         QueryOrder* ord, bool allow_lazy = false) {
     *ord = QueryOrder{d_q, d_n, nullptr, nullptr};
@@ -298,7 +288,7 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
         std::swap(ws.keys, ws.keys_alt);
         std::swap(ws.vals, ws.vals_alt);
     }
-    if (allow_lazy && !MSH_SLOT_GATHER && !d_n) {
+    if (allow_lazy && !d_n) {
         *ord = QueryOrder{d_q, nullptr, ws.vals.as<uint32_t>(), ws.inv.as<uint32_t>(), false};
         return MSH_OK;
     }

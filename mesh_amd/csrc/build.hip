@@ -436,10 +436,7 @@ __device__ inline ObbFrame range_frame(const double4* __restrict__ P, int first,
 }
 
 constexpr int kObbLane = 32;    // nodes over at most this many leaves: one lane each; up to kObbBig: one wave each
-#ifndef MSH_OBB_BIG
-#define MSH_OBB_BIG 4096
-#endif
-constexpr int kObbBig = MSH_OBB_BIG;  // larger nodes (the top levels): kObbChunk-leaf chunks, one block per chunk
+constexpr int kObbBig = 4096;  // larger nodes (the top levels): kObbChunk-leaf chunks, one block per chunk
 constexpr int kObbChunk = 1024;
 
 // Oriented boxes of nodes over at most kObbLane leaves, one lane per node (most nodes: the lower levels)

@@ -23,10 +23,7 @@
 namespace msh {
 
 constexpr int kBlock = 256;          // 4 waves of 64 lanes
-#ifndef MSH_STACK
-#define MSH_STACK 16
-#endif
-constexpr int kStack = MSH_STACK;           // per-lane LDS stack entries; deeper entries spill to global memory
+constexpr int kStack = 16;           // per-lane LDS stack entries; deeper entries spill to global memory
 constexpr double kSlack = 1.0 + 9.094947017729282e-13;  // 1 + 2^-40: fp64 rounding margin for culls
 
 // float index within a node:  0-5 frame (n0 t0 n1 t1 n2 t2: the (n_k, t_k) pairs are 8-B aligned, so

@@ -76,7 +76,7 @@ struct SlotOut {
 // Order in which a launch visits its queries: q (and n) are the rows in slot order; perm maps a slot
 // to the caller's row and inv back (both nullptr: identity, the caller's arrays are used directly).
 // gathered == false: q (and n) are still the caller's rows; the traversal reads row perm[i] for slot i
-// and records inv itself (MSH_SLOT_GATHER=0 experiment)
+// and records inv itself (closest-point launches)
 struct QueryOrder {
     const double* q;
     const double* n;

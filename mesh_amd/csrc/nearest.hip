@@ -19,9 +19,10 @@
 //     groups steal).  One lane per query, near-child-first depth-first traversal: one 64-B node read
 //     bounds both children by their fp32 oriented boxes; the far child is pushed (16-entry LDS stack
 //     per lane, [depth][lane] layout, deeper entries spill to a lane-interleaved global area sized
-//     from the tree depth).  Leaf children are parked and tested in wave-wide leaf phases (Aila &
-//     Laine's postponed leaves) with CGAL's exact fp64 construction.  Pass 1 runs over the leader
-//     slots first and then over the followers, which start from their leaders' bound.
+//     from the tree depth).  Leaf children that survive the bound go to the wave leaf list, a ring in LDS
+//     the wave evaluates in full rounds of 64 with CGAL's exact fp64 construction (postponed leaves,
+//     Aila & Laine, dealt to every lane of the wave).  Pass 1 runs over super-leader slots, then leader
+//     slots, then followers, each starting from the leaf of its nearest leader's answer.
 //     The fp32 pruning radius is cached per lane and refreshed only when the best distance changes.
 //     A lane that exceeds `budget` node steps stops and appends its query (with its exact best so far)
 //     to a deferred list: queries near the centre of a closed surface are equidistant from most of it
@@ -88,7 +89,7 @@ struct KnnArgs {
     unsigned budget;
     // leader / follower ordering (sorted closest-point launches, MODE 0 and 3): phase 0 = every slot,
     // unhinted; phase 1 = leader slots (i % kLead == 0); phase 2 = the other slots, each starting from the
-    // upper bound given by its 64-slot tile's leaders (see hint_from_leaders)
+    // leaf of the nearest leader's closest point in its 64-slot window (see leader_leaf)
     int phase;
     // direct: the sorted path writes each answer straight to the caller's row perm[i] (no k_unpermute);
     // slot-order records are kept only for the leader phases, whose records are the followers' hints
@@ -442,55 +443,28 @@ __device__ inline D3 load_q(const KnnArgs& a, size_t i) {
     return D3{a.q[3 * r], a.q[3 * r + 1], a.q[3 * r + 2]};
 }
 
-#ifndef MSH_LEAD
-#define MSH_LEAD 8
-#endif
-constexpr unsigned kLead = MSH_LEAD;  // one leader slot per kLead slots (0: leader ordering off)
-#ifndef MSH_LEAF_K
-#define MSH_LEAF_K 64
-#endif
-constexpr int kLeafK = MSH_LEAF_K;  // a leaf phase runs when blocked lanes >= traversing lanes / kLeafK
-#ifndef MSH_LEAF_ROUND
-#define MSH_LEAF_ROUND 2
-#endif
-// leaves a lane tests per leaf phase: fewer rounds per phase keep more of the wave's lanes busy in each (the
-// rounds of a phase run until its fullest queue is empty)
-constexpr int kLeafRound = MSH_LEAF_ROUND;
-#ifndef MSH_LEAF_FULL
-#define MSH_LEAF_FULL 0
-#endif
-constexpr int kLeafFull = MSH_LEAF_FULL;  // compacted phases: also flush once the wave holds this many leaves
-#ifndef MSH_LEAF_Q
-#define MSH_LEAF_Q 4
-#endif
-constexpr int kLeafQ = MSH_LEAF_Q;  // leaves a lane may hold before it stops traversing (2..4)
-static_assert(kLeafQ >= 2 && kLeafQ <= 8, "kLeafQ: 2..8");
-#ifndef MSH_LEAF_PARK
-#define MSH_LEAF_PARK 1
-#endif
-constexpr bool kLeafPark = MSH_LEAF_PARK;  // lanes traverse while their queue has room for one leaf (step_collect)
+// ---- pass-1 constants (each measured on C3 100M; A/B records in profiles/r02_*_ab.jsonl, r03_*_ab.jsonl) ----
+// Leader ordering: one leader slot per kLead slots (4: -4 %, 16: -1 %, none: -22 %), one super-leader per kLead2
+// slots; super-leaders run first and unhinted, leaders take their hint from the kLWin super-leaders of their
+// window (4: -1.1 %), followers from the leaders of their kFWin-slot window (32: +-0, 128: -3 %).
+constexpr unsigned kLead = 8;
+constexpr unsigned kLead2 = 256;
+constexpr size_t kFWin = 64;
+constexpr size_t kLWin = 8;
+static_assert(kLead2 % kLead == 0 && kLead2 / kLead >= 2, "kLead2: a multiple of kLead");
+// Per-lane leaf queues (the path of trees with >= 2^26 leaves, and of the normals-metric and point modes): up
+// to kLeafQ leaves per lane, a lane traverses while its queue has room for one more (a second leaf child is
+// parked on its stack); leaf phases run as soon as one lane is blocked; the uncompacted phases (MODE 1, 2) test
+// at most kLeafRound leaves per lane each.
+constexpr int kLeafQ = 4;
+constexpr int kLeafRound = 2;
 
-#ifndef MSH_LEAD2
-#define MSH_LEAD2 256
-#endif
-#ifndef MSH_FWIN
-#define MSH_FWIN 64  // followers take their bound from the leaders of their MSH_FWIN-slot window
-#endif
-#ifndef MSH_LWIN
-#define MSH_LWIN 8   // leaders take theirs from the MSH_LWIN super-leaders of their window (4: -1.1 %)
-#endif
-// second level: one super-leader per kLead2 slots (0: off), run first and unhinted; the other leaders
-// then start from the bound of the 4 super-leaders of their 4 * kLead2-slot window
-constexpr unsigned kLead2 = MSH_LEAD2;
-static_assert(kLead2 == 0 || (kLead > 1 && kLead2 % kLead == 0 && kLead2 / kLead >= 2), "kLead2: a multiple of kLead");
-
-// slot of work unit k in the launch's phase: 3 super-leaders, 1 leaders (without the super-leaders
-// when kLead2 > 0), 2 followers, 0 every slot
+// slot of work unit k in the launch's phase: 3 super-leaders, 1 leaders (without the super-leaders), 2
+// followers, 0 every slot
 __device__ inline size_t slot_of(const KnnArgs& a, size_t k) {
     if (a.phase == 3) return k * kLead2;
     if (a.phase == 1) {
-        if (kLead2 == 0) return k * kLead;
-        constexpr size_t r = kLead2 / (kLead ? kLead : 1);
+        constexpr size_t r = kLead2 / kLead;
         return kLead * (k + k / (r - 1) + 1);
     }
     if (a.phase == 2) {
@@ -500,44 +474,12 @@ __device__ inline size_t slot_of(const KnnArgs& a, size_t k) {
     return k;
 }
 
-// Upper bound of slot i's squared distance from the closest points found by the leaders at slots
-// base, base + stride, ... < base + window (base = the window containing i): a leader's point p_L lies on
-// a mesh triangle, so d*(q) <= |q - p_L|.  The bound is widened by 2^-30 relative and (2^-40 M)^2
-// absolute (M = largest |coordinate|) against the rounding of the fp64 constructions; the caller still
-// re-runs the query unhinted whenever its final best exceeds the bound, so a bound that is too tight
-// costs time, never correctness.  Leaders of another mesh (batched trees), deferred leaders (NO_FACE
-// until pass 2 runs) and non-finite ones are skipped.
-__device__ inline double hint_from_leaders(const KnnArgs& a, size_t i, const D3& q, size_t window, size_t stride) {
-    const size_t base = (i / window) * window;
-    const size_t mesh = a.orgs ? i / a.qper : 0;
-    double h = INFINITY;
-    for (size_t L = 0; L < window; L += stride) {
-        const size_t li = base + L;
-        if (li >= a.S) break;
-        if (a.orgs && li / a.qper != mesh) continue;
-        const uint4 r0 = reinterpret_cast<const uint4*>(a.res + li)[0];
-        if (r0.x == MSH_NO_FACE) continue;
-        const double2 r1 = reinterpret_cast<const double2*>(a.res + li)[1];
-        const double x = __longlong_as_double((long long)(((unsigned long long)r0.w << 32) | r0.z));
-        const double dx = q.x - x, dy = q.y - r1.x, dz = q.z - r1.y;
-        h = fmin(h, dx * dx + dy * dy + dz * dz);
-    }
-    if (h == INFINITY) return h;
-    const double M = fmax(fmax(fabs(q.x), fabs(q.y)), fabs(q.z));
-    const double e = M * 9.094947017729282e-13;  // 2^-40 M
-    return h * (1.0 + 9.313225746154785e-10) + e * e;  // 1 + 2^-30
-}
-
-// The leaf holding the closest point of the leader (at base, base + stride, ... < base + window, as
-// hint_from_leaders) nearest to q, or -1: with kHintFace a slot starts by testing that leaf exactly, as if
-// the traversal had reached it first — a real candidate (d^2, face, leaf), so no hint can be too tight and
-// nothing re-runs, and the exact distance to the leader's face is at most |q - p_L|.  Neighbouring queries
-// mostly share their closest face: the first bound is usually the answer (host model: 14 % fewer leaf tests
-// than the |q - p_L| hint).
-#ifndef MSH_HINT_FACE
-#define MSH_HINT_FACE 1
-#endif
-constexpr bool kHintFace = MSH_HINT_FACE;
+// The leaf holding the closest point p_L of the leader (at slots base, base + stride, ... < base + window of
+// the window containing i) nearest to q, or -1.  A hinted slot starts by testing that leaf exactly, as if the
+// traversal had reached it first: a real candidate (d^2, face, leaf), so no hint can be too tight, and its
+// exact distance is at most |q - p_L| (host model: 14 % fewer leaf tests than a |q - p_L| bound; C3: the
+// hint leaf is the answer for 17 % of the followers).  Leaders of another mesh (batched trees) and deferred
+// leaders (NO_FACE until pass 2 answers them) are skipped.
 __device__ inline int leader_leaf(const KnnArgs& a, size_t i, const D3& q, size_t window, size_t stride) {
     const size_t base = (i / window) * window;
     const size_t mesh = a.orgs ? i / a.qper : 0;
@@ -563,37 +505,27 @@ __device__ inline int leader_leaf(const KnnArgs& a, size_t i, const D3& q, size_
 
 // Pass 1 runs 4 waves per SIMD: the register budget drops from 139 to 128 VGPRs at the cost of a few
 // spills of loop-invariant values outside the node step (C3: +10 % over the compiler's 3 waves).
-#ifndef MSH_WAVES
-#define MSH_WAVES 4
-#endif
-#ifndef MSH_COMPACT
-#define MSH_COMPACT 1
-#endif
 // Wave leaf list (closest-point modes): lanes append the leaf children that survive their node's bound to a
 // ring of (leaf << 6 | owner lane) entries in LDS shared by the wave, and the wave evaluates them in rounds of
 // 64 — one entry per lane, every round full except when nobody can move — instead of per-lane queues flushed
-// part-empty.  A lane stops traversing while kPend of its leaves wait (its bound is stale).  Each round's
+// part-empty.  A lane stops traversing while kPend of its leaves wait.  Each round's
 // results reach their owners through LDS: an atomic min of the squared distance's bits per owner, then an
 // atomic min of (face << 32 | leaf) among the entries that reached it: the lexicographic (d2, face) rule.
-#ifndef MSH_LIST
-#define MSH_LIST 1
-#endif
-#ifndef MSH_PEND
-#define MSH_PEND 32
-#endif
-#ifndef MSH_ROUND_AT
-#define MSH_ROUND_AT 64
-#endif
-constexpr int kPend = MSH_PEND;     // unevaluated leaves a lane may hold before it stops traversing
+// kPend: unevaluated leaves a lane may hold before it stops traversing (3: 1236, 4: 1346, 8: 1593, 16: 1677,
+// 32: 1706, unbounded: 1689 M q/s; the per-lane queues measured 1541 in the same session)
+constexpr int kPend = 32;
 constexpr unsigned kRing = 256;     // ring entries per wave: < 64 left after full rounds + <= 128 per step
 constexpr size_t kListMaxLeaves = (size_t)1 << 26;  // leaf index bits of a ring entry
+constexpr size_t kLeadMinLeaves = 4096;  // smaller trees skip the leader phases (C1: 0.56 -> 0.29 ms)
 
-// (not for the normals metric, MODE 1, whose larger live set would spill in the node step)
-#define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 1 : MSH_WAVES)))
+// Pass 1 runs 4 waves per SIMD (not the normals metric, MODE 1, whose larger live set would spill in the node
+// step): the register budget drops from 139 to 128 VGPRs at the cost of a few spills of loop-invariant values
+// outside the node step (C3: +10 % over the compiler's 3 waves; 5 waves spill in the loop: -30 %).
+#define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 1 : 4)))
 template <int MODE, bool STATS, bool LIST>
 __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
-    constexpr bool kCompact = (MODE == 0 || MODE == 3) && MSH_COMPACT;
+    constexpr bool kCompact = MODE == 0 || MODE == 3;  // per-lane queues dealt to the wave (else: per-lane rounds)
     constexpr bool kList = (MODE == 0 || MODE == 3) && LIST;  // a separate instantiation: its own registers
     // compacted leaf phases: kLeafQ entries per lane; the wave leaf list shares this space (a.list)
     constexpr size_t kEntWords = kCompact && !kList ? (size_t)kBlock * kLeafQ * 2 : 1;
@@ -629,26 +561,17 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         if (live && !fin) {  // no distance is defined: NO_FACE / NaN, no traversal
             if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
         }
-        double hint = INFINITY;
         int hint_leaf = -1;  // STATS
         if constexpr (MODE == 0 || MODE == 3) {
-            if (fin && (a.phase == 2 || (a.phase == 1 && kLead2 > 0))) {
-                if constexpr (kHintFace) {
-                    const int lf = a.phase == 2 ? leader_leaf(a, i, q, MSH_FWIN, kLead)
-                                                : leader_leaf(a, i, q, MSH_LWIN * kLead2, kLead2);
-                    if (STATS) hint_leaf = lf;
-                    if (lf >= 0) {
-                        pol.test(lf);
-                        if (STATS) {
-                            ++n_leaves;
-                            ++n_hinted;
-                        }
+            if (fin && (a.phase == 2 || a.phase == 1)) {
+                const int lf = a.phase == 2 ? leader_leaf(a, i, q, kFWin, kLead) : leader_leaf(a, i, q, kLWin * kLead2, kLead2);
+                if (STATS) hint_leaf = lf;
+                if (lf >= 0) {
+                    pol.test(lf);
+                    if (STATS) {
+                        ++n_leaves;
+                        ++n_hinted;
                     }
-                } else {
-                    hint = a.phase == 2 ? hint_from_leaders(a, i, q, MSH_FWIN, kLead)
-                                        : hint_from_leaders(a, i, q, MSH_LWIN * kLead2, kLead2);
-                    pol.shared = hint;
-                    pol.relim();
                 }
             }
         }
@@ -791,7 +714,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     ++nq;
                 }
                 tail += (unsigned)(__popcll(m1) + __popcll(m2));
-                if (tail - head >= (unsigned)MSH_ROUND_AT) run_rounds(head + ((tail - head) & ~63u));
+                if (tail - head >= 64u) run_rounds(head + ((tail - head) & ~63u));
             }
             if (STATS) {  // per-tile step profile of this phase (stats[8 + 9 * phase slot ...])
                 unsigned mx = tot, sm = tot;
@@ -852,31 +775,16 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             const unsigned max_steps = (unsigned)min(a.T, (size_t)UINT_MAX);
             unsigned tot = 0;  // STATS: node steps of this lane, restarts included
             // Wave-synchronous loop.  Lanes that reach leaves queue them; a lane keeps traversing while
-            // its queue has room for a node's two children.  Leaf tests run when the blocked lanes are
-            // at least 1/kLeafK of the traversing ones (or nobody can traverse), so the expensive fp64
-            // leaf path executes for many lanes at once instead of stalling the wave on one lane every
-            // iteration (Aila & Laine 2009, "postponed leaf" while-while).
+            // its queue has room for one more leaf.  Leaf tests run as soon as one lane is blocked (or nobody
+            // can traverse), so the expensive fp64 leaf path executes for many lanes at once instead of
+            // stalling the wave on one lane every iteration (Aila & Laine 2009, "postponed leaf" while-while).
             for (;;) {
-                // a hinted lane whose result is not below its hint re-runs unhinted (hint_from_leaders)
-                if (!active && !deferred && nq == 0 && hint != INFINITY && !(pol.best <= hint)) {
-                    hint = INFINITY;
-                    pol.shared = INFINITY;
-                    pol.relim();
-                    w = Walker{root, 0};
-                    steps = 0;
-                    active = true;
-                }
-                const bool can = active && nq <= kLeafQ - (kLeafPark ? 1 : 2);
+                const bool can = active && nq <= kLeafQ - 1;
                 const bool has = nq > 0;
                 const unsigned long long bl = __ballot(has);
                 const unsigned long long bt = __ballot(can);
                 if ((bl | bt) == 0ull) break;
-                const int nb = __popcll(__ballot(has && !can)), nt = __popcll(bt);
-                bool flush = nt == 0 || kLeafK * nb >= nt;
-                if constexpr (kCompact && kLeafFull > 0) {
-                    if (!flush && bl != 0ull)
-                        flush = __popcll(bl) + __popcll(__ballot(nq >= 2)) + __popcll(__ballot(nq >= 3)) >= kLeafFull;
-                }
+                const bool flush = bt == 0ull || __ballot(has && !can) != 0ull;
                 if (bl != 0ull && flush) {
                     if constexpr (kCompact) {
                         // Compacted leaf phase: the wave's queued leaves (newest first per lane) are dealt to
@@ -937,7 +845,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 }
                 if (STATS && lane == 0) {
                     ++u_trav_it;
-                    u_trav_lanes += nt;
+                    u_trav_lanes += __popcll(bt);
                 }
                 if (can) {
                     int l0 = -1, l1 = -1;
@@ -1047,10 +955,7 @@ __device__ inline double wave_min(double x) {
     return x;
 }
 
-#ifndef MSH_FRONT
-#define MSH_FRONT 512
-#endif
-constexpr int kFront = MSH_FRONT;  // pass 2: 2 kFront work-list entries per wave (LDS)
+constexpr int kFront = 512;  // pass 2: 2 kFront work-list entries per wave (LDS)
 
 template <int MODE, bool STATS>
 __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
@@ -1188,10 +1093,7 @@ __global__ __launch_bounds__(kBlock) void k_query_morton(const double* __restric
     vals[i] = (uint32_t)i;
 }
 
-#ifndef MSH_QBOX_MARGIN
-#define MSH_QBOX_MARGIN 0.1f
-#endif
-constexpr float kQueryBoxMargin = MSH_QBOX_MARGIN;
+constexpr float kQueryBoxMargin = 0.1f;
 int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* keys, uint32_t* vals, hipStream_t s) {
     if (S == 0) return MSH_OK;
     TimedLaunch tl("morton", s);
@@ -1284,25 +1186,13 @@ static int device_cus(int dev) {
     return cache[dev];
 }
 
-#ifndef MSH_BUDGET
-#define MSH_BUDGET 512
-#endif
-constexpr unsigned kBudget = MSH_BUDGET;  // pass-1 node steps per lane before a query is deferred
-#ifndef MSH_BUDGET3
-#define MSH_BUDGET3 256
-#endif
+constexpr unsigned kBudget = 512;  // pass-1 node steps per lane before a query is deferred
 // super-leaders: their launch has few tiles (C3: 6104 for 8192 wave slots), so its slowest tile sets its
 // length; with 256 steps the launch takes 1.4 instead of 2.9 ms and pass 2 gets ~18k more (cheap) items
 // (+0.4 ms).  A deferred super-leader publishes its best point so far as its leaders' hint.
-constexpr unsigned kBudget3 = MSH_BUDGET3;
-#ifndef MSH_BUDGET1
-#define MSH_BUDGET1 512
-#endif
-constexpr unsigned kBudget1 = MSH_BUDGET1;  // leaders (C3: 13.8 -> 12.6 ms, pass 2 +0.5 ms)
-#ifndef MSH_KNN_BPC
-#define MSH_KNN_BPC 4
-#endif
-constexpr unsigned kKnnBlocksPerCU = MSH_KNN_BPC;  // resident pass-1 blocks per CU (persistent grid)
+constexpr unsigned kBudget3 = 256;
+constexpr unsigned kBudget1 = 512;  // leaders (C3: 13.8 -> 12.6 ms, pass 2 +0.5 ms)
+constexpr unsigned kKnnBlocksPerCU = 4;  // resident pass-1 blocks per CU (persistent grid)
 
 // Common launch: grid, counters, spill area, deferred list; pass 1 then pass 2 (both also in STATS
 // mode, so the instrumented counts describe the traversal that is timed).
@@ -1318,21 +1208,15 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     a.n_deferred = a.counters + 8 * 32;
     MSH_HIP(hipMemsetAsync(a.counters, 0, 10 * 32 * sizeof(unsigned), s));  // + the pass-2 item counter
     // leader ordering: closest-point launches over a Morton-sorted slot order (records in a.res)
-// leader phases only for trees of >= MSH_LEAD_MIN_T leaves: on a small tree the hint saves little and the
+// leader phases only for trees of >= kLeadMinLeaves leaves: on a small tree the hint saves little and the
 // three dependent launches serialise their slowest tiles (C1: 0.56 -> 0.29 ms)
-#ifndef MSH_LEAD_MIN_T
-#define MSH_LEAD_MIN_T 4096
-#endif
     const bool lead = kLead > 1 && (MODE == 0 || MODE == 3) && a.res != nullptr && a.S >= 64 * (size_t)kLead &&
-                      a.T >= (size_t)MSH_LEAD_MIN_T;
+                      a.T >= kLeadMinLeaves;
     const size_t n_lead = (a.S + kLead - 1) / kLead;
     const unsigned max_tiles = (unsigned)((a.S + 63) / 64);
     const unsigned nblk_max = std::min<unsigned>((max_tiles + 3) / 4, ncu * kKnnBlocksPerCU);
     // pass 2 lanes carry up to 2 kFront/64 dealt subtrees on top of a depth-first path
-#ifndef MSH_P2_BLOCKS
-#define MSH_P2_BLOCKS 2
-#endif
-    const unsigned nblk2 = ncu * (unsigned)MSH_P2_BLOCKS;
+    const unsigned nblk2 = ncu * 2;  // pass 2: 2 blocks per CU
     const int need = tree->max_depth + 1 + 2 * kFront / 64 + 1;
     a.spill = nullptr;
     a.spill_depth = 0;
@@ -1344,7 +1228,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     a.budget = kBudget;
     {
         const char* e = getenv("MESH_AMD_LEAF_LIST");  // 0: per-lane leaf queues (the path of larger trees)
-        a.list = (MODE == 0 || MODE == 3) && MSH_LIST && !(e && atoi(e) == 0) && tree->B * tree->T < kListMaxLeaves;
+        a.list = (MODE == 0 || MODE == 3) && !(e && atoi(e) == 0) && tree->B * tree->T < kListMaxLeaves;
     }
     a.max_deferred = (unsigned)std::min<size_t>(a.S, (a.S / 16) + 65536);
     DevBuf& dbuf = ws.flags;
@@ -1356,10 +1240,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         // small trees: a query that walks T/16 nodes (the centre of a coarse closed mesh) goes to the
         // wave-cooperative pass 2 instead of holding its tile for up to T serial steps (C1, 840 faces:
         // traversal 1.15 -> 0.56 ms; with no leader phases below, 0.29 ms)
-#ifndef MSH_SMALL_DIV
-#define MSH_SMALL_DIV 16
-#endif
-        a.budget = std::min<unsigned>(a.budget, (unsigned)std::max<size_t>(64, a.T / MSH_SMALL_DIV));
+        a.budget = std::min<unsigned>(a.budget, (unsigned)std::max<size_t>(64, a.T / 16));
         a.nunits = nunits;
         a.ntiles = (unsigned)((nunits + 63) / 64);
         const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, ncu * kKnnBlocksPerCU);
@@ -1401,10 +1282,6 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     return MSH_OK;
 }
 
-#ifndef MSH_DIRECT_OUT
-#define MSH_DIRECT_OUT 1
-#endif
-constexpr bool kDirectOut = MSH_DIRECT_OUT;
 
 // Slot-order plumbing shared by the point-query launchers: with a permutation the kernels write 32-B
 // records (plus nw weights) into the workspace and k_unpermute scatters them to the caller's arrays.
@@ -1422,7 +1299,7 @@ static int run_knn(msh_tree* tree, KnnArgs a, const QueryOrder& ord, const SlotO
     if (ord.perm) {  // STATS launches keep the records too: followers take their hints from them
         MSH_TRY(ws.res.reserve(a.S * sizeof(QRes)));
         a.res = ws.res.as<QRes>();
-        a.direct = kDirectOut && !STATS && (MODE == 0 || MODE == 3);
+        a.direct = !STATS && (MODE == 0 || MODE == 3);
         a.rec_leaf = a.direct || STATS;
         if (nw && !a.direct) {
             MSH_TRY(ws.res_w.reserve(a.S * (size_t)nw * sizeof(double)));

@@ -277,14 +277,10 @@ __device__ inline unsigned dequeue_tile_r(unsigned* counters, unsigned ntiles, u
 
 __device__ inline bool finite_d3(const D3& x) { return isfinite(x.x) && isfinite(x.y) && isfinite(x.z); }
 
-#ifndef MSH_RAY_WAVES
-#define MSH_RAY_WAVES 4  // visibility: 4 waves per SIMD (127 VGPRs, no spills)
-#endif
-#ifndef MSH_ALONG_WAVES
-#define MSH_ALONG_WAVES 3  // alongnormal: at 4 waves the fp64 leaf test spills 37 VGPRs (C5: 7.41 vs 6.62 ms)
-#endif
+// waves per SIMD: visibility 4 (127 VGPRs, no spills); alongnormal 3 (at 4 the fp64 leaf test spills 37 VGPRs:
+// C5 7.41 vs 6.62 ms)
 template <int MODE, bool STATS>  // MODE 0 alongnormal, 1 visibility
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? MSH_ALONG_WAVES : MSH_RAY_WAVES))) void k_rays(RayArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? 3 : 4))) void k_rays(RayArgs a) {
     unsigned n_nodes = 0, n_leaves = 0;
     __shared__ uint2 stk[kStack * kBlock];
     const int tid = threadIdx.x, lane = tid & 63;
