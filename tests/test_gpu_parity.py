@@ -168,10 +168,14 @@ def test_c3_full_size_properties(oracle):
     dc = np.linalg.norm(cpt - q[idx], axis=1)
     assert np.all(np.abs(dg - dc) <= 1e-9 * diag)
     same = face[idx] == cf
-    # the icosphere is tie-heavy: queries outside project onto shared edges / vertices
-    assert same.mean() > 0.5
+    # the icosphere is tie-heavy (queries outside project onto shared edges / vertices), so the CGAL tree's
+    # traversal-order tie rule picks another face for some rows; where the faces agree the points are equal
     assert (pt[idx][same] == cpt[same]).all()
     assert np.all(np.abs(pt[idx] - cpt) <= 1e-6 * diag)
+    # and with the same tie rule (lexicographic (d2, face)) the exhaustive oracle agrees bit for bit
+    sub = idx[:1000]
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[sub])
+    assert np.array_equal(face[sub], bf) and np.array_equal(part[sub], bp) and np.array_equal(pt[sub], bpt)
 
 
 def test_c3_headline_stream(oracle):
