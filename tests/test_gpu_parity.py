@@ -517,7 +517,14 @@ def test_host_api_pinned_results(monkeypatch):
     monkeypatch.setenv("MESH_AMD_HOST_REGISTER", "1")
     for a, b in zip(spatialsearch.aabbtree_nearest(t, q), ref[0]):
         assert np.array_equal(a, b)
+    monkeypatch.delenv("MESH_AMD_HOST_REGISTER")
     assert N.lib().msh_host_pool_trim() == 0
+    # a pool too small for the block: the call falls back to pageable arrays with the same answer
+    monkeypatch.setenv("MESH_AMD_PINNED_POOL_MB", "4")
+    out = spatialsearch.aabbtree_nearest(t, q)  # 22 MB of results
+    assert out[0].base is None
+    for a, b in zip(out, ref[0]):
+        assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("name", ["ico", "ico60", "c2", "offset"])
