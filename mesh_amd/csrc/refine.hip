@@ -5,10 +5,12 @@
 // patches into slivers wherever the surface is oblique to the cycling planes, and a closest-point query
 // visits every node whose oriented box comes within its distance — ~3 per level.  Here every subtree of at
 // most K leaves is rebuilt top down, level by level over all subtrees at once: a node's primitives are split
-// at the spatial middle of the longest centroid spread among five directions, x, y, z and the two tangent
-// axes (t, b) of the node's own frame (the area-weighted normal of its triangles, t from the x or y axis, as
-// k_obb's frames).  Splitting along the surface keeps patches compact in the plane the oriented boxes are
-// thin across.  Host model (tools/bvh_model.cpp, C3 followers with leader hints): 68.0 -> 56.7 node visits.
+// at the spatial middle of the longer centroid spread along the two tangent axes (t, b) of the node's own
+// frame (the area-weighted normal of its triangles, t from the x or y axis, as k_obb's frames); x, y and z
+// only when neither tangent axis separates them.  Splitting along the surface, and along the axes of the
+// frame the children's boxes are taken in, keeps patches compact in the plane the oriented boxes are thin
+// across (C3: 77.2 node visits for the plain LBVH, 64.4 with the longest of the five spreads, 62.5 tangent
+// axes first).  Host model (tools/bvh_model.cpp, C3 followers with leader hints): 68.0 -> 56.7 node visits.
 // CGAL's own tree (spatialsearchmodule.cpp:122, AABB_tree::rebuild) is also a top-down split, at the median
 // of the longest axis of the primitives' box.
 //
@@ -18,7 +20,7 @@
 //   k_rb_frame      per segment: the frame (t, b), min / max slots reset
 //   k_rb_minmax     per position: projections of its centroid on x, y, z, t, b -> segment min / max
 //                   (ordered-int atomics; a wave whose lanes share a segment reduces first)
-//   k_rb_choose     per segment: the direction of largest spread and its middle (else: split by count)
+//   k_rb_choose     per segment: the tangent axis of larger spread (else x, y or z) and its middle (else: by count)
 //   k_rb_flags      per position: left of the split?  -> exclusive scan (sort.hip)
 //   k_rb_scatter    stable partition into the other order buffer; per segment the node record: id, range,
 //                   leaf children, the link from its parent, and the two child segments of the next level
@@ -37,13 +39,14 @@ namespace msh {
 
 constexpr uint32_t kInact = 0xFFFFFFFFu;    // position not in an active segment
 constexpr uint32_t kRootPar = 0xFFFFFFFFu;  // segment parent of the tree root (id 0)
+constexpr int kRbAxes = 5;  // split directions: x, y, z, t, b
 constexpr int kSpatialLevels = 40;          // deeper levels split by count (bounds the depth)
 
 struct RbSeg {
     float t[3], b[3];
     float mid;
-    int axis;  // 0..4 (x, y, z, t, b), -1: split by count
-    uint32_t mm[10];
+    int axis;  // 0..kRbAxes-1 (x, y, z, t, b, ...), -1: split by count
+    uint32_t mm[2 * kRbAxes];
 };
 
 __device__ inline uint32_t ford(float x) {
@@ -213,9 +216,9 @@ __global__ __launch_bounds__(kBlock) void k_rb_frame(const uint32_t* __restrict_
     g.t[0] = (float)t.x; g.t[1] = (float)t.y; g.t[2] = (float)t.z;
     g.b[0] = (float)bb.x; g.b[1] = (float)bb.y; g.b[2] = (float)bb.z;
 #pragma unroll
-    for (int k = 0; k < 5; ++k) {
+    for (int k = 0; k < kRbAxes; ++k) {
         g.mm[k] = 0xFFFFFFFFu;
-        g.mm[5 + k] = 0u;
+        g.mm[kRbAxes + k] = 0u;
     }
 }
 
@@ -233,21 +236,21 @@ __global__ __launch_bounds__(kBlock) void k_rb_minmax(const uint32_t* __restrict
     const size_t p = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const bool act = p < T && sb[p] != kInact;
     const uint32_t s = act ? sb[p] : kInact;
-    uint32_t v[10];
+    uint32_t v[2 * kRbAxes];
     if (act) {
         const float4 c = cen[idx[p]];
         const RbSeg& g = seg[s];
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
+        for (int k = 0; k < kRbAxes; ++k) {
             const uint32_t o = ford(rb_key(c, g, k));
             v[k] = o;
-            v[5 + k] = o;
+            v[kRbAxes + k] = o;
         }
     } else {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
+        for (int k = 0; k < kRbAxes; ++k) {
             v[k] = 0xFFFFFFFFu;
-            v[5 + k] = 0u;
+            v[kRbAxes + k] = 0u;
         }
     }
     // a wave whose active lanes all belong to one segment reduces first (the top levels: one atomic per wave)
@@ -259,23 +262,23 @@ __global__ __launch_bounds__(kBlock) void k_rb_minmax(const uint32_t* __restrict
 #pragma unroll
         for (int o = 32; o > 0; o >>= 1) {
 #pragma unroll
-            for (int k = 0; k < 5; ++k) {
+            for (int k = 0; k < kRbAxes; ++k) {
                 v[k] = min(v[k], (uint32_t)__shfl_xor((int)v[k], o));
-                v[5 + k] = max(v[5 + k], (uint32_t)__shfl_xor((int)v[5 + k], o));
+                v[kRbAxes + k] = max(v[kRbAxes + k], (uint32_t)__shfl_xor((int)v[kRbAxes + k], o));
             }
         }
         if ((threadIdx.x & 63) == (unsigned)first) {
 #pragma unroll
-            for (int k = 0; k < 5; ++k) {
+            for (int k = 0; k < kRbAxes; ++k) {
                 atomicMin(&seg[s0].mm[k], v[k]);
-                atomicMax(&seg[s0].mm[5 + k], v[5 + k]);
+                atomicMax(&seg[s0].mm[kRbAxes + k], v[kRbAxes + k]);
             }
         }
     } else if (act) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
+        for (int k = 0; k < kRbAxes; ++k) {
             atomicMin(&seg[s].mm[k], v[k]);
-            atomicMax(&seg[s].mm[5 + k], v[5 + k]);
+            atomicMax(&seg[s].mm[kRbAxes + k], v[kRbAxes + k]);
         }
     }
 }
@@ -289,9 +292,13 @@ __global__ __launch_bounds__(kBlock) void k_rb_choose(const uint32_t* __restrict
     float best = 0.f, mid = 0.f;
     if (level < kSpatialLevels) {
 #pragma unroll
-        for (int k = 0; k < 5; ++k) {
-            const float lo = unord(g.mm[k]), hi = unord(g.mm[5 + k]);
-            const float w = hi - lo, m = 0.5f * lo + 0.5f * hi;
+        for (int k = 0; k < kRbAxes; ++k) {
+            const float lo = unord(g.mm[k]), hi = unord(g.mm[kRbAxes + k]);
+            // the node frame's tangent axes take precedence: splitting along t or b keeps the children's boxes in
+            // that frame compact, x, y and z are the fallback (C3: 64.4 -> 62.5 node visits; spreads compared
+            // across all five: 64.4; diagonal tangent directions (t +- b)/sqrt2 added: 86.9 — their strips are
+            // wide along both axes of the boxes)
+            const float w = (hi - lo) * (k >= 3 ? 1e6f : 1.0f), m = 0.5f * lo + 0.5f * hi;
             // a usable split: finite, and the middle strictly inside (both sides non-empty)
             if (w > best && w < INFINITY && lo < m && m < hi) {
                 best = w;
