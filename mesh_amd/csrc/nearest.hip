@@ -503,16 +503,13 @@ __device__ inline int leader_leaf(const KnnArgs& a, size_t i, const D3& q, size_
     return leaf;
 }
 
-// Pass 1 runs 4 waves per SIMD: the register budget drops from 139 to 128 VGPRs at the cost of a few
-// spills of loop-invariant values outside the node step (C3: +10 % over the compiler's 3 waves).
 // Wave leaf list (closest-point modes): lanes append the leaf children that survive their node's bound to a
 // ring of (leaf << 6 | owner lane) entries in LDS shared by the wave, and the wave evaluates them in rounds of
 // 64 — one entry per lane, every round full except when nobody can move — instead of per-lane queues flushed
-// part-empty.  A lane stops traversing while kPend of its leaves wait.  Each round's
-// results reach their owners through LDS: an atomic min of the squared distance's bits per owner, then an
-// atomic min of (face << 32 | leaf) among the entries that reached it: the lexicographic (d2, face) rule.
-// kPend: unevaluated leaves a lane may hold before it stops traversing (3: 1236, 4: 1346, 8: 1593, 16: 1677,
-// 32: 1706, unbounded: 1689 M q/s; the per-lane queues measured 1541 in the same session)
+// part-empty.  A lane stops traversing while kPend of its leaves wait.  Each round's results reach their
+// owners through LDS: an atomic min of the squared distance's bits per owner, then an atomic min of
+// (face << 32 | leaf) among the entries that reached it: the lexicographic (d2, face) rule.
+// kPend (C3, M q/s): 3: 1236, 4: 1346, 8: 1593, 16: 1677, 32: 1706, unbounded: 1689; per-lane queues 1541.
 constexpr int kPend = 32;
 constexpr unsigned kRing = 256;     // ring entries per wave: < 64 left after full rounds + <= 128 per step
 constexpr size_t kListMaxLeaves = (size_t)1 << 26;  // leaf index bits of a ring entry
@@ -520,7 +517,8 @@ constexpr size_t kLeadMinLeaves = 4096;  // smaller trees skip the leader phases
 
 // Pass 1 runs 4 waves per SIMD (not the normals metric, MODE 1, whose larger live set would spill in the node
 // step): the register budget drops from 139 to 128 VGPRs at the cost of a few spills of loop-invariant values
-// outside the node step (C3: +10 % over the compiler's 3 waves; 5 waves spill in the loop: -30 %).
+// outside the node step (C3: +10 % over the compiler's 3 waves; 5 waves spill in the loop: -30 %; 5 waves also
+// need <= 32 KB of LDS per block).
 #define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 1 : 4)))
 template <int MODE, bool STATS, bool LIST>
 __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
