@@ -132,6 +132,27 @@ def test_c2_near_surface_bit_exact(oracle, monkeypatch, leaf_list):
     _assert_bit_exact_vs_brute(oracle, v, f, q)
 
 
+@pytest.mark.parametrize("leaf_list", ["1", "0"])
+def test_non_finite_queries(oracle, monkeypatch, leaf_list):
+    # NaN / inf rows (documented deviation: the reference's CGAL call is undefined for them) answer NO_FACE,
+    # part 0 and a NaN point; they sit among finite rows of a sorted launch with leader phases (C2 mesh: 13,776
+    # faces, 20k queries), so some of them are leaders whose records followers must skip; every finite row
+    # still matches brute force bit for bit
+    monkeypatch.setenv("MESH_AMD_LEAF_LIST", leaf_list)
+    v, f = W.c2_mesh()
+    q, _ = W.surface_samples(v, f, 20000, seed=41, sigma=0.01)
+    bad = np.random.default_rng(42).choice(q.shape[0], 800, replace=False)
+    vals = np.array([np.nan, np.inf, -np.inf])
+    q[bad, np.random.default_rng(43).integers(0, 3, bad.shape[0])] = vals[np.arange(bad.shape[0]) % 3]
+    q[bad[:8] - bad[:8] % 8] = np.nan  # whole rows at leader slots of the caller's order too
+    face, part, pt = _nearest(v, f, q)
+    nf = ~np.isfinite(q).all(axis=1)
+    assert nf.sum() >= 800
+    assert (face[nf] == 0xFFFFFFFF).all() and (part[nf] == 0).all() and np.isnan(pt[nf]).all()
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[~nf])
+    assert np.array_equal(face[~nf], bf) and np.array_equal(part[~nf], bp) and np.array_equal(pt[~nf], bpt)
+
+
 def test_c3_sample_both_leaf_paths(oracle, monkeypatch):
     # C3 mesh, 200k uniform queries (leader phases on): the wave leaf list and the per-lane queues give the
     # same arrays, and both match brute force on a 2000-row sample
