@@ -1,10 +1,12 @@
-"""One-off parity sweep of the C3 headline stream (not part of the test suite: it takes about a minute of
-host brute force).  Runs bench.py's exact query stream (100M uniform queries generated in HBM, seed 3)
-through the device entry point, then checks K random rows plus the rows nearest the sphere's centre (the
-deferred pass-2 queries) bit for bit against the oracle's exhaustive brute force (same tie rule), and
-prints one JSON line.
+"""One-off parity sweeps at full config sizes (not part of the test suite: each takes up to a minute of host
+brute force), one JSON line per config:
+  c3  bench.py's exact query stream (100M uniform queries generated in HBM, seed 3) through the device entry
+      point; K random rows plus the rows nearest the sphere's centre (the deferred pass-2 queries);
+  c2  the 10M C2 queries through the numpy entry point (aabbtree_nearest); K random rows;
+  c5  the 10M C5 nearest_alongnormal rays through the numpy entry point; K random rays.
+Every checked row must equal the oracle's exhaustive brute force bit for bit (same tie rule).
 
-    python scripts/parity_sweep.py [--rows 20000] [--centre 2000]
+    python scripts/parity_sweep.py [--configs c3,c2,c5] [--rows 20000] [--centre 2000]
 """
 import argparse
 import json
@@ -18,18 +20,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--rows", type=int, default=20000)
-    ap.add_argument("--centre", type=int, default=2000)
-    args = ap.parse_args()
+def sweep_c3(args):
     import torch
     from mesh_amd import _native, spatialsearch
     from mesh_amd.distributed import nearest_device
     from oracle import oracle as O
     import workloads as W
-
-    _native.set_device(0)
     v, f = W.c3_mesh()
     S = 100_000_000
     g = torch.Generator(device="cuda:0")
@@ -42,6 +38,7 @@ def main():
     nearest_device(t, dq, df, dp, dpt)
     torch.cuda.synchronize()
     q = dq.cpu().numpy()
+    del dq
     face = df.cpu().numpy().view(np.uint32)
     part = dp.cpu().numpy().view(np.uint32)
     pt = dpt.cpu().numpy()
@@ -49,16 +46,69 @@ def main():
     idx = np.concatenate([np.random.default_rng(11).choice(S, args.rows, replace=False),
                           np.argpartition(r, args.centre)[:args.centre]])
     t0 = time.perf_counter()
-    bf, bp, bpt, _ = O.brute_nearest(v, f, q[idx])
-    brute_s = time.perf_counter() - t0
+    chunks = []
+    for c0 in range(0, idx.size, 10000):  # progress lines: a long silent brute force looks hung on the GPU box
+        chunks.append(O.brute_nearest(v, f, q[idx[c0:c0 + 10000]]))
+        print("c3 brute force: %d / %d rows" % (min(c0 + 10000, idx.size), idx.size), file=sys.stderr, flush=True)
+    bf, bp, bpt = (np.concatenate([c[k] for c in chunks]) for k in range(3))
     bad = np.nonzero((face[idx] != bf) | (part[idx] != bp) | np.any(pt[idx] != bpt, axis=1))[0]
-    print(json.dumps({"workload": "C3 headline stream (100M uniform queries, seed 3, device entry point)",
-                      "build_id": _native.build_id(), "rows_checked": int(idx.size),
-                      "random_rows": args.rows, "centre_rows": args.centre, "mismatches": int(bad.size),
-                      "first_mismatch_rows": idx[bad[:10]].tolist(), "brute_force_s": brute_s,
-                      "check": "face, part code and point bit-exact vs oracle.brute_nearest (lexicographic (d2, face))"}),
-          flush=True)
-    sys.exit(1 if bad.size else 0)
+    return dict(workload="C3 headline stream (100M uniform queries, seed 3, device entry point)",
+                random_rows=args.rows, centre_rows=args.centre, rows_checked=int(idx.size), mismatches=int(bad.size),
+                first_mismatch_rows=idx[bad[:10]].tolist(), brute_force_s=time.perf_counter() - t0,
+                check="face, part code and point bit-exact vs oracle.brute_nearest (lexicographic (d2, face))")
+
+
+def sweep_c2(args):
+    from mesh_amd import spatialsearch
+    from oracle import oracle as O
+    import workloads as W
+    v, f = W.c2_mesh()
+    q = W.c2_queries()
+    face, part, pt = spatialsearch.aabbtree_nearest(spatialsearch.aabbtree_compute(v, f), q)
+    idx = np.random.default_rng(12).choice(q.shape[0], 5 * args.rows, replace=False)
+    t0 = time.perf_counter()
+    bf, bp, bpt, _ = O.brute_nearest(v, f, q[idx])
+    bad = np.nonzero((face[0][idx] != bf) | (part[0][idx] != bp) | np.any(pt[idx] != bpt, axis=1))[0]
+    return dict(workload="C2 10M near-surface queries (numpy entry point aabbtree_nearest)", rows_checked=int(idx.size),
+                mismatches=int(bad.size), first_mismatch_rows=idx[bad[:10]].tolist(), brute_force_s=time.perf_counter() - t0,
+                check="face, part code and point bit-exact vs oracle.brute_nearest")
+
+
+def sweep_c5(args):
+    from mesh_amd import spatialsearch
+    from oracle import oracle as O
+    import workloads as W
+    v, f = W.c5_mesh()
+    p, n, _, _ = W.c5_rays(v, f)
+    d, face, pt = spatialsearch.aabbtree_nearest_alongnormal(spatialsearch.aabbtree_compute(v, f), p, n)
+    idx = np.random.default_rng(13).choice(p.shape[0], args.rows // 5, replace=False)
+    t0 = time.perf_counter()
+    bd, bf, bpt = O.brute_alongnormal(v, f, p[idx], n[idx])
+    hit = bd < 1e100
+    same_pt = np.all((pt[idx] == bpt) | ~hit[:, None], axis=1)
+    bad = np.nonzero((d[idx] != bd) | (face[idx] != bf) | ~same_pt)[0]
+    return dict(workload="C5 10M nearest_alongnormal rays on the 5M-face bumped icosphere (numpy entry point)",
+                rows_checked=int(idx.size), mismatches=int(bad.size), first_mismatch_rows=idx[bad[:10]].tolist(),
+                misses=int((~hit).sum()), brute_force_s=time.perf_counter() - t0,
+                check="dist, face and (for hits) point bit-exact vs oracle.brute_alongnormal")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="c3")
+    ap.add_argument("--rows", type=int, default=20000)
+    ap.add_argument("--centre", type=int, default=2000)
+    args = ap.parse_args()
+    from mesh_amd import _native
+    _native.set_device(0)
+    fails = 0
+    for c in args.configs.split(","):
+        r = {"c3": sweep_c3, "c2": sweep_c2, "c5": sweep_c5}[c](args)
+        r["config"] = c
+        r["build_id"] = _native.build_id()
+        fails += r["mismatches"]
+        print(json.dumps(r), flush=True)
+    sys.exit(1 if fails else 0)
 
 
 if __name__ == "__main__":
