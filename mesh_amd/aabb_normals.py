@@ -39,8 +39,7 @@ def aabbtree_n_nearest(tree, v, n):
     v = np.ascontiguousarray(v, dtype=np.float64)
     n = np.ascontiguousarray(n, dtype=np.float64)
     S = v.shape[0]
-    face = np.empty((1, S), dtype=np.uint32)
-    pt = np.empty((S, 3), dtype=np.float64)
+    face, pt = N.empty_results(((1, S), np.uint32), ((S, 3), np.float64))
     N.check(N.lib().msh_ntree_nearest(tree.ptr, N.dptr(v), N.dptr(n), S, N.uptr(face), N.dptr(pt)))
     return face, pt
 

@@ -1192,34 +1192,17 @@ int msh_ntree_nearest(msh_tree* t, const double* q, const double* n, size_t S, u
     MSH_TRY(check_tree(t, kNormals, "msh_ntree_nearest"));
     MSH_TRY(check_count(S, "msh_ntree_nearest"));
     if (S == 0) return MSH_OK;
-    hipStream_t s = t->stream;
-    Workspace& ws = t->ws;
-    int st = MSH_OK;
-    {
+    if (!q || !n || !face || !pt) { set_error("msh_ntree_nearest: null argument"); return MSH_EINVAL; }
+    // rows: q (24 B in) | n (24 B in) | face (4 B out) | point (24 B out); chunked like msh_tree_nearest
+    const std::vector<HostArr> arrs = {{q, nullptr, 24}, {n, nullptr, 24}, {nullptr, face, 4}, {nullptr, pt, 24}};
+    return pipelined(t, S, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
+        hipStream_t s = t->stream;
         WsOrder order(t, s);
-        do {
-            if ((st = upload(ws.q, q, 3 * S, s)) != MSH_OK) break;
-            if ((st = upload(ws.n, n, 3 * S, s)) != MSH_OK) break;
-            if ((st = ws.out_a.reserve(S * sizeof(uint32_t))) != MSH_OK) break;
-            if ((st = ws.out_c.reserve(3 * S * sizeof(double))) != MSH_OK) break;
-            QueryOrder ord;
-            if ((st = sort_queries(t, ws.q.as<double>(), ws.n.as<double>(), S, s, &ord)) != MSH_OK) break;
-            if ((st = launch_nnearest(t, ord, S, SlotOut{ws.out_a.as<uint32_t>(), nullptr, ws.out_c.as<double>(), nullptr,
-                                                        nullptr}, s)) != MSH_OK)
-                break;
-            hipError_t e;
-            if ((e = hipMemcpyAsync(face, ws.out_a.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-                (e = hipMemcpyAsync(pt, ws.out_c.ptr, 3 * S * sizeof(double), hipMemcpyDeviceToHost, s)) != hipSuccess) {
-                set_error("normals nearest: %s", hipGetErrorString(e));
-                st = MSH_EDEVICE;
-            }
-        } while (0);
-    }
-    if (hipStreamSynchronize(s) != hipSuccess && st == MSH_OK) {
-        set_error("normals nearest: kernel failure");
-        st = MSH_EDEVICE;
-    }
-    return st;
+        QueryOrder ord;
+        MSH_TRY(sort_queries(t, reinterpret_cast<const double*>(d[0]), reinterpret_cast<const double*>(d[1]), c, s, &ord));
+        return launch_nnearest(t, ord, c, SlotOut{reinterpret_cast<uint32_t*>(d[2]), nullptr, reinterpret_cast<double*>(d[3]),
+                                                  nullptr, nullptr}, s);
+    });
 }
 
 int msh_ntree_selfintersects(msh_tree* t, int64_t* count) {
@@ -1300,33 +1283,17 @@ int msh_points_nearest(msh_tree* t, const double* q, size_t S, uint32_t* idx, do
     MSH_TRY(check_tree(t, kPoints, "msh_points_nearest"));
     MSH_TRY(check_count(S, "msh_points_nearest"));
     if (S == 0) return MSH_OK;
-    hipStream_t s = t->stream;
-    Workspace& ws = t->ws;
-    int st = MSH_OK;
-    {
+    if (!q || !idx || !dist) { set_error("msh_points_nearest: null argument"); return MSH_EINVAL; }
+    // rows: q (24 B in) | index (4 B out) | distance (8 B out); chunked like msh_tree_nearest
+    const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, idx, 4}, {nullptr, dist, 8}};
+    return pipelined(t, S, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
+        hipStream_t s = t->stream;
         WsOrder order(t, s);
-        do {
-            if ((st = upload(ws.q, q, 3 * S, s)) != MSH_OK) break;
-            if ((st = ws.out_a.reserve(S * sizeof(uint32_t))) != MSH_OK) break;
-            if ((st = ws.out_c.reserve(S * sizeof(double))) != MSH_OK) break;
-            QueryOrder ord;
-            if ((st = sort_queries(t, ws.q.as<double>(), nullptr, S, s, &ord)) != MSH_OK) break;
-            if ((st = launch_points_nearest(t, ord, S, SlotOut{ws.out_a.as<uint32_t>(), nullptr, nullptr,
-                                                                ws.out_c.as<double>(), nullptr}, s)) != MSH_OK)
-                break;
-            hipError_t e;
-            if ((e = hipMemcpyAsync(idx, ws.out_a.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-                (e = hipMemcpyAsync(dist, ws.out_c.ptr, S * sizeof(double), hipMemcpyDeviceToHost, s)) != hipSuccess) {
-                set_error("points nearest: %s", hipGetErrorString(e));
-                st = MSH_EDEVICE;
-            }
-        } while (0);
-    }
-    if (hipStreamSynchronize(s) != hipSuccess && st == MSH_OK) {
-        set_error("points nearest: kernel failure");
-        st = MSH_EDEVICE;
-    }
-    return st;
+        QueryOrder ord;
+        MSH_TRY(sort_queries(t, reinterpret_cast<const double*>(d[0]), nullptr, c, s, &ord));
+        return launch_points_nearest(t, ord, c, SlotOut{reinterpret_cast<uint32_t*>(d[1]), nullptr, nullptr,
+                                                        reinterpret_cast<double*>(d[2]), nullptr}, s);
+    });
 }
 
 // ---- mesh geometry ----

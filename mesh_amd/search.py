@@ -80,8 +80,7 @@ class ClosestPointTree(object):
     def _query(self, v_samples):
         q = _f64c(v_samples).reshape(-1, 3)
         S = q.shape[0]
-        idx = np.empty(S, dtype=np.uint32)
-        dist = np.empty(S, dtype=np.float64)
+        idx, dist = N.empty_results(((S,), np.uint32), ((S,), np.float64))
         N.check(N.lib().msh_points_nearest(self._h.ptr, N.dptr(q), S, N.uptr(idx), N.dptr(dist)))
         return idx.astype(np.intp), dist
 

@@ -548,6 +548,41 @@ def test_host_api_pinned_results(monkeypatch):
         assert np.array_equal(a, b)
 
 
+def test_normals_and_points_host_chunked(oracle, monkeypatch):
+    # aabb_normals.aabbtree_n_nearest and ClosestPointTree run through the chunked host pipeline (pinned result
+    # arrays, several chunks) and give exactly the answers of small unchunked calls on the same rows; a sample
+    # matches brute force
+    from mesh_amd import _native as N, aabb_normals
+    from mesh_amd.mesh import Mesh
+    from mesh_amd.search import ClosestPointTree
+    v, f = W.c2_mesh()
+    q, fi = W.surface_samples(v, f, 400000, seed=51, sigma=0.01)
+    tri = v[f[fi].astype(np.int64)]
+    n = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
+    n /= np.linalg.norm(n, axis=1)[:, None]
+    n += np.random.default_rng(52).normal(scale=0.2, size=n.shape)
+    monkeypatch.setattr(N, "PINNED_MIN_BYTES", 1 << 20)
+    monkeypatch.setenv("MESH_AMD_HOST_CHUNK", "131072")  # 4 chunks: both slabs reused
+    h = aabb_normals.aabbtree_n_compute(v, f, 0.1)
+    face, pt = aabb_normals.aabbtree_n_nearest(h, q, n)
+    owner = face
+    while isinstance(owner, np.ndarray):
+        owner = owner.base
+    assert isinstance(owner, N._PinnedBlock)
+    parts = [aabb_normals.aabbtree_n_nearest(h, q[k:k + 50000], n[k:k + 50000]) for k in range(0, q.shape[0], 50000)]
+    assert np.array_equal(face, np.concatenate([p[0] for p in parts], axis=1))
+    assert np.array_equal(pt, np.concatenate([p[1] for p in parts]))
+    rows = np.random.default_rng(53).choice(q.shape[0], 3000, replace=False)
+    bf, bpt = oracle.brute_nnearest(v, f, 0.1, q[rows], n[rows])[:2]
+    assert np.array_equal(face[0][rows], np.asarray(bf).reshape(-1)) and np.array_equal(pt[rows], bpt)
+    t = ClosestPointTree(Mesh(v=v, f=f))
+    idx, dist = t._query(q)
+    pidx = np.concatenate([t._query(q[k:k + 50000])[0] for k in range(0, q.shape[0], 50000)])
+    assert np.array_equal(idx, pidx)
+    bi, bd = oracle.brute_vertex_nn(v, q[rows])
+    assert np.array_equal(idx[rows], np.asarray(bi).astype(idx.dtype)) and np.array_equal(dist[rows], bd)
+
+
 @pytest.mark.parametrize("name", ["ico", "ico60", "c2", "offset"])
 def test_tree_bounds_contain_primitives(name):
     # every child's quantised oriented box (frame n, t, n x t) contains all vertices below it
