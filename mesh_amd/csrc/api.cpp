@@ -165,6 +165,7 @@ static void free_tree(msh_tree* t) {
     if (t->d_leaves) (void)hipFree(t->d_leaves);
     if (t->d_vorder) (void)hipFree(t->d_vorder);
     if (t->d_vorder_shard) (void)hipFree(t->d_vorder_shard);
+    if (t->d_cut) (void)hipFree(t->d_cut);
     for (int b = 0; b < 2; ++b) {
         if (t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
         if (t->d_stage[b]) (void)hipFree(t->d_stage[b]);
@@ -211,6 +212,63 @@ struct WsOrder {
     }
 };
 
+// Entry cut of a single triangle tree (nearest.hip cut_start / k_cut_build): a G^3 grid over the scene box
+// widened by 1/4 on every side (each axis at least 1/20 of the largest, so flat meshes get cells of a sane
+// shape), ~2 cells per leaf up to 2^22 cells (C3: G = 126, 2M cells, 128 MB); the cell centres are answered
+// by the tree itself, then every cell's start entries are cut from the root.  Trees under kCutMinLeaves
+// leaves start at the root (their top levels are few).  MESH_AMD_ENTRY_CUT=0 turns it off (A/B).
+constexpr size_t kCutMinLeaves = 4096;
+static int build_entry_cut(msh_tree* t) {
+    const char* env = getenv("MESH_AMD_ENTRY_CUT");
+    if ((env && atoi(env) == 0) || t->kind != kTriangles || t->B != 1 || t->T < kCutMinLeaves || !t->d_nodes)
+        return MSH_OK;
+    const size_t cells = std::min<size_t>(2 * t->T, (size_t)1 << 22);
+    int G = std::max(16, (int)std::lround(std::cbrt((double)cells)));
+    if (const char* eg = getenv("MESH_AMD_CUT_G")) G = std::max(4, std::min(256, atoi(eg)));
+    double half[3], H = 0.0, lo[3], w[3];
+    for (int k = 0; k < 3; ++k) {
+        half[k] = 0.5 * ((double)t->scene_hi[k] - (double)t->scene_lo[k]);
+        H = std::max(H, half[k]);
+    }
+    if (!(H > 0.0) || !std::isfinite(H)) return MSH_OK;
+    for (int k = 0; k < 3; ++k) {
+        const double m = 0.5 * ((double)t->scene_hi[k] + (double)t->scene_lo[k]);
+        const double e = 1.25 * std::max(half[k], 0.05 * H);
+        lo[k] = m - e;
+        w[k] = 2.0 * e / G;
+    }
+    const size_t n = (size_t)G * G * G;
+    hipStream_t s = t->stream;
+    DevBuf dq, df, dp;
+    MSH_TRY(dq.reserve(n * 3 * sizeof(double)));
+    MSH_TRY(df.reserve(n * sizeof(uint32_t)));
+    MSH_TRY(dp.reserve(n * 3 * sizeof(double)));
+    MSH_TRY(cut_centres(G, lo, w, dq.as<double>(), s));
+    MSH_TRY(msh_tree_nearest_device(t, dq.as<double>(), n, df.as<uint32_t>(), nullptr, dp.as<double>(), s));
+    uint2* cut = nullptr;
+    hipError_t e = hipMalloc(&cut, n * kCutK * sizeof(uint2));
+    if (e != hipSuccess) {
+        set_error("hipMalloc entry cut: %s", hipGetErrorString(e));
+        return MSH_ENOMEM;
+    }
+    int st = cut_build(t, G, lo, w, dp.as<double>(), cut, s);
+    if (st == MSH_OK && (e = hipStreamSynchronize(s)) != hipSuccess) {
+        set_error("entry cut build: %s", hipGetErrorString(e));
+        st = MSH_EDEVICE;
+    }
+    if (st != MSH_OK) {
+        (void)hipFree(cut);
+        return st;
+    }
+    t->d_cut = cut;
+    t->cut_G = G;
+    for (int k = 0; k < 3; ++k) {
+        t->cut_lo[k] = lo[k];
+        t->cut_iw[k] = 1.0 / w[k];
+    }
+    return MSH_OK;
+}
+
 // Triangle tree over v (P rows) and f (T rows, indices into v).
 // Subtrees of the LBVH over at most 2^kResplitLog2 leaves are rebuilt top down along the surface (refine.hip;
 // C3: 2^12 and 2^17 measured slower, profiles/r03_c3_resplit_ab.jsonl)
@@ -244,6 +302,7 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
                                   static_cast<TriRec*>(t->d_leaves), s)) != MSH_OK)
             break;
         if ((st = build_obb(t, true)) != MSH_OK) break;
+        if ((st = build_entry_cut(t)) != MSH_OK) break;
         (void)hipEventRecord(e1, s);
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) { set_error("LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
@@ -902,6 +961,10 @@ int msh_tree_build(const double* v, size_t P, const uint32_t* f, size_t T, msh_t
 int msh_ntree_build(const double* v, size_t P, const uint32_t* f, size_t T, double eps, msh_tree** out) {
     MSH_TRY(msh_tree_build_ex(v, P, f, T, nullptr, 0, nullptr, 0, out));
     (*out)->kind = kNormals;
+    if ((*out)->d_cut) {  // the normals metric starts at the root
+        (void)hipFree((*out)->d_cut);
+        (*out)->d_cut = nullptr;
+    }
     (*out)->eps = eps;
     return MSH_OK;
 }
@@ -1537,7 +1600,9 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
         if (hipStreamSynchronize(t->stream) != hipSuccess) {
             set_error("blob unpack: origin upload failed");
             st = MSH_EDEVICE;
+            break;
         }
+        st = build_entry_cut(t);  // derived from the tree: rebuilt here, not shipped
         t->ws.release();
     } while (0);
     if (st != MSH_OK) {

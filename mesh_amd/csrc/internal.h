@@ -118,6 +118,11 @@ struct msh_tree {
     hipEvent_t e_up[2] = {nullptr, nullptr}, e_run[2] = {nullptr, nullptr}, e_down[2] = {nullptr, nullptr};
     double build_ms = 0.0;
     int max_depth = 0;             // bound of the deepest leaf (root children = 1): k_karras prefix lengths
+    // entry cut (single triangle trees; nearest.hip build_entry_cut): a G^3 grid over the scene box widened by
+    // 1/4, kCutK start entries per cell; d_cut == nullptr: every query starts at the root
+    uint2* d_cut = nullptr;
+    int cut_G = 0;
+    double cut_lo[3] = {0, 0, 0}, cut_iw[3] = {0, 0, 0};
     msh::Workspace ws;
 };
 
@@ -172,6 +177,11 @@ int gather_rows(const double* d_a, const double* d_b, const uint32_t* d_perm, si
 // caller row j <- slot inv[j] (record fields + nw doubles per row from d_w)
 int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32_t* d_inv, size_t S, const SlotOut& o,
                       hipStream_t s);
+// Entry cut of a single triangle tree: the start entries of every grid cell from the exact closest points
+// of the cell centres (d_pts, G^3 rows, answered by the tree itself), written to tree->d_cut (kCutK per cell)
+constexpr int kCutK = 8;
+int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s);
+int cut_build(msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, uint2* d_cut, hipStream_t s);
 // closest point: o.face, o.part (nullable), o.pt; with o.w (3 per row) the barycentric variant (part unused)
 int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s);
 // batched trees: n = B*S queries, slot i answered on mesh i / S (the batched sort is mesh-major)

@@ -98,6 +98,11 @@ struct KnnArgs {
     // field carries the winner's leaf index instead of its part code (leader_leaf)
     bool rec_leaf;
     bool list;      // closest-point modes: wave leaf list (trees of < 2^26 leaves) instead of per-lane queues
+    // entry cut (list path; single trees): a query inside the grid starts from its cell's entries instead of
+    // the root (build_entry_cut); nullptr: from the root
+    const uint2* cut;
+    int cut_G;
+    double cut_lo[3], cut_iw[3];
     size_t nunits;  // work units of this phase (slots it covers)
     DeferRec* deferred;
     unsigned* n_deferred;
@@ -520,6 +525,39 @@ constexpr size_t kLeadMinLeaves = 4096;  // smaller trees skip the leader phases
 // outside the node step (C3: +10 % over the compiler's 3 waves; 5 waves spill in the loop: -30 %; 5 waves also
 // need <= 32 KB of LDS per block).
 #define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 1 : 4)))
+// Entry cut.  The grid cell of q (centre c, half-diagonal r) holds up to kCutK tree entries (node or ~leaf)
+// whose bound from c is within (d(c) + 2r)^2, d(c) = c's exact distance to the mesh, and which together cover
+// every such subtree; any other subtree lies farther than d(c) + 2r from c, so farther than d(c) + r >= d(q)
+// from q, and can hold neither q's closest face nor a tie.  Each entry carries max(s, 0)^2 rounded down,
+// s = sqrt(bound from c) - r: a lower bound of the squared distance from q to its subtree.  The entries go
+// on the stack with it, nearest to c popped first, and the walk starts from the first entry within the
+// current limit.  false: no entry survives the hint's bound (the hint is the answer).
+constexpr uint32_t kCutEmpty = 0x7FFFFFFFu;  // not a node id (ids < T - 1 <= 2^31 - 2) nor a ~leaf
+template <class Pol>
+__device__ inline bool cut_start(const KnnArgs& a, const D3& q, const Pol& pol, Walker& w, uint2* __restrict__ lds,
+                                 uint2* __restrict__ spill) {
+    const double G = (double)a.cut_G;
+    const double ux = (q.x - a.cut_lo[0]) * a.cut_iw[0], uy = (q.y - a.cut_lo[1]) * a.cut_iw[1],
+                 uz = (q.z - a.cut_lo[2]) * a.cut_iw[2];
+    if (!(ux >= 0.0 && ux < G && uy >= 0.0 && uy < G && uz >= 0.0 && uz < G)) return true;  // outside: the root
+    const size_t cell = ((size_t)(unsigned)uz * (size_t)a.cut_G + (unsigned)uy) * (size_t)a.cut_G + (unsigned)ux;
+    const uint4* c = reinterpret_cast<const uint4*>(a.cut + cell * kCutK);
+    const uint4 e0 = c[0], e1 = c[1], e2 = c[2], e3 = c[3];
+    auto put = [&](uint32_t ref, uint32_t sb) {
+        if (ref == kCutEmpty) return;
+        w.push(make_uint2(ref, sb), lds, spill);
+    };
+    put(e3.z, e3.w);
+    put(e3.x, e3.y);
+    put(e2.z, e2.w);
+    put(e2.x, e2.y);
+    put(e1.z, e1.w);
+    put(e1.x, e1.y);
+    put(e0.z, e0.w);
+    put(e0.x, e0.y);
+    return w.pop(pol, lds, spill);
+}
+
 template <int MODE, bool STATS, bool LIST>
 __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     __shared__ uint2 stk[kStack * kBlock];
@@ -586,11 +624,13 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             QF qf;
             const int root = query_root(a, i, q, qf);
             Walker w{root, 0};
+            bool start = fin;
+            if (a.cut && fin) start = cut_start(a, q, pol, w, lds, spill);
             uint32_t* ring = lsh + (tid >> 6) * (kRing + 64 * 4);
             unsigned long long* bd = reinterpret_cast<unsigned long long*>(ring + kRing);  // per owner: d2 bits
             unsigned long long* bfl = bd + 64;                                              // (face << 32 | leaf)
             const unsigned long long lt = (1ull << lane) - 1ull;
-            bool active = fin, want_defer = false, deferred = false;
+            bool active = start, want_defer = false, deferred = false;
             int nq = 0;              // this lane's leaves appended since all of them were last evaluated (a bound)
             unsigned last_pos = 0;   // ring counter of this lane's newest entry
             unsigned head = 0, tail = 0;  // wave-uniform ring counters: entries [head, tail) wait
@@ -1215,7 +1255,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     const unsigned nblk_max = std::min<unsigned>((max_tiles + 3) / 4, ncu * kKnnBlocksPerCU);
     // pass 2 lanes carry up to 2 kFront/64 dealt subtrees on top of a depth-first path
     const unsigned nblk2 = ncu * 2;  // pass 2: 2 blocks per CU
-    const int need = tree->max_depth + 1 + 2 * kFront / 64 + 1;
+    const int need = tree->max_depth + 1 + 2 * kFront / 64 + 1 + (a.cut ? kCutK : 0);
     a.spill = nullptr;
     a.spill_depth = 0;
     if (need > kStack) {
@@ -1332,8 +1372,20 @@ static KnnArgs tree_args(const msh_tree* tree, size_t S) {
     return a;
 }
 
+// the entry cut of a single tree (list path of the closest-point modes)
+static void cut_args(const msh_tree* tree, KnnArgs& a) {
+    if (!tree->d_cut || tree->B != 1) return;
+    a.cut = tree->d_cut;
+    a.cut_G = tree->cut_G;
+    for (int k = 0; k < 3; ++k) {
+        a.cut_lo[k] = tree->cut_lo[k];
+        a.cut_iw[k] = tree->cut_iw[k];
+    }
+}
+
 int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s) {
     KnnArgs a = tree_args(tree, S);
+    cut_args(tree, a);
     SlotOut oo = o;
     oo.dist = nullptr;
     if (o.w) {
@@ -1361,6 +1413,7 @@ int launch_nearest_batch(const msh_tree* tree, const QueryOrder& ord, size_t n, 
 int launch_nearest_stats(const msh_tree* tree, const QueryOrder& ord, size_t S, unsigned long long* d_counts,
                          hipStream_t s) {
     KnnArgs a = tree_args(tree, S);
+    cut_args(tree, a);
     a.stats = d_counts;
     return run_knn<0, true>(const_cast<msh_tree*>(tree), a, ord, SlotOut{}, 0, s, "nearest_stats");
 }
@@ -1382,6 +1435,122 @@ int launch_points_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S,
     oo.face = o.face;
     oo.dist = o.dist;
     return run_knn<2, false>(const_cast<msh_tree*>(tree), a, ord, oo, 0, s, "points_nearest");
+}
+
+// ---- entry cut (build time) ----
+// cell (ix, iy, iz) = row (iz G + iy) G + ix; centre lo + (i + 1/2) w per axis
+__global__ __launch_bounds__(kBlock) void k_cut_centres(int G, double lx, double ly, double lz, double wx, double wy,
+                                                        double wz, double* __restrict__ q) {
+    const size_t n = (size_t)G * G * G;
+    const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (cell >= n) return;
+    const size_t ix = cell % (size_t)G, iy = (cell / (size_t)G) % (size_t)G, iz = cell / ((size_t)G * G);
+    q[3 * cell] = lx + ((double)ix + 0.5) * wx;
+    q[3 * cell + 1] = ly + ((double)iy + 0.5) * wy;
+    q[3 * cell + 2] = lz + ((double)iz + 0.5) * wz;
+}
+
+// One thread per cell.  From the root, entries (internal nodes or ~leaves) are replaced by their children
+// whose bound from the centre c is within R^2 = ((d(c) + 2r) (1 + 1e-6))^2 (r = the cell's half-diagonal
+// + 0.1 %, so a query rounded into a neighbouring cell stays covered), in passes over the list, while the
+// list keeps at most kCutK entries; a child outside R is dropped (the cull is the traversal's own: bound >
+// fp32(R^2 (1 + 2^-40)) rounded up).  Out: entries nearest-first, (ref, max(s, 0)^2 rounded down to fp32 with
+// s = sqrt(bound) (1 - 1e-5) - r (1 + 1e-5)), unused ones kCutEmpty; a centre without an answer keeps the root.
+__global__ __launch_bounds__(kBlock) void k_cut_build(const BNode* __restrict__ nodes, double ox, double oy, double oz,
+                                                      double tm, int G, double lx, double ly, double lz, double wx,
+                                                      double wy, double wz, const double* __restrict__ pts,
+                                                      uint2* __restrict__ cut) {
+    const size_t n = (size_t)G * G * G;
+    const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (cell >= n) return;
+    const size_t ix = cell % (size_t)G, iy = (cell / (size_t)G) % (size_t)G, iz = cell / ((size_t)G * G);
+    const D3 c = D3{lx + ((double)ix + 0.5) * wx, ly + ((double)iy + 0.5) * wy, lz + ((double)iz + 0.5) * wz};
+    const D3 p = D3{pts[3 * cell], pts[3 * cell + 1], pts[3 * cell + 2]};
+    const double r = 0.5 * sqrt(wx * wx + wy * wy + wz * wz) * 1.001;
+    const double R = (sqrt(sqdist(c, p)) + 2.0 * r) * (1.0 + 1e-6);
+    int ref[kCutK];
+    float bd[kCutK];
+    int m = 1;
+    ref[0] = 0;
+    bd[0] = 0.f;
+    if (R < INFINITY) {  // NaN / inf (no answer): the root only
+        const float limf = __double2float_ru(R * R * kSlack);
+        const double o[3] = {ox, oy, oz};
+        const QF qf = make_qf(c, o, tm);
+        for (int pass = 0; pass < 256; ++pass) {
+            bool changed = false;
+            const int m0 = m;
+            for (int k = 0; k < m0 && k < m; ++k) {
+                if (ref[k] < 0) continue;
+                const NodeV nd = load_node(nodes, ref[k]);
+                float d0, d1;
+                node_child_bounds(nd, qf, d0, d1);
+                const bool h0 = d0 <= limf, h1 = d1 <= limf;
+                const int cnt = (int)h0 + (int)h1;
+                if (m - 1 + cnt > kCutK) continue;
+                changed = true;
+                if (cnt == 0) {  // nothing within R below this entry
+                    ref[k] = ref[m - 1];
+                    bd[k] = bd[m - 1];
+                    --m;
+                    continue;
+                }
+                const int c0 = nd.child(0), c1 = nd.child(1);
+                if (h0) {
+                    ref[k] = c0;
+                    bd[k] = d0;
+                    if (h1) {
+                        ref[m] = c1;
+                        bd[m] = d1;
+                        ++m;
+                    }
+                } else {
+                    ref[k] = c1;
+                    bd[k] = d1;
+                }
+            }
+            if (!changed || m == 0) break;
+        }
+        if (m == 0) {  // cannot happen for a consistent tree (c's own closest face is within R): keep the root
+            m = 1;
+            ref[0] = 0;
+            bd[0] = 0.f;
+        }
+    }
+    for (int k = 1; k < m; ++k)  // nearest first
+        for (int j = k; j > 0 && bd[j] < bd[j - 1]; --j) {
+            const int tr = ref[j];
+            ref[j] = ref[j - 1];
+            ref[j - 1] = tr;
+            const float tb = bd[j];
+            bd[j] = bd[j - 1];
+            bd[j - 1] = tb;
+        }
+    uint2* out = cut + cell * kCutK;
+    for (int k = 0; k < kCutK; ++k) {
+        uint2 e = make_uint2(kCutEmpty, 0u);
+        if (k < m) {
+            const double sv = sqrt((double)bd[k]) * (1.0 - 1e-5) - r * (1.0 + 1e-5);
+            e = make_uint2((uint32_t)ref[k], __float_as_uint(sv > 0.0 ? __double2float_rd(sv * sv) : 0.f));
+        }
+        out[k] = e;
+    }
+}
+
+int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s) {
+    const size_t n = (size_t)G * G * G;
+    k_cut_centres<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_q);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+int cut_build(msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, uint2* d_cut, hipStream_t s) {
+    const size_t n = (size_t)G * G * G;
+    k_cut_build<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+        tree->d_nodes, tree->origin[0], tree->origin[1], tree->origin[2], tree_margin(tree->half_diag), G, lo[0], lo[1],
+        lo[2], w[0], w[1], w[2], d_pts, d_cut);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
 }
 
 }  // namespace msh

@@ -170,6 +170,33 @@ def test_c3_sample_both_leaf_paths(oracle, monkeypatch):
     assert np.array_equal(outs[0][2][rows], bpt)
 
 
+def test_entry_cut_bit_exact(oracle, monkeypatch):
+    # C3 mesh: walks from the entry cut (default grid, a coarse 8^3 grid) give the arrays of walks from the
+    # root (MESH_AMD_ENTRY_CUT=0), on uniform queries reaching past the grid (+-1.25 around the unit sphere),
+    # near-surface queries and queries on cell faces of the default grid; 2000 rows match brute force
+    v, f = W.c3_mesh()
+    rng = np.random.default_rng(41)
+    G = int(round(np.cbrt(2 * f.shape[0])))
+    lo, w = -1.25, 2.5 / G  # scene box +-1 (icosphere vertices on the unit sphere), widened by 1/4
+    on_faces = rng.uniform(-1.2, 1.2, (20_000, 3))
+    on_faces[np.arange(20_000), rng.integers(0, 3, 20_000)] = lo + rng.integers(0, G + 1, 20_000) * w
+    surf, _ = W.surface_samples(v, f, 50_000, seed=42, sigma=0.003)
+    q = np.concatenate([rng.uniform(-1.4, 1.4, (150_000, 3)), surf, on_faces])
+    outs = []
+    for cut, g in (("0", None), ("1", None), ("1", "8")):
+        monkeypatch.setenv("MESH_AMD_ENTRY_CUT", cut)
+        if g:
+            monkeypatch.setenv("MESH_AMD_CUT_G", g)
+        outs.append(_nearest(v, f, q))
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert np.array_equal(a, b)
+    rows = rng.choice(q.shape[0], 2000, replace=False)
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[rows])
+    assert np.array_equal(outs[1][0][rows], bf) and np.array_equal(outs[1][1][rows], bp)
+    assert np.array_equal(outs[1][2][rows], bpt)
+
+
 def test_c3_full_size_properties(oracle):
     # BASELINE C3 mesh (1,003,520 faces) with 1M queries: size-independent properties on all queries,
     # tie-tolerant parity against the CGAL-tree restatement on a 3000-query sample.
