@@ -214,7 +214,8 @@ struct WsOrder {
 
 // Entry cut of a single triangle tree (nearest.hip cut_start / k_cut_build): a G^3 grid over the scene box
 // widened by 1/4 on every side (each axis at least 1/20 of the largest, so flat meshes get cells of a sane
-// shape), ~2 cells per leaf up to 2^22 cells (C3: G = 126, 2M cells, 128 MB); the cell centres are answered
+// shape), ~8 cells per leaf up to 2^23 cells (C3: G = 200, 8M cells, 512 MB; G = 64 / 126 / 160: 1718 /
+// 1742-1765 / 1782 M q/s against 1789-1800); the cell centres are answered
 // by the tree itself, then every cell's start entries are cut from the root.  Trees under kCutMinLeaves
 // leaves start at the root (their top levels are few).  MESH_AMD_ENTRY_CUT=0 turns it off (A/B).
 constexpr size_t kCutMinLeaves = 4096;
@@ -222,7 +223,7 @@ static int build_entry_cut(msh_tree* t) {
     const char* env = getenv("MESH_AMD_ENTRY_CUT");
     if ((env && atoi(env) == 0) || t->kind != kTriangles || t->B != 1 || t->T < kCutMinLeaves || !t->d_nodes)
         return MSH_OK;
-    const size_t cells = std::min<size_t>(2 * t->T, (size_t)1 << 22);
+    const size_t cells = std::min<size_t>(8 * t->T, (size_t)1 << 23);
     int G = std::max(16, (int)std::lround(std::cbrt((double)cells)));
     if (const char* eg = getenv("MESH_AMD_CUT_G")) G = std::max(4, std::min(256, atoi(eg)));
     double half[3], H = 0.0, lo[3], w[3];

@@ -179,7 +179,7 @@ int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32
                       hipStream_t s);
 // Entry cut of a single triangle tree: the start entries of every grid cell from the exact closest points
 // of the cell centres (d_pts, G^3 rows, answered by the tree itself), written to tree->d_cut (kCutK per cell)
-constexpr int kCutK = 8;
+constexpr int kCutK = 8;  // 4: 1773-1800 M q/s (49.5-51.2 visits), 16: 1285 (C3, profiles/r03_c3_entry_cut_ab.jsonl)
 int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s);
 int cut_build(msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, uint2* d_cut, hipStream_t s);
 // closest point: o.face, o.part (nullable), o.pt; with o.w (3 per row) the barycentric variant (part unused)

@@ -542,19 +542,18 @@ __device__ inline bool cut_start(const KnnArgs& a, const D3& q, const Pol& pol, 
     if (!(ux >= 0.0 && ux < G && uy >= 0.0 && uy < G && uz >= 0.0 && uz < G)) return true;  // outside: the root
     const size_t cell = ((size_t)(unsigned)uz * (size_t)a.cut_G + (unsigned)uy) * (size_t)a.cut_G + (unsigned)ux;
     const uint4* c = reinterpret_cast<const uint4*>(a.cut + cell * kCutK);
-    const uint4 e0 = c[0], e1 = c[1], e2 = c[2], e3 = c[3];
+    uint4 e[kCutK / 2];
+#pragma unroll
+    for (int j = 0; j < kCutK / 2; ++j) e[j] = c[j];
     auto put = [&](uint32_t ref, uint32_t sb) {
         if (ref == kCutEmpty) return;
         w.push(make_uint2(ref, sb), lds, spill);
     };
-    put(e3.z, e3.w);
-    put(e3.x, e3.y);
-    put(e2.z, e2.w);
-    put(e2.x, e2.y);
-    put(e1.z, e1.w);
-    put(e1.x, e1.y);
-    put(e0.z, e0.w);
-    put(e0.x, e0.y);
+#pragma unroll
+    for (int j = kCutK / 2 - 1; j >= 0; --j) {
+        put(e[j].z, e[j].w);
+        put(e[j].x, e[j].y);
+    }
     return w.pop(pol, lds, spill);
 }
 
