@@ -31,14 +31,28 @@ def short(name):
     return m.group(1) if m else name
 
 
-def counters(pmc_dir):
+def skip_build(rows, skip):
+    """Drop the traversal dispatches of the first `skip` traversals of a run (the tree build answers the entry
+    cut's cell centres with the same kernels before the bench starts): every TRAVERSAL row whose dispatch id is
+    <= that of the skip-th pass-2 dispatch."""
+    if skip <= 0:
+        return rows
+    coop = sorted({int(r["Dispatch_Id"]) for r in rows if short(r.get("Kernel_Name", "")) == TRAVERSAL[1]})
+    if len(coop) < skip:
+        return rows
+    last = coop[skip - 1]
+    return [r for r in rows if not (short(r.get("Kernel_Name", "")) in TRAVERSAL and int(r["Dispatch_Id"]) <= last)]
+
+
+def counters(pmc_dir, skip=0):
     """{kernel: {counter: total over dispatches, '_dispatches': n}} over every *counter_collection.csv
     under pmc_dir (per-dispatch rows of one counter are summed first)."""
     vals = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))  # kernel -> counter -> dispatch -> sum
     vgpr = {}
     for path in glob.glob(os.path.join(pmc_dir, "**", "*counter_collection.csv"), recursive=True):
         with open(path) as fh:
-            for row in csv.DictReader(fh):
+            rows = skip_build(list(csv.DictReader(fh)), skip)
+            for row in rows:
                 k = short(row.get("Kernel_Name", ""))
                 c = row.get("Counter_Name")
                 d = (path, row.get("Dispatch_Id") or row.get("Correlation_Id"))
@@ -55,13 +69,15 @@ def counters(pmc_dir):
     return out
 
 
-def kernel_stats(stats_dir):
-    """{kernel: (calls, total ns)} from the --stats pass."""
+def kernel_stats(stats_dir, skip=0):
+    """{kernel: (calls, total ns)} from the --stats pass's kernel trace (build traversals dropped)."""
     out = {}
-    for path in glob.glob(os.path.join(stats_dir, "**", "*kernel_stats.csv"), recursive=True):
+    for path in glob.glob(os.path.join(stats_dir, "**", "*kernel_trace.csv"), recursive=True):
         with open(path) as fh:
-            for row in csv.DictReader(fh):
-                out[short(row["Name"])] = (int(row["Calls"]), float(row["TotalDurationNs"]))
+            for row in skip_build(list(csv.DictReader(fh)), skip):
+                k = short(row["Kernel_Name"])
+                c, ns = out.get(k, (0, 0.0))
+                out[k] = (c + 1, ns + float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
     return out
 
 
@@ -75,15 +91,17 @@ def main():
                          "the box by profile_pmc.sh)")
     ap.add_argument("--queries", type=float, default=1e8)
     ap.add_argument("--freq", type=int, default=224)
+    ap.add_argument("--build-traversals", type=int, default=1,
+                    help="traversals per run that belong to the tree build (the entry cut's cell centres), dropped")
     args = ap.parse_args()
     S = int(args.queries)
     allc = {}
     for p in sorted(os.listdir(args.pmc)):
         d = os.path.join(args.pmc, p)
         if os.path.isdir(d) and p != "stats":
-            for k, cs in counters(d).items():
+            for k, cs in counters(d, args.build_traversals).items():
                 allc.setdefault(k, {}).update(cs)
-    stats = kernel_stats(os.path.join(args.pmc, "stats"))
+    stats = kernel_stats(os.path.join(args.pmc, "stats"), args.build_traversals)
     T = 20 * args.freq ** 2
     workload = "C3: geodesic icosphere freq %d (%d faces, %d vertices), %d uniform queries in [-1.1,1.1]^3 per GPU" % (
         args.freq, T, 10 * args.freq ** 2 + 2, S)
@@ -127,7 +145,8 @@ def main():
         "wave_cycles_valu_frac": ratio("SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES"),
         "units": "FETCH_SIZE / WRITE_SIZE in KB as rocprofv3 reports them; gfx950: bytes = "
                  "(2 * FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md §HBM); TCC_HIT/MISS summed over "
-                 "channels; every figure per traversal = pass-1 launches (leaders + followers) + pass 2",
+                 "channels; every figure per traversal = pass-1 launches (leaders + followers) + pass 2; the "
+                 "first %d traversal(s) of each run (the tree build's entry-cut centres) excluded" % args.build_traversals,
         "kernels": kern,
         "bytes_per_launch": tot_bytes or None,
         "bytes_per_query": (tot_bytes / S) if tot_bytes else None,
