@@ -166,6 +166,7 @@ static void free_tree(msh_tree* t) {
     if (t->d_vorder) (void)hipFree(t->d_vorder);
     if (t->d_vorder_shard) (void)hipFree(t->d_vorder_shard);
     if (t->d_cut) (void)hipFree(t->d_cut);
+    if (t->d_cut_hint) (void)hipFree(t->d_cut_hint);
     for (int b = 0; b < 2; ++b) {
         if (t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
         if (t->d_stage[b]) (void)hipFree(t->d_stage[b]);
@@ -247,21 +248,29 @@ static int build_entry_cut(msh_tree* t) {
     MSH_TRY(cut_centres(G, lo, w, dq.as<double>(), s));
     MSH_TRY(msh_tree_nearest_device(t, dq.as<double>(), n, df.as<uint32_t>(), nullptr, dp.as<double>(), s));
     uint2* cut = nullptr;
+    int* hint = nullptr;
     hipError_t e = hipMalloc(&cut, n * kCutK * sizeof(uint2));
+    if (e == hipSuccess) e = hipMalloc(&hint, n * sizeof(int));
     if (e != hipSuccess) {
         set_error("hipMalloc entry cut: %s", hipGetErrorString(e));
+        if (cut) (void)hipFree(cut);
         return MSH_ENOMEM;
     }
     int st = cut_build(t, G, lo, w, dp.as<double>(), cut, s);
+    DevBuf dinv;
+    if (st == MSH_OK) st = dinv.reserve(t->T * sizeof(uint32_t));
+    if (st == MSH_OK) st = cut_hints(t, df.as<uint32_t>(), n, dinv.as<uint32_t>(), hint, s);
     if (st == MSH_OK && (e = hipStreamSynchronize(s)) != hipSuccess) {
         set_error("entry cut build: %s", hipGetErrorString(e));
         st = MSH_EDEVICE;
     }
     if (st != MSH_OK) {
         (void)hipFree(cut);
+        (void)hipFree(hint);
         return st;
     }
     t->d_cut = cut;
+    t->d_cut_hint = hint;
     t->cut_G = G;
     for (int k = 0; k < 3; ++k) {
         t->cut_lo[k] = lo[k];
@@ -964,7 +973,9 @@ int msh_ntree_build(const double* v, size_t P, const uint32_t* f, size_t T, doub
     (*out)->kind = kNormals;
     if ((*out)->d_cut) {  // the normals metric starts at the root
         (void)hipFree((*out)->d_cut);
+        (void)hipFree((*out)->d_cut_hint);
         (*out)->d_cut = nullptr;
+        (*out)->d_cut_hint = nullptr;
     }
     (*out)->eps = eps;
     return MSH_OK;

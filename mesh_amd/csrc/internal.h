@@ -121,6 +121,7 @@ struct msh_tree {
     // entry cut (single triangle trees; nearest.hip build_entry_cut): a G^3 grid over the scene box widened by
     // 1/4, kCutK start entries per cell; d_cut == nullptr: every query starts at the root
     uint2* d_cut = nullptr;
+    int* d_cut_hint = nullptr;  // per cell: the leaf of the closest face of its centre (-1: none)
     int cut_G = 0;
     double cut_lo[3] = {0, 0, 0}, cut_iw[3] = {0, 0, 0};
     msh::Workspace ws;
@@ -182,6 +183,8 @@ int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32
 constexpr int kCutK = 8;  // 4: 1773-1800 M q/s (49.5-51.2 visits), 16: 1285 (C3, profiles/r03_c3_entry_cut_ab.jsonl)
 int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s);
 int cut_build(msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, uint2* d_cut, hipStream_t s);
+// d_hint[cell] = the leaf holding face d_face[cell] (d_inv: T scratch words)
+int cut_hints(const msh_tree* tree, const uint32_t* d_face, size_t n, uint32_t* d_inv, int* d_hint, hipStream_t s);
 // closest point: o.face, o.part (nullable), o.pt; with o.w (3 per row) the barycentric variant (part unused)
 int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s);
 // batched trees: n = B*S queries, slot i answered on mesh i / S (the batched sort is mesh-major)

@@ -101,6 +101,7 @@ struct KnnArgs {
     // entry cut (list path; single trees): a query inside the grid starts from its cell's entries instead of
     // the root (build_entry_cut); nullptr: from the root
     const uint2* cut;
+    const int* cut_hint;  // per cell: the leaf of its centre's closest face, the hint of unhinted phases
     int cut_G;
     double cut_lo[3], cut_iw[3];
     size_t nunits;  // work units of this phase (slots it covers)
@@ -533,14 +534,19 @@ constexpr size_t kLeadMinLeaves = 4096;  // smaller trees skip the leader phases
 // on the stack with it, nearest to c popped first, and the walk starts from the first entry within the
 // current limit.  false: no entry survives the hint's bound (the hint is the answer).
 constexpr uint32_t kCutEmpty = 0x7FFFFFFFu;  // not a node id (ids < T - 1 <= 2^31 - 2) nor a ~leaf
-template <class Pol>
-__device__ inline bool cut_start(const KnnArgs& a, const D3& q, const Pol& pol, Walker& w, uint2* __restrict__ lds,
-                                 uint2* __restrict__ spill) {
+constexpr size_t kNoCell = ~(size_t)0;
+// grid cell of q, or kNoCell outside the grid (or without a cut)
+__device__ inline size_t cut_cell(const KnnArgs& a, const D3& q) {
+    if (!a.cut) return kNoCell;
     const double G = (double)a.cut_G;
     const double ux = (q.x - a.cut_lo[0]) * a.cut_iw[0], uy = (q.y - a.cut_lo[1]) * a.cut_iw[1],
                  uz = (q.z - a.cut_lo[2]) * a.cut_iw[2];
-    if (!(ux >= 0.0 && ux < G && uy >= 0.0 && uy < G && uz >= 0.0 && uz < G)) return true;  // outside: the root
-    const size_t cell = ((size_t)(unsigned)uz * (size_t)a.cut_G + (unsigned)uy) * (size_t)a.cut_G + (unsigned)ux;
+    if (!(ux >= 0.0 && ux < G && uy >= 0.0 && uy < G && uz >= 0.0 && uz < G)) return kNoCell;
+    return ((size_t)(unsigned)uz * (size_t)a.cut_G + (unsigned)uy) * (size_t)a.cut_G + (unsigned)ux;
+}
+template <class Pol>
+__device__ inline bool cut_start(const KnnArgs& a, size_t cell, const Pol& pol, Walker& w, uint2* __restrict__ lds,
+                                 uint2* __restrict__ spill) {
     const uint4* c = reinterpret_cast<const uint4*>(a.cut + cell * kCutK);
     uint4 e[kCutK / 2];
 #pragma unroll
@@ -597,8 +603,21 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
         }
         int hint_leaf = -1;  // STATS
+        const size_t cell = kList && fin ? cut_cell(a, q) : kNoCell;
         if constexpr (MODE == 0 || MODE == 3) {
-            if (fin && (a.phase == 2 || a.phase == 1)) {
+            if (kList && a.cut_hint && cell != kNoCell && a.phase != 2) {
+                // slots without a leader (super-leaders, leaders, unled launches) inside the grid: the leaf of
+                // the cell centre's closest face, within d(c) + r of q's own answer
+                const int lf = a.cut_hint[cell];
+                if (STATS) hint_leaf = lf;
+                if (lf >= 0) {
+                    pol.test(lf);
+                    if (STATS) {
+                        ++n_leaves;
+                        ++n_hinted;
+                    }
+                }
+            } else if (fin && (a.phase == 2 || a.phase == 1)) {
                 const int lf = a.phase == 2 ? leader_leaf(a, i, q, kFWin, kLead) : leader_leaf(a, i, q, kLWin * kLead2, kLead2);
                 if (STATS) hint_leaf = lf;
                 if (lf >= 0) {
@@ -624,7 +643,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             const int root = query_root(a, i, q, qf);
             Walker w{root, 0};
             bool start = fin;
-            if (a.cut && fin) start = cut_start(a, q, pol, w, lds, spill);
+            if (cell != kNoCell) start = cut_start(a, cell, pol, w, lds, spill);
             uint32_t* ring = lsh + (tid >> 6) * (kRing + 64 * 4);
             unsigned long long* bd = reinterpret_cast<unsigned long long*>(ring + kRing);  // per owner: d2 bits
             unsigned long long* bfl = bd + 64;                                              // (face << 32 | leaf)
@@ -1375,6 +1394,8 @@ static KnnArgs tree_args(const msh_tree* tree, size_t S) {
 static void cut_args(const msh_tree* tree, KnnArgs& a) {
     if (!tree->d_cut || tree->B != 1) return;
     a.cut = tree->d_cut;
+    const char* e = getenv("MESH_AMD_CUT_HINT");  // 0: unled slots start without a hint (A/B)
+    a.cut_hint = (e && atoi(e) == 0) ? nullptr : tree->d_cut_hint;
     a.cut_G = tree->cut_G;
     for (int k = 0; k < 3; ++k) {
         a.cut_lo[k] = tree->cut_lo[k];
@@ -1534,6 +1555,32 @@ __global__ __launch_bounds__(kBlock) void k_cut_build(const BNode* __restrict__ 
         }
         out[k] = e;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void k_face_leaf(const TriRec* __restrict__ tris, size_t T, uint32_t* __restrict__ inv) {
+    const size_t l = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (l >= T) return;
+    D3 x, y, z;
+    uint32_t face;
+    load_tri(tris, (int)l, x, y, z, face);
+    if (face < T) inv[face] = (uint32_t)l;
+}
+__global__ __launch_bounds__(kBlock) void k_cut_hint(const uint32_t* __restrict__ face, size_t n, size_t T,
+                                                     const uint32_t* __restrict__ inv, int* __restrict__ hint) {
+    const size_t c = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (c >= n) return;
+    const uint32_t f = face[c];
+    hint[c] = f < T ? (int)inv[f] : -1;
+}
+
+int cut_hints(const msh_tree* tree, const uint32_t* d_face, size_t n, uint32_t* d_inv, int* d_hint, hipStream_t s) {
+    const size_t T = tree->T;
+    k_face_leaf<<<(unsigned)((T + kBlock - 1) / kBlock), kBlock, 0, s>>>(static_cast<const TriRec*>(tree->d_leaves), T,
+                                                                          d_inv);
+    MSH_HIP(hipGetLastError());
+    k_cut_hint<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(d_face, n, T, d_inv, d_hint);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
 }
 
 int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s) {

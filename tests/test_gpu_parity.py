@@ -171,8 +171,8 @@ def test_c3_sample_both_leaf_paths(oracle, monkeypatch):
 
 
 def test_entry_cut_bit_exact(oracle, monkeypatch):
-    # C3 mesh: walks from the entry cut (default grid, a coarse 8^3 grid) give the arrays of walks from the
-    # root (MESH_AMD_ENTRY_CUT=0), on uniform queries reaching past the grid (+-1.25 around the unit sphere),
+    # C3 mesh: walks from the entry cut (default grid with and without the cell hints, a coarse 8^3 grid) give
+    # the arrays of walks from the root (MESH_AMD_ENTRY_CUT=0), on uniform queries reaching past the grid (+-1.25 around the unit sphere),
     # near-surface queries and queries on cell faces of the default grid; 2000 rows match brute force
     v, f = W.c3_mesh()
     rng = np.random.default_rng(41)
@@ -183,8 +183,9 @@ def test_entry_cut_bit_exact(oracle, monkeypatch):
     surf, _ = W.surface_samples(v, f, 50_000, seed=42, sigma=0.003)
     q = np.concatenate([rng.uniform(-1.4, 1.4, (150_000, 3)), surf, on_faces])
     outs = []
-    for cut, g in (("0", None), ("1", None), ("1", "8")):
+    for cut, hint, g in (("0", "1", None), ("1", "1", None), ("1", "0", None), ("1", "1", "8")):
         monkeypatch.setenv("MESH_AMD_ENTRY_CUT", cut)
+        monkeypatch.setenv("MESH_AMD_CUT_HINT", hint)  # unled slots hinted by their cell's centre answer
         if g:
             monkeypatch.setenv("MESH_AMD_CUT_G", g)
         outs.append(_nearest(v, f, q))
