@@ -84,11 +84,7 @@ int msh_set_device(int device);
 
 /* ---- spatialsearch (spatialsearchmodule.cpp) ---- */
 /* aabbtree_compute(v, f) -> capsule: spatialsearchmodule.cpp:74-127 (TreeAndTri build :108-123).
- * GPU LBVH build: Morton codes of triangle centroids, LDS radix sort, Karras emission, exact extents, the
- * top-down re-split of subtrees along the surface, oriented child boxes; for trees of >= 4096 faces also the
- * entry cut of the closest-point queries: a grid of ~8 cells per face (at most 2^23 cells) around the mesh,
- * 68 B per cell in HBM (C3, 1M faces: 544 MB), start entries and a hint leaf per cell.  It only changes where
- * a query's walk starts, never its answer.  MESH_AMD_ENTRY_CUT=0 (read at build time) builds without it. */
+ * GPU LBVH build: Morton codes of triangle centroids, LDS radix sort, Karras emission, atomic refit. */
 int msh_tree_build(const double* v, size_t P, const uint32_t* f, size_t T, msh_tree** out);
 /* visibility_compute(v=, f=, extra_v=, extra_f=) builds over main + extra triangles:
  * py_visibility.cpp:114-163.  extra may be NULL/0. */
