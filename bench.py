@@ -1,22 +1,25 @@
 """Benchmark: closest-point queries/sec against a 1M-face mesh on MI355X (BASELINE.json metric).
 
-Workload: class-I geodesic icosphere, frequency 224 = 1,003,520 faces / 501,762
-vertices; every GPU answers its own shard of 100M queries uniform in [-1.1, 1.1]^3 (seed 3 + rank),
-generated directly in HBM.  One step = one pass of the hot path over one batch resident in HBM:
-query Morton codes -> LDS radix sort -> LBVH traversal with fp64 CGAL-construction refinement ->
-results scattered back to query order (face u32, part u32, point 3 x f64), and for N > 1 the all-gather
-of every rank's (face, part, point) slab into the whole answer on every rank (SURVEY §8(d)'s primary
-metric; RCCL over xGMI, each batch's gather overlapped with the next batch's traversal by a
-double-buffered ResultRing, every gather finished inside the timed region).  `value_without_allgather`
-repeats the steps without the exchange.  The BVH build is setup (reported as build_ms); for N > 1 it is
-built on rank 0 and replicated with one RCCL broadcast.
+Workload (BASELINE.json configs[2]): class-I geodesic icosphere, frequency 224 = 1,003,520
+faces / 501,762 vertices; ONE stream of 100M queries uniform in [-1.1, 1.1]^3 (seed 3) per step, sharded
+contiguously over the N GPUs: every rank draws the whole stream in HBM (the same rows on every device) and
+answers its shard_range.  One step = one pass of the hot path over the stream: query Morton codes -> LDS radix
+sort -> LBVH traversal with fp64 CGAL-construction refinement -> results scattered back to query order (face
+u32, part u32, point 3 x f64), and for N > 1 the all-gather of every rank's (face, part, point) slab, so the
+whole 100M-row answer is on every rank (SURVEY §8(d)'s primary metric; RCCL over xGMI, each batch's gather
+overlapped with the next batch's traversal by a double-buffered ResultRing, every gather finished inside the
+timed region).  `value` = 100M x steps / max-over-ranks wall time (strong scaling).  Beside it for N > 1:
+`value_without_allgather` (the same steps without the exchange) and `value_weak_100M_per_gpu` (every rank
+answers the whole 100M stream and the N x 100M answers are all-gathered: the round-3 weak-scaling line).
+The BVH build is setup (reported as build_ms); for N > 1 it is built on rank 0 and replicated with one RCCL
+broadcast.  The entry cut is built by the first (warm-up) query, its time reported as entry_cut_ms.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--queries Q]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Rank 0 prints ONE JSON line.  `roofline` is for the traversal kernel (k_knn): algorithmic bytes per
-launch = S * (56 + 64 * nodes/query + 80 * leaves/query) with the per-query counts
-from the instrumented traversal of the same queries, divided by that kernel's average duration
+Rank 0 prints ONE JSON line.  `roofline` is for the traversal kernel (k_knn) on rank 0's shard: algorithmic
+bytes per launch = S_rank * (56 + 64 * nodes/query + 80 * leaves/query) with the per-query
+counts from the instrumented traversal of the same queries, divided by that kernel's average duration
 measured with HIP events on its launch stream over the timed region.  `cpu_baseline` times the
 oracle's CGAL-faithful restatement (1 thread, the reference's effective serial path) on a bounded
 sample of the same workload.
@@ -41,7 +44,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--queries", type=int, default=100_000_000, help="queries per GPU per step")
+    ap.add_argument("--queries", type=int, default=100_000_000,
+                    help="queries per step: one C3 stream, sharded contiguously over the GPUs")
+    ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling (100M per GPU) line")
     ap.add_argument("--freq", type=int, default=224, help="icosphere frequency (224 -> 1,003,520 faces)")
     ap.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU baseline time budget (both modes)")
     ap.add_argument("--no-cpu", action="store_true")
@@ -65,7 +70,9 @@ def cpu_baseline(v, f, budget_s):
       * 1 thread (the reference's aabbtree_nearest loop is serial: its omp pragma is compiled out,
         spatialsearchmodule.cpp:212-214) -> the reported `cpu_baseline`;
       * all host threads this process may use (OpenMP over queries) -> `cpu_baseline_allcores`.
-    The chunk size is chosen so the 13 chunks of a mode take about budget_s / 2 seconds."""
+    The chunk size is chosen so the 13 chunks of the 1-thread mode take about 2/3 of budget_s and those of the
+    all-threads mode the rest: the reported (1-thread) chunks hold ~3k queries each, so the few costly queries
+    near the sphere's centre (equidistant from much of the mesh) weigh alike in every chunk."""
     from oracle import oracle as O
     t0 = time.perf_counter()
     tree = O.CgalTree(v, f, hint=True)
@@ -73,13 +80,13 @@ def cpu_baseline(v, f, budget_s):
     rng = np.random.default_rng(3)
     pool = rng.uniform(-1.1, 1.1, (4_000_000, 3))
     out = {}
-    for mode, threads in (("1", 1), ("all", host_threads())):
+    for mode, threads, share in (("1", 1, 2.0 / 3.0), ("all", host_threads(), 1.0 / 3.0)):
         # calibrate: how many queries per second at this thread count
-        n = 2000 * threads
+        n = 4000 * threads
         t0 = time.perf_counter()
         tree.nearest(pool[:n], threads=threads)
         rate0 = n / max(time.perf_counter() - t0, 1e-6)
-        chunk = int(min(max(rate0 * budget_s / 2 / 13, 500), pool.shape[0] // 13))
+        chunk = int(min(max(rate0 * budget_s * share / 13, 500), pool.shape[0] // 13))
         rates, off = [], 0
         for k in range(13):
             q = pool[off:off + chunk]
@@ -137,14 +144,14 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from mesh_amd import _native, spatialsearch
-    from mesh_amd.distributed import nearest_device, replicate_tree
+    from mesh_amd.distributed import ResultRing, nearest_device, replicate_tree
     import workloads as W
 
     _native.set_device(local)
     v, f = W.geodesic_icosphere(args.freq)
     T = int(f.shape[0])
-    workload = "C3: geodesic icosphere freq %d (%d faces, %d vertices), %d uniform queries in [-1.1,1.1]^3 per GPU" % (
-        args.freq, T, v.shape[0], args.queries)
+    S = args.queries
+    workload = W.c3_workload_name(args.freq, S)
 
     # ---- setup: BVH build (rank 0) + RCCL replication ----
     tree = None
@@ -159,32 +166,32 @@ def main():
         tree = replicate_tree(tree, src=0)
         bcast_ms = (time.perf_counter() - t0) * 1e3
 
-    # ---- inputs resident in HBM ----
-    S = args.queries
-    g = torch.Generator(device=dev)
-    g.manual_seed(3 + rank)
-    q = (torch.rand((S, 3), generator=g, dtype=torch.float64, device=dev) * 2.2 - 1.1).contiguous()
+    # ---- inputs resident in HBM: the whole stream on every rank, this rank's contiguous shard ----
+    q_all = W.c3_stream(S, dev)
+    q, (a0, b0) = W.c3_shard(q_all, rank, world)
+    S_loc = b0 - a0
+    rows = -(-S // world)  # slab rows: the largest shard (equal shards for the all-gather)
     stream = torch.cuda.current_stream(dev).cuda_stream
-    slabs = [(torch.empty(S, dtype=torch.int32, device=dev), torch.empty(S, dtype=torch.int32, device=dev),
-              torch.empty((S, 3), dtype=torch.float64, device=dev)) for _ in range(2 if world > 1 else 1)]
+
+    def slab(n):
+        return (torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
+                torch.empty((n, 3), dtype=torch.float64, device=dev))
+
+    slabs = [slab(rows) for _ in range(2 if world > 1 else 1)]
     ring = None
     if world > 1:
-        from mesh_amd.distributed import ResultRing
-        gathered = (torch.empty(world * S, dtype=torch.int32, device=dev),
-                    torch.empty(world * S, dtype=torch.int32, device=dev),
-                    torch.empty((world * S, 3), dtype=torch.float64, device=dev))
-        ring = ResultRing(slabs, gathered)
+        ring = ResultRing(slabs, [slab(world * rows) for _ in range(2)])
 
-    def answer(slab):
-        nearest_device(tree, q, slab[0], slab[1], slab[2], stream=stream)
+    def answer(sl):
+        nearest_device(tree, q, sl[0][:S_loc], sl[1][:S_loc], sl[2][:S_loc], stream=stream)
 
-    def step():  # one batch: the query pipeline, and for N > 1 the all-gather of its results
+    def step():  # one batch: the query pipeline on this rank's shard, and for N > 1 the all-gather of the answer
         if ring is None:
             answer(slabs[0])
         else:
             ring.step(answer)
 
-    def timed(run, steps):
+    def timed(run, steps, rg=None):
         """barrier + sync, `steps` calls of run (every gather drained), sync + barrier; max over ranks"""
         if world > 1:
             dist.barrier()
@@ -192,8 +199,8 @@ def main():
         t0 = time.perf_counter()
         for _ in range(steps):
             run()
-        if ring is not None:
-            ring.drain()
+        if rg is not None:
+            rg.drain()
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
@@ -204,16 +211,17 @@ def main():
             el = float(t.item())
         return el
 
-    for _ in range(args.warmup):
+    for _ in range(args.warmup):  # the first query also builds the tree's entry cut (lazily, once)
         step()
     if ring is not None:
         ring.drain()
     torch.cuda.synchronize()
+    cut = tree.entry_cut_info()
 
     # ---- timed region: K steps (N > 1: each with its result all-gather) ----
     _native.timing_reset()
     _native.timing_enable(True)
-    elapsed = timed(step, args.steps)
+    elapsed = timed(step, args.steps, ring)
     _native.timing_enable(False)
     k_ms, k_n = _native.timing_get("nearest")
     p1_ms, p1_n = _native.timing_get("knn_pass1")
@@ -226,15 +234,33 @@ def main():
     g_ms, g_n = _native.timing_get("gather")
     u_ms, u_n = _native.timing_get("unpermute")
 
-    # ---- N > 1: the same steps without the exchange (reported beside value, never as value) ----
-    elapsed_no_ag = timed(lambda: answer(slabs[0]), args.steps) if world > 1 else None
+    # ---- N > 1, reported beside value (never as value): the same steps without the exchange, and the
+    # weak-scaling line (every rank answers the whole stream; the world x S answers are all-gathered) ----
+    elapsed_no_ag = elapsed_weak = None
+    if world > 1:
+        elapsed_no_ag = timed(lambda: answer(slabs[0]), args.steps)
+        if not args.no_weak:
+            del ring, slabs
+            torch.cuda.empty_cache()
+            wslabs = [slab(S) for _ in range(2)]
+            wg = slab(world * S)  # one gathered buffer written by both batches in turn: only the timing matters
+            wring = ResultRing(wslabs, [wg, wg])
 
-    # ---- instrumented traversal (untimed): algorithmic bytes ----
+            def weak_step():
+                wring.step(lambda sl: nearest_device(tree, q_all, sl[0], sl[1], sl[2], stream=stream))
+
+            weak_step()
+            wring.drain()
+            elapsed_weak = timed(weak_step, args.steps, wring)
+            del wring, wslabs, wg
+            torch.cuda.empty_cache()
+
+    # ---- instrumented traversal (untimed): algorithmic bytes of this rank's shard ----
     nodes, leaves = _native.ctypes.c_uint64(0), _native.ctypes.c_uint64(0)
-    _native.check(_native.lib().msh_tree_nearest_stats(tree.ptr, q.data_ptr(), S, _native.ctypes.byref(nodes),
+    _native.check(_native.lib().msh_tree_nearest_stats(tree.ptr, q.data_ptr(), S_loc, _native.ctypes.byref(nodes),
                                                         _native.ctypes.byref(leaves)))
-    n_node = nodes.value / S
-    n_leaf = leaves.value / S
+    n_node = nodes.value / S_loc
+    n_leaf = leaves.value / S_loc
     info = tree.info()
     node_b, leaf_b = int(info.node_bytes), int(info.leaf_bytes)
     # bytes the traversal requests per query with this layout (node_b-B nodes, leaf_b-B leaves), and the
@@ -248,12 +274,12 @@ def main():
             dist.destroy_process_group()
         return
     avg_kernel_s = (k_ms / max(k_n, 1)) / 1e3
-    achieved = S * bytes_per_query / avg_kernel_s / 1e9
-    achieved_s8d = S * bytes_per_query_s8d / avg_kernel_s / 1e9
+    achieved = S_loc * bytes_per_query / avg_kernel_s / 1e9
+    achieved_s8d = S_loc * bytes_per_query_s8d / avg_kernel_s / 1e9
     build_id = _native.build_id()
-    tr, tr_reason = load_traffic(workload, S, build_id)
+    tr, tr_reason = load_traffic(workload, S, build_id) if world == 1 else (None, "PMC profiles are of the N = 1 run")
     traffic = tr.get("bytes_per_launch") if tr else None
-    total_q = S * world * args.steps
+    total_q = S * args.steps
     out = {
         "metric": METRIC,
         "value": total_q / elapsed,
@@ -263,29 +289,31 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (seeded icosphere mesh + uniform queries generated in HBM)",
-        "config": {"workload": workload, "faces": T, "queries_per_gpu": S,
-                   "parallelism": "dp%d (queries sharded per GPU, BVH replicated by RCCL broadcast)" % world},
+        "data": "synthetic (seeded icosphere mesh + uniform query stream generated in HBM)",
+        "config": {"workload": workload, "faces": T, "queries_total": S, "queries_per_gpu": S_loc,
+                   "parallelism": "dp%d (one query stream sharded contiguously per GPU, BVH replicated by RCCL "
+                                  "broadcast, answers all-gathered)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "k_knn<0,false,true> + k_knn_coop<0,false> (pass 1 + pass 2: traversal + fp64 refinement)",
-                     "kernel_ms": avg_kernel_s * 1e3, "bytes_per_query": bytes_per_query,
+                     "kernel_ms": avg_kernel_s * 1e3, "queries_per_launch": S_loc, "bytes_per_query": bytes_per_query,
                      "node_bytes": node_b, "leaf_bytes": leaf_b,
                      "nodes_per_query": n_node, "leaves_per_query": n_leaf,
                      "s8d_64B_nodes": {"bytes_per_query": bytes_per_query_s8d, "achieved": achieved_s8d,
                                        "frac": achieved_s8d / HBM_PEAK_GBS},
                      "measured": ({"hbm_GBps": tr["bytes_per_launch"] / avg_kernel_s / 1e9,
                                    "l2_hit_rate": tr.get("l2_hit_rate"), "code": tr.get("code"),
-                                   "build_id": tr.get("build_id"), "pmc_traversal_ms": tr.get("traversal_ms")}
+                                   "build_id": tr.get("build_id"), "pmc_traversal_ms": tr.get("traversal_ms"),
+                                   "isa": tr.get("isa")}
                                   if tr else None),
                      "traffic_note": tr_reason,
                      # latency side: what bounds the kernel (node steps issued per second, live; lane
                      # occupancy and memory waits from the same build's SQ counters)
-                     "latency": {"node_steps_per_s": S * n_node / avg_kernel_s,
-                                 "leaf_tests_per_s": S * n_leaf / avg_kernel_s,
+                     "latency": {"node_steps_per_s": S_loc * n_node / avg_kernel_s,
+                                 "leaf_tests_per_s": S_loc * n_leaf / avg_kernel_s,
                                  "lanes_active_valu": tr.get("lanes_active_valu") if tr else None,
                                  "wave_cycles_waiting_frac": tr.get("wave_cycles_waiting_frac") if tr else None,
                                  "wave_cycles_valu_frac": tr.get("wave_cycles_valu_frac") if tr else None}},
@@ -296,13 +324,18 @@ def main():
                                   "morton": m_ms / max(m_n, 1), "gather": g_ms / max(g_n, 1),
                                   "unpermute": u_ms / max(u_n, 1)},
         "build_ms": build_ms,
+        "entry_cut_ms": cut["build_ms"],
+        "entry_cut": {"state": cut["state"], "G": cut["G"], "bytes": cut["bytes"]},
         "build_id": build_id,
         "bvh_broadcast_ms": bcast_ms,
     }
     if elapsed_no_ag is not None:
         out["value_without_allgather"] = total_q / elapsed_no_ag
         out["ms_per_step_without_allgather"] = elapsed_no_ag / args.steps * 1e3
-        out["allgather_bytes_per_step"] = world * S * 32  # (face u32, part u32, point 3 x f64) of every rank
+        out["allgather_bytes_per_step"] = world * rows * 32  # (face u32, part u32, point 3 x f64) of every shard
+    if elapsed_weak is not None:
+        out["value_weak_100M_per_gpu"] = world * S * args.steps / elapsed_weak
+        out["ms_per_step_weak"] = elapsed_weak / args.steps * 1e3
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"], out["cpu_baseline_allcores"] = cpu_baseline(v, f, args.cpu_seconds)
     print(json.dumps(out), flush=True)

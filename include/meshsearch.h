@@ -112,6 +112,30 @@ int msh_tree_nearest_bary(msh_tree* tree, const double* q, size_t S, uint32_t* f
 int msh_tree_nearest_bary_device(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_face, double* d_pt,
                                  double* d_w, void* stream);
 
+/* The order in which the closest-point path visits the S query rows (d_perm[slot] = row): stable by the top
+ * 24 bits of their 30-bit Morton codes in the tree's scene box widened by 10 %.  sorter 0 = the path's own
+ * sort (one-sweep, decoupled look-back, for calls of < 2^30 rows), 1 = the 3-launch-per-pass radix sort it
+ * replaced (and that larger calls use); both give the same permutation.  Asynchronous on `stream`. */
+int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_perm, int sorter, void* stream);
+
+/* Entry cut of a triangle tree (no reference counterpart: derived acceleration data).  A grid
+ * of G^3 cells over the scene box widened by 1/4, 68 B per cell (8 start entries + a hint leaf), from which
+ * closest-point queries start their walks instead of the root; it changes where a walk starts, never an
+ * answer.  It is built lazily, on the first closest-point query of the handle (msh_tree_nearest*,
+ * msh_tree_nearest_bary*, msh_tree_nearest_stats), so trees used only for rays, visibility or the normals
+ * metric never hold it.  Trees of < 4096 faces never get one.
+ *   G < 0: automatic grid (about 8 cells per face, at most 2^23 cells: C3 G = 200, 544 MB) — the default;
+ *   G = 0: no cut (frees one already built); queries start at the root;
+ *   G > 0: G^3 cells.
+ * Changing G frees the current cut; the next closest-point query builds the new one.  A cut that cannot be
+ * built (device memory) is not an error: the handle records the failure (state 3) and queries start at the
+ * root. */
+int msh_tree_set_entry_cut(msh_tree* tree, int G);
+/* state: 0 not built yet, 1 built, 2 off (G = 0, or a tree it does not apply to), 3 build failed;
+ * G: cells per axis of the built cut (0 if none); bytes: device bytes it holds; build_ms: GPU time of its
+ * build (cell-centre queries + cut + hints).  Any output pointer may be NULL. */
+int msh_tree_entry_cut_info(const msh_tree* tree, int* state, int* G, uint64_t* bytes, double* build_ms);
+
 /* aabbtree_nearest_alongnormal(tree, p, n) -> (dist (S,) f64, face (S,) u32, point (S,3) f64):
  * spatialsearchmodule.cpp:222-323.  Nearest hit of the rays (p, n) and (p, -n); hit point = CGAL's
  * Plane_3 / Line_3 construction.  No hit: dist = 1e100 (as the reference), face = MSH_NO_FACE,

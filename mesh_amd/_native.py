@@ -42,6 +42,9 @@ SIGNATURES = [
     ("msh_tree_nearest_stats", _i, [_vp, _vp, _sz, _c_u64_p, _c_u64_p]),
     ("msh_tree_nearest_bary", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_double_p, _c_double_p]),
     ("msh_tree_nearest_bary_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    ("msh_tree_set_entry_cut", _i, [_vp, _i]),
+    ("msh_tree_query_order", _i, [_vp, _vp, _sz, _vp, _i, _vp]),
+    ("msh_tree_entry_cut_info", _i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), _c_u64_p, ctypes.POINTER(ctypes.c_double)]),
     ("msh_tree_nearest_alongnormal", _i, [_vp, _c_double_p, _c_double_p, _sz, _c_double_p, _c_u32_p, _c_double_p]),
     ("msh_tree_nearest_alongnormal_device", _i, [_vp, _vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     ("msh_tree_nearest_alongnormal_stats", _i, [_vp, _vp, _vp, _sz, _c_u64_p, _c_u64_p]),
@@ -221,6 +224,21 @@ class Handle(object):
         inf = TreeInfo()
         check(lib().msh_tree_get_info(self.ptr, ctypes.byref(inf)))
         return inf
+
+    def set_entry_cut(self, G=-1):
+        """msh_tree_set_entry_cut: G < 0 automatic grid (default), 0 none, > 0 G^3 cells; built lazily by the
+        next closest-point query."""
+        check(lib().msh_tree_set_entry_cut(self.ptr, int(G)))
+
+    CUT_STATES = {0: "pending", 1: "built", 2: "off", 3: "failed"}
+
+    def entry_cut_info(self):
+        """msh_tree_entry_cut_info -> dict(state, G, bytes, build_ms)"""
+        st, g, nb, ms = _i(0), _i(0), ctypes.c_uint64(0), ctypes.c_double(0)
+        check(lib().msh_tree_entry_cut_info(self.ptr, ctypes.byref(st), ctypes.byref(g), ctypes.byref(nb),
+                                            ctypes.byref(ms)))
+        return {"state": self.CUT_STATES.get(st.value, st.value), "G": g.value, "bytes": nb.value,
+                "build_ms": ms.value}
 
     def free(self):
         if self.ptr:

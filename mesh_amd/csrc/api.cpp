@@ -215,24 +215,44 @@ struct WsOrder {
 
 // Entry cut of a single triangle tree (nearest.hip cut_start / k_cut_build): a G^3 grid over the scene box
 // widened by 1/4 on every side (each axis at least 1/20 of the largest, so flat meshes get cells of a sane
-// shape), ~8 cells per leaf up to 2^23 cells (C3: G = 200, 8M cells, 512 MB; G = 64 / 126 / 160: 1718 /
+// shape), ~8 cells per leaf up to 2^23 cells (C3: G = 200, 8M cells, 544 MB; G = 64 / 126 / 160: 1718 /
 // 1742-1765 / 1782 M q/s against 1789-1800); the cell centres are answered
 // by the tree itself, then every cell's start entries are cut from the root.  Trees under kCutMinLeaves
-// leaves start at the root (their top levels are few).  MESH_AMD_ENTRY_CUT=0 turns it off (A/B).
+// leaves start at the root (their top levels are few).  Built lazily by the first closest-point query
+// (ensure_entry_cut), so ray-only, visibility and normals-metric trees never pay its memory or build time;
+// msh_tree_set_entry_cut chooses the grid or turns it off.
 constexpr size_t kCutMinLeaves = 4096;
+enum { kCutPending = 0, kCutBuilt = 1, kCutOff = 2, kCutFailed = 3 };
+
+static bool cut_applies(const msh_tree* t) {
+    return t->kind == kTriangles && t->B == 1 && !t->d_boxes && t->T >= kCutMinLeaves && t->d_nodes && t->cut_req != 0;
+}
+
+static void free_entry_cut(msh_tree* t) {
+    if (t->d_cut || t->d_cut_hint) {
+        (void)hipSetDevice(t->device);
+        if (t->ws_done) (void)hipEventSynchronize(t->ws_done);  // no launch may still read the cut
+        if (t->d_cut) (void)hipFree(t->d_cut);
+        if (t->d_cut_hint) (void)hipFree(t->d_cut_hint);
+    }
+    t->d_cut = nullptr;
+    t->d_cut_hint = nullptr;
+    t->cut_G = 0;
+    t->cut_ms = 0.0;
+}
+
 static int build_entry_cut(msh_tree* t) {
-    const char* env = getenv("MESH_AMD_ENTRY_CUT");
-    if ((env && atoi(env) == 0) || t->kind != kTriangles || t->B != 1 || t->T < kCutMinLeaves || !t->d_nodes)
-        return MSH_OK;
     const size_t cells = std::min<size_t>(8 * t->T, (size_t)1 << 23);
-    int G = std::max(16, (int)std::lround(std::cbrt((double)cells)));
-    if (const char* eg = getenv("MESH_AMD_CUT_G")) G = std::max(4, std::min(256, atoi(eg)));
+    const int G = t->cut_req > 0 ? t->cut_req : std::max(16, (int)std::lround(std::cbrt((double)cells)));
     double half[3], H = 0.0, lo[3], w[3];
     for (int k = 0; k < 3; ++k) {
         half[k] = 0.5 * ((double)t->scene_hi[k] - (double)t->scene_lo[k]);
         H = std::max(H, half[k]);
     }
-    if (!(H > 0.0) || !std::isfinite(H)) return MSH_OK;
+    if (!(H > 0.0) || !std::isfinite(H)) {
+        set_error("entry cut: degenerate scene box");
+        return MSH_EINVAL;
+    }
     for (int k = 0; k < 3; ++k) {
         const double m = 0.5 * ((double)t->scene_hi[k] + (double)t->scene_lo[k]);
         const double e = 1.25 * std::max(half[k], 0.05 * H);
@@ -240,43 +260,89 @@ static int build_entry_cut(msh_tree* t) {
         w[k] = 2.0 * e / G;
     }
     const size_t n = (size_t)G * G * G;
-    hipStream_t s = t->stream;
-    DevBuf dq, df, dp;
-    MSH_TRY(dq.reserve(n * 3 * sizeof(double)));
-    MSH_TRY(df.reserve(n * sizeof(uint32_t)));
-    MSH_TRY(dp.reserve(n * 3 * sizeof(double)));
-    MSH_TRY(cut_centres(G, lo, w, dq.as<double>(), s));
-    MSH_TRY(msh_tree_nearest_device(t, dq.as<double>(), n, df.as<uint32_t>(), nullptr, dp.as<double>(), s));
-    uint2* cut = nullptr;
-    int* hint = nullptr;
-    hipError_t e = hipMalloc(&cut, n * kCutK * sizeof(uint2));
-    if (e == hipSuccess) e = hipMalloc(&hint, n * sizeof(int));
-    if (e != hipSuccess) {
-        set_error("hipMalloc entry cut: %s", hipGetErrorString(e));
-        if (cut) (void)hipFree(cut);
+    if (n > 0xFFFFFFFFull) {
+        set_error("entry cut: %d^3 cells exceed one query call", G);
         return MSH_ENOMEM;
     }
-    int st = cut_build(t, G, lo, w, dp.as<double>(), cut, s);
-    DevBuf dinv;
-    if (st == MSH_OK) st = dinv.reserve(t->T * sizeof(uint32_t));
-    if (st == MSH_OK) st = cut_hints(t, df.as<uint32_t>(), n, dinv.as<uint32_t>(), hint, s);
-    if (st == MSH_OK && (e = hipStreamSynchronize(s)) != hipSuccess) {
-        set_error("entry cut build: %s", hipGetErrorString(e));
-        st = MSH_EDEVICE;
+    hipStream_t s = t->stream;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    MSH_HIP(hipEventCreate(&e0));
+    hipError_t e = hipEventCreate(&e1);
+    if (e != hipSuccess) {
+        (void)hipEventDestroy(e0);
+        MSH_HIP(e);
     }
-    if (st != MSH_OK) {
-        (void)hipFree(cut);
-        (void)hipFree(hint);
-        return st;
+    (void)hipEventRecord(e0, s);
+    uint2* cut = nullptr;
+    int* hint = nullptr;
+    int st = MSH_OK;
+    {
+        DevBuf dq, df, dp, dinv;
+        do {
+            if ((st = dq.reserve(n * 3 * sizeof(double))) != MSH_OK) break;
+            if ((st = df.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
+            if ((st = dp.reserve(n * 3 * sizeof(double))) != MSH_OK) break;
+            if ((st = cut_centres(G, lo, w, dq.as<double>(), s)) != MSH_OK) break;
+            // the centres' own walks start at the root (no cut is installed while it is built)
+            if ((st = msh_tree_nearest_device(t, dq.as<double>(), n, df.as<uint32_t>(), nullptr, dp.as<double>(), s)) != MSH_OK)
+                break;
+            e = hipMalloc(&cut, n * kCutK * sizeof(uint2));
+            if (e == hipSuccess) e = hipMalloc(&hint, n * sizeof(int));
+            if (e != hipSuccess) {
+                set_error("hipMalloc entry cut (%zu cells): %s", n, hipGetErrorString(e));
+                st = MSH_ENOMEM;
+                break;
+            }
+            if ((st = cut_build(t, G, lo, w, dp.as<double>(), cut, s)) != MSH_OK) break;
+            if ((st = dinv.reserve(t->T * sizeof(uint32_t))) != MSH_OK) break;
+            if ((st = cut_hints(t, df.as<uint32_t>(), n, dinv.as<uint32_t>(), hint, s)) != MSH_OK) break;
+            (void)hipEventRecord(e1, s);
+            if ((e = hipStreamSynchronize(s)) != hipSuccess) {
+                set_error("entry cut build: %s", hipGetErrorString(e));
+                st = MSH_EDEVICE;
+            }
+        } while (0);
+        (void)hipStreamSynchronize(s);  // the temporaries die with this scope
     }
-    t->d_cut = cut;
-    t->d_cut_hint = hint;
-    t->cut_G = G;
-    for (int k = 0; k < 3; ++k) {
-        t->cut_lo[k] = lo[k];
-        t->cut_iw[k] = 1.0 / w[k];
+    if (st == MSH_OK) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        t->cut_ms = ms;
+        t->d_cut = cut;
+        t->d_cut_hint = hint;
+        t->cut_G = G;
+        for (int k = 0; k < 3; ++k) {
+            t->cut_lo[k] = lo[k];
+            t->cut_iw[k] = 1.0 / w[k];
+        }
+    } else {
+        if (cut) (void)hipFree(cut);
+        if (hint) (void)hipFree(hint);
     }
-    return MSH_OK;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return st;
+}
+
+// First closest-point query of a handle: build its entry cut.  The cut is an optimisation, so a failure (device
+// memory, most likely: 544 MB plus ~420 MB of temporaries on C3) is not the query's: the partial buffers are
+// freed, the error is cleared, the handle remembers the failure and its queries start at the root.
+static void ensure_entry_cut(msh_tree* t) {
+    if (t->cut_state != kCutPending) return;
+    if (!cut_applies(t)) {
+        t->cut_state = kCutOff;
+        return;
+    }
+    t->cut_state = kCutOff;  // while it is built: the cell-centre queries start at the root
+    const std::string keep = g_err;
+    const int st = build_entry_cut(t);
+    if (st == MSH_OK) {
+        t->cut_state = kCutBuilt;
+    } else {
+        (void)hipGetLastError();  // clear a sticky launch / allocation error of the failed build
+        t->cut_state = kCutFailed;
+    }
+    g_err = keep;
 }
 
 // Triangle tree over v (P rows) and f (T rows, indices into v).
@@ -312,7 +378,6 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
                                   static_cast<TriRec*>(t->d_leaves), s)) != MSH_OK)
             break;
         if ((st = build_obb(t, true)) != MSH_OK) break;
-        if ((st = build_entry_cut(t)) != MSH_OK) break;
         (void)hipEventRecord(e1, s);
         e = hipStreamSynchronize(s);
         if (e != hipSuccess) { set_error("LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
@@ -339,6 +404,8 @@ static const size_t kSortMin = 4096;  // below this the query Morton sort costs 
 // C3's 100M queries put ~6 in a cell, and the traversal runs the same node counts as with the full code
 // (sort 3.44 -> 3.08 ms, traversal unchanged).  The order within a cell is the caller's (stable sort).
 constexpr int kQuerySortLo = 6;
+// calls of up to 2^30 - 1 queries take the one-sweep sort (query_sort); larger ones the 3-launch-per-pass radix sort
+constexpr size_t kOneSweepMax = ((size_t)1 << 30) - 1;
 static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_t S, hipStream_t s,
                         QueryOrder* ord, bool allow_lazy = false) {
     *ord = QueryOrder{d_q, d_n, nullptr, nullptr};
@@ -349,10 +416,15 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
     MSH_TRY(ws.keys_alt.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.vals_alt.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.inv.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
     bool in_alt = false;
-    MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
-                             ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
+    if (S <= kOneSweepMax) {
+        MSH_TRY(query_order(t, d_q, S, kQuerySortLo, ws.keys.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
+                            ws.vals.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), ws, s, &in_alt));
+    } else {
+        MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
+        MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
+                                 ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
+    }
     if (in_alt) {  // odd pass count: the sorted pairs are in the alt buffers; swap roles instead of copying
         std::swap(ws.keys, ws.keys_alt);
         std::swap(ws.vals, ws.vals_alt);
@@ -884,9 +956,11 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
             if (e != hipSuccess) { fail(e, "download"); break; }
         }
     } while (0);
-    (void)hipStreamSynchronize(up);
-    (void)hipStreamSynchronize(down);
-    (void)hipStreamSynchronize(sc);
+    // every chunk's kernels and copies end here: in direct_out mode no earlier wait saw their status (the loop
+    // only waits for uploads), so an asynchronous kernel or copy failure surfaces through these syncs
+    const hipError_t e1 = hipStreamSynchronize(up), e2 = hipStreamSynchronize(down), e3 = hipStreamSynchronize(sc);
+    const hipError_t ef = e1 != hipSuccess ? e1 : (e2 != hipSuccess ? e2 : e3);
+    if (st == MSH_OK && ef != hipSuccess) fail(ef, "host call (kernels / download)");
     return st;
 }
 
@@ -970,13 +1044,7 @@ int msh_tree_build(const double* v, size_t P, const uint32_t* f, size_t T, msh_t
 
 int msh_ntree_build(const double* v, size_t P, const uint32_t* f, size_t T, double eps, msh_tree** out) {
     MSH_TRY(msh_tree_build_ex(v, P, f, T, nullptr, 0, nullptr, 0, out));
-    (*out)->kind = kNormals;
-    if ((*out)->d_cut) {  // the normals metric starts at the root
-        (void)hipFree((*out)->d_cut);
-        (void)hipFree((*out)->d_cut_hint);
-        (*out)->d_cut = nullptr;
-        (*out)->d_cut_hint = nullptr;
-    }
+    (*out)->kind = kNormals;  // the normals metric starts at the root: no entry cut is ever built
     (*out)->eps = eps;
     return MSH_OK;
 }
@@ -1031,6 +1099,53 @@ int msh_points_build(const double* v, size_t P, msh_tree** out) {
 
 void msh_tree_free(msh_tree* tree) { free_tree(tree); }
 
+int msh_tree_query_order(msh_tree* t, const double* d_q, size_t S, uint32_t* d_perm, int sorter, void* stream) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_tree_query_order"));
+    MSH_TRY(check_count(S, "msh_tree_query_order"));
+    if (sorter != 0 && sorter != 1) { set_error("msh_tree_query_order: sorter %d (0 or 1)", sorter); return MSH_EINVAL; }
+    if (S == 0) return MSH_OK;
+    if (!d_q || !d_perm) { set_error("msh_tree_query_order: null argument"); return MSH_EINVAL; }
+    hipStream_t s = pick(t, stream);
+    WsOrder order(t, s);
+    Workspace& ws = t->ws;
+    MSH_TRY(ws.keys.reserve(S * sizeof(uint32_t)));
+    MSH_TRY(ws.vals.reserve(S * sizeof(uint32_t)));
+    MSH_TRY(ws.keys_alt.reserve(S * sizeof(uint32_t)));
+    MSH_TRY(ws.vals_alt.reserve(S * sizeof(uint32_t)));
+    bool in_alt = false;
+    if (sorter == 0 && S <= kOneSweepMax) {
+        MSH_TRY(query_order(t, d_q, S, kQuerySortLo, ws.keys.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
+                            ws.vals.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), ws, s, &in_alt));
+    } else {
+        MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
+        MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
+                                 ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
+    }
+    MSH_HIP(hipMemcpyAsync(d_perm, in_alt ? ws.vals_alt.ptr : ws.vals.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    return MSH_OK;
+}
+
+int msh_tree_set_entry_cut(msh_tree* t, int G) {
+    if (!t) { set_error("msh_tree_set_entry_cut: null tree handle"); return MSH_EINVAL; }
+    if (G > 4096) { set_error("msh_tree_set_entry_cut: G = %d cells per axis (at most 4096)", G); return MSH_EINVAL; }
+    const int want = G < 0 ? -1 : G;
+    if (want == t->cut_req && t->cut_state != kCutFailed) return MSH_OK;
+    free_entry_cut(t);
+    t->cut_req = want;
+    t->cut_state = kCutPending;
+    return MSH_OK;
+}
+
+int msh_tree_entry_cut_info(const msh_tree* t, int* state, int* G, uint64_t* bytes, double* build_ms) {
+    if (!t) { set_error("msh_tree_entry_cut_info: null tree handle"); return MSH_EINVAL; }
+    const uint64_t n = t->d_cut ? (uint64_t)t->cut_G * t->cut_G * t->cut_G : 0;
+    if (state) *state = t->cut_state == kCutPending && !cut_applies(t) ? kCutOff : t->cut_state;
+    if (G) *G = t->d_cut ? t->cut_G : 0;
+    if (bytes) *bytes = n * (kCutK * sizeof(uint2) + sizeof(int));
+    if (build_ms) *build_ms = t->cut_ms;
+    return MSH_OK;
+}
+
 int msh_tree_get_info(const msh_tree* t, msh_tree_info* info) {
     if (!t || !info) { set_error("null argument"); return MSH_EINVAL; }
     info->device = t->device;
@@ -1059,6 +1174,7 @@ int msh_tree_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* 
                             void* stream) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_device"));
     MSH_TRY(check_count(S, "msh_tree_nearest_device"));
+    ensure_entry_cut(t);
     if (S == 0) return MSH_OK;
     hipStream_t s = pick(t, stream);
     WsOrder order(t, s);
@@ -1071,6 +1187,7 @@ int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint3
                                  void* stream) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_bary_device"));
     MSH_TRY(check_count(S, "msh_tree_nearest_bary_device"));
+    ensure_entry_cut(t);
     if (S == 0) return MSH_OK;
     if (!d_w) { set_error("msh_tree_nearest_bary_device: null weights"); return MSH_EINVAL; }
     hipStream_t s = pick(t, stream);
@@ -1083,6 +1200,7 @@ int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint3
 int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest"));
     MSH_TRY(check_count(S, "msh_tree_nearest"));
+    ensure_entry_cut(t);
     if (S == 0) return MSH_OK;
     if (!q || !face || !pt) { set_error("msh_tree_nearest: null argument"); return MSH_EINVAL; }
     // rows: q (24 B in) | face (4 B out) | part (4 B out) | point (24 B out)
@@ -1097,6 +1215,7 @@ int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uin
 int msh_tree_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face, double* pt, double* w) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_bary"));
     MSH_TRY(check_count(S, "msh_tree_nearest_bary"));
+    ensure_entry_cut(t);
     if (S == 0) return MSH_OK;
     if (!q || !face || !pt || !w) { set_error("msh_tree_nearest_bary: null argument"); return MSH_EINVAL; }
     const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, pt, 24}, {nullptr, w, 24}};
@@ -1109,6 +1228,7 @@ int msh_tree_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face
 int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* nodes, uint64_t* leaves) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_stats"));
     MSH_TRY(check_count(S, "msh_tree_nearest_stats"));
+    ensure_entry_cut(t);
     *nodes = 0;
     *leaves = 0;
     if (S == 0) return MSH_OK;
@@ -1614,7 +1734,7 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
             st = MSH_EDEVICE;
             break;
         }
-        st = build_entry_cut(t);  // derived from the tree: rebuilt here, not shipped
+        // the entry cut is derived from the tree: not shipped, built by the first closest-point query here
         t->ws.release();
     } while (0);
     if (st != MSH_OK) {

@@ -464,6 +464,26 @@ __device__ inline uint2 stack_get(const uint2* __restrict__ lds, const uint2* __
     return make_uint2((unsigned)v, (unsigned)(v >> 32));
 }
 
+// 30-bit Morton code of a query point in the box [l, h] (fp32 cell coordinates, 1024 cells per axis, clamped)
+__device__ inline uint32_t query_morton30(double x, double y, double z, float lx, float ly, float lz, float hx, float hy,
+                                          float hz) {
+    const float ex = hx - lx, ey = hy - ly, ez = hz - lz;
+    float nx = ex > 0.f ? ((float)x - lx) / ex : 0.5f;
+    float ny = ey > 0.f ? ((float)y - ly) / ey : 0.5f;
+    float nz = ez > 0.f ? ((float)z - lz) / ez : 0.5f;
+    nx = fminf(fmaxf(nx * 1024.f, 0.f), 1023.f);
+    ny = fminf(fmaxf(ny * 1024.f, 0.f), 1023.f);
+    nz = fminf(fmaxf(nz * 1024.f, 0.f), 1023.f);
+    auto ex10 = [](uint32_t v) {
+        v = (v * 0x00010001u) & 0xFF0000FFu;
+        v = (v * 0x00000101u) & 0x0F00F00Fu;
+        v = (v * 0x00000011u) & 0xC30C30C3u;
+        v = (v * 0x00000005u) & 0x49249249u;
+        return v;
+    };
+    return (ex10((uint32_t)nx) << 2) | (ex10((uint32_t)ny) << 1) | ex10((uint32_t)nz);
+}
+
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // blocks b and b+8 share an XCD, so give each XCD a contiguous range of logical tiles — adjacent
 // Morton-sorted query tiles then share that XCD's L2.

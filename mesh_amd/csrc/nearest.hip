@@ -1131,21 +1131,7 @@ __global__ __launch_bounds__(kBlock) void k_query_morton(const double* __restric
                                                          uint32_t* __restrict__ vals) {
     const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= S) return;
-    const float ex = hx - lx, ey = hy - ly, ez = hz - lz;
-    float nx = ex > 0.f ? ((float)q[3 * i] - lx) / ex : 0.5f;
-    float ny = ey > 0.f ? ((float)q[3 * i + 1] - ly) / ey : 0.5f;
-    float nz = ez > 0.f ? ((float)q[3 * i + 2] - lz) / ez : 0.5f;
-    nx = fminf(fmaxf(nx * 1024.f, 0.f), 1023.f);
-    ny = fminf(fmaxf(ny * 1024.f, 0.f), 1023.f);
-    nz = fminf(fmaxf(nz * 1024.f, 0.f), 1023.f);
-    auto ex10 = [](uint32_t v) {
-        v = (v * 0x00010001u) & 0xFF0000FFu;
-        v = (v * 0x00000101u) & 0x0F00F00Fu;
-        v = (v * 0x00000011u) & 0xC30C30C3u;
-        v = (v * 0x00000005u) & 0x49249249u;
-        return v;
-    };
-    keys[i] = (ex10((uint32_t)nx) << 2) | (ex10((uint32_t)ny) << 1) | ex10((uint32_t)nz);
+    keys[i] = query_morton30(q[3 * i], q[3 * i + 1], q[3 * i + 2], lx, ly, lz, hx, hy, hz);
     vals[i] = (uint32_t)i;
 }
 
@@ -1168,6 +1154,17 @@ int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* ke
                                                                            hi[2], keys, vals);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
+}
+
+int query_order(const msh_tree* tree, const double* d_q, size_t S, int lo_bit, uint32_t* keys, uint32_t* keys_alt,
+                uint32_t* perm, uint32_t* perm_alt, Workspace& ws, hipStream_t s, bool* in_alt) {
+    float lo[3], hi[3];  // the cells of query_morton
+    for (int k = 0; k < 3; ++k) {
+        const float e = tree->scene_hi[k] - tree->scene_lo[k];
+        lo[k] = tree->scene_lo[k] - kQueryBoxMargin * e;
+        hi[k] = tree->scene_hi[k] + kQueryBoxMargin * e;
+    }
+    return query_sort(d_q, S, lo, hi, lo_bit, keys, keys_alt, perm, perm_alt, ws, s, in_alt);
 }
 
 // slot i <- row perm[i] of the caller's (S, 3) array (two arrays at once when b != nullptr);
@@ -1394,8 +1391,7 @@ static KnnArgs tree_args(const msh_tree* tree, size_t S) {
 static void cut_args(const msh_tree* tree, KnnArgs& a) {
     if (!tree->d_cut || tree->B != 1) return;
     a.cut = tree->d_cut;
-    const char* e = getenv("MESH_AMD_CUT_HINT");  // 0: unled slots start without a hint (A/B)
-    a.cut_hint = (e && atoi(e) == 0) ? nullptr : tree->d_cut_hint;
+    a.cut_hint = tree->d_cut_hint;
     a.cut_G = tree->cut_G;
     for (int k = 0; k < 3; ++k) {
         a.cut_lo[k] = tree->cut_lo[k];

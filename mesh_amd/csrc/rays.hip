@@ -456,6 +456,9 @@ static int vertex_order(msh_tree* t, size_t v0, size_t nv, const uint32_t** orde
         t->d_vorder = buf;
     } else {
         if (t->d_vorder_shard) {
+            // the previous shard's launches may still run on another caller stream: wait for the end of the
+            // handle's last launch sequence (ws_done, recorded on whatever stream it ran) and for this stream
+            if (t->ws_done) (void)hipEventSynchronize(t->ws_done);
             (void)hipStreamSynchronize(s);
             (void)hipFree(t->d_vorder_shard);
         }

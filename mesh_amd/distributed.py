@@ -116,36 +116,47 @@ def gather_results_into(out, local, group=None, async_op=False):
 
 class ResultRing(object):
     """Double-buffered result slabs of a stream of query batches on every rank, each batch's results
-    all-gathered into `gathered` (the whole answer on every rank, rank-major rows).  Batch k is answered into
-    slab k % 2 while the all-gather of batch k - 1 runs on the process group's stream (over xGMI on RCCL), so
-    the exchange overlaps the next traversal instead of following it; a slab is rewritten only after the
-    gather that read it has completed (its handle is waited on, on the current stream, first).
+    all-gathered into its own gathered buffer (the whole answer on every rank, rank-major rows).  Batch k is
+    answered into slab k % 2 and gathered into gathered[k % 2] while the all-gather of batch k - 1 runs on the
+    process group's stream (over xGMI on RCCL), so the exchange overlaps the next traversal instead of following
+    it; a slab and its gathered buffer are rewritten only after the gather that used them has completed (its
+    handle is waited on, on the current stream, first).
 
-    slabs: two tuples of local result tensors (e.g. face, part, point); gathered: a tuple of the matching
-    (world n, ...) tensors.  step(compute) calls compute(slab) to enqueue batch k's work on the current
-    stream, then starts its gathers; drain() waits for every gather still running."""
+    slabs: two tuples of local result tensors (e.g. face, part, point); gathered: two tuples of the matching
+    (world n, ...) tensors (passing the same tuple twice is allowed when only the timing matters: the two
+    gathers then write one buffer in turn).  step(compute) calls compute(slab) to enqueue batch k's work on the
+    current stream, starts its gathers and returns k % 2; result(b) waits for batch b's gathers and returns
+    gathered[b] — the answer of the newest batch started in that buffer; drain() waits for every gather."""
 
     def __init__(self, slabs, gathered, group=None):
-        if len(slabs) != 2 or any(len(s) != len(gathered) for s in slabs):
-            raise ValueError("ResultRing: two slabs of %d tensors each" % len(gathered))
+        if len(slabs) != 2 or len(gathered) != 2 or any(len(s) != len(gathered[0]) for s in slabs) or \
+                len(gathered[1]) != len(gathered[0]):
+            raise ValueError("ResultRing: two slabs and two gathered buffers of the same tensors")
         self.slabs, self.gathered, self.group = slabs, gathered, group
         self.pending = [[], []]
         self.k = 0
 
     def step(self, compute):
         b = self.k & 1
-        for w in self.pending[b]:
-            w.wait()
+        self._wait(b)
         compute(self.slabs[b])
         self.pending[b] = [gather_results_into(g, x, self.group, async_op=True)
-                           for g, x in zip(self.gathered, self.slabs[b])]
+                           for g, x in zip(self.gathered[b], self.slabs[b])]
         self.k += 1
+        return b
+
+    def _wait(self, b):
+        for w in self.pending[b]:
+            w.wait()
+        self.pending[b] = []
+
+    def result(self, b):
+        self._wait(b)
+        return self.gathered[b]
 
     def drain(self):
         for b in (0, 1):
-            for w in self.pending[b]:
-                w.wait()
-            self.pending[b] = []
+            self._wait(b)
 
 
 def nearest_device(tree, q, face, part, pt, stream=None):

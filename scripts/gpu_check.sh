@@ -33,6 +33,7 @@ for s in $STAGES; do
     c5)     timeout -k 10 900 python scripts/bench_configs.py --configs c5 --reps 3 > gpurun_out/bench_c5.log 2>&1; ok c5 $? ;;
     configs) timeout -k 10 900 python scripts/bench_configs.py > gpurun_out/bench_configs.log 2>&1; ok configs $? ;;
     bench)  timeout -k 10 900 python bench.py > gpurun_out/bench.log 2>&1; ok bench $? ;;
+    repl)   timeout -k 10 300 python scripts/replication_timing.py > gpurun_out/repl.log 2>&1; ok repl $? ;;
     bench_stats) MESH_AMD_STATS_DUMP=1 timeout -k 10 600 python bench.py --steps 2 --warmup 1 --no-cpu > gpurun_out/bench_stats.log 2>&1; ok bench_stats $? ;;
     prof_small) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof_small" -o run -- python3 "$OLDPWD/bench.py" --queries 10000000 --steps 2 --warmup 1 --no-cpu > "$OLDPWD/gpurun_out/prof_small.log" 2>&1); ok prof_small $? ;;
     prof)   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 3 --warmup 1 --no-cpu > "$OLDPWD/gpurun_out/prof.log" 2>&1); ok prof $? ;;

@@ -26,6 +26,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TRAVERSAL = ("msh::k_knn<0, false, true>", "msh::k_knn_coop<0, false>")
 
 
+def sys_path_root():
+    import sys
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+
+
 def short(name):
     m = re.search(r"(msh::[A-Za-z_0-9]+(<[^>]*>)?)", name)
     return m.group(1) if m else name
@@ -58,14 +64,20 @@ def counters(pmc_dir, skip=0):
                 d = (path, row.get("Dispatch_Id") or row.get("Correlation_Id"))
                 vals[k][c][d] += float(row.get("Counter_Value") or 0.0)
                 if row.get("VGPR_Count"):
-                    vgpr[k] = (int(float(row["VGPR_Count"])), int(float(row.get("Accum_VGPR_Count") or 0)),
-                               int(float(row.get("SGPR_Count") or 0)), int(float(row.get("LDS_Block_Size") or 0)))
+                    # raw rocprofv3 fields: on gfx950 its VGPR_Count decodes the kernel descriptor's granulated
+                    # count with a granule of 4 where gfx950 allocates in granules of 8 (a 128-VGPR kernel reads
+                    # 64), so the register figures of record come from the ISA (isa_of_build below)
+                    vgpr[k] = {"VGPR_Count_rocprof_raw": int(float(row["VGPR_Count"])),
+                               "Accum_VGPR_Count": int(float(row.get("Accum_VGPR_Count") or 0)),
+                               "SGPR_Count": int(float(row.get("SGPR_Count") or 0)),
+                               "LDS_Block_Size": int(float(row.get("LDS_Block_Size") or 0)),
+                               "Scratch_Size_per_lane": int(float(row.get("Scratch_Size") or 0))}
     out = {}
     for k, cs in vals.items():
         out[k] = {c: sum(ds.values()) for c, ds in cs.items()}
         out[k]["_dispatches"] = max(len(ds) for ds in cs.values())
         if k in vgpr:
-            out[k]["_vgpr_agpr_sgpr_lds"] = vgpr[k]
+            out[k]["_launch_fields"] = vgpr[k]
     return out
 
 
@@ -79,6 +91,22 @@ def kernel_stats(stats_dir, skip=0):
                 c, ns = out.get(k, (0, 0.0))
                 out[k] = (c + 1, ns + float(row["End_Timestamp"]) - float(row["Start_Timestamp"]))
     return out
+
+
+def isa_of_build(build_id):
+    """Register allocation of the pass-1 kernel from the gfx950 ISA of the current sources (scripts/isa_check.py:
+    .vgpr_count, .vgpr_spill_count, scratch instructions), recorded only when those sources are the profiled build."""
+    import sys
+    sys.path.insert(0, ROOT)
+    from mesh_amd import _native
+    from scripts import isa_check
+    if _native.source_build_id() != build_id:
+        return {"note": "sources differ from the profiled build %s: ISA not recorded" % build_id}
+    try:
+        isa_check.LIST = True
+        return dict(isa_check.report(isa_check.compile_asm([]), 0), kernel=TRAVERSAL[0])
+    except Exception as e:  # hipcc missing: leave the field empty rather than fail the summary
+        return {"note": "ISA check failed: %s" % e}
 
 
 def main():
@@ -103,8 +131,9 @@ def main():
                 allc.setdefault(k, {}).update(cs)
     stats = kernel_stats(os.path.join(args.pmc, "stats"), args.build_traversals)
     T = 20 * args.freq ** 2
-    workload = "C3: geodesic icosphere freq %d (%d faces, %d vertices), %d uniform queries in [-1.1,1.1]^3 per GPU" % (
-        args.freq, T, 10 * args.freq ** 2 + 2, S)
+    sys_path_root()
+    import workloads
+    workload = workloads.c3_workload_name(args.freq, S)
     # one traversal = the pass-1 launches (leaders + followers) + one pass-2 launch: normalise every
     # figure per traversal by the number of pass-2 dispatches
     coop = TRAVERSAL[1]
@@ -154,6 +183,7 @@ def main():
         "traversal_ms": tot_ns / 1e6,
         "hbm_GBps": (tot_bytes / tot_ns) if (tot_bytes and tot_ns) else None,
     }
+    res["isa"] = isa_of_build(build_id)
     os.makedirs(os.path.join(ROOT, "profiles"), exist_ok=True)
     with open(os.path.join(ROOT, "profiles", "pmc_traffic.json"), "w") as fh:
         json.dump(res, fh, indent=1)

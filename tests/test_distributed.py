@@ -165,7 +165,8 @@ def _worker_ring(rank, world, port, out_q):
         from mesh_amd.distributed import ResultRing, gather_results_into
         n = 257
         slabs = [(torch.empty(n, dtype=torch.int32), torch.empty((n, 3), dtype=torch.float64)) for _ in range(2)]
-        gathered = (torch.empty(world * n, dtype=torch.int32), torch.empty((world * n, 3), dtype=torch.float64))
+        gathered = [(torch.empty(world * n, dtype=torch.int32), torch.empty((world * n, 3), dtype=torch.float64))
+                    for _ in range(2)]
         ring = ResultRing(slabs, gathered)
 
         def compute(k):
@@ -175,10 +176,15 @@ def _worker_ring(rank, world, port, out_q):
                 pt.copy_(face.to(torch.float64)[:, None] * torch.tensor([1.0, -1.0, 0.5], dtype=torch.float64))
             return run
 
+        res = {"batches": []}
         for k in range(5):  # batch k - 1's gather may still run while batch k is computed
-            ring.step(compute(k))
-        ring.drain()  # after draining, gathered holds the last batch
-        res = {"face": gathered[0].numpy().copy(), "pt": gathered[1].numpy().copy()}
+            b = ring.step(compute(k))
+            if k >= 1:  # the previous batch's answer is intact in its own buffer while batch k runs
+                g = ring.result(1 - b)
+                res["batches"].append((k - 1, g[0].numpy().copy(), g[1].numpy().copy()))
+        ring.drain()
+        g = ring.result(b)
+        res["batches"].append((4, g[0].numpy().copy(), g[1].numpy().copy()))
         # shape / dtype validation of the equal-shard gather
         try:
             gather_results_into(torch.empty(world * n + 1, dtype=torch.int32), slabs[0][0])
@@ -202,9 +208,50 @@ def test_result_ring_world2():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    n, k = 257, 4
-    want = np.concatenate([np.arange(n) + 1000 * r + 100000 * k for r in range(world)]).astype(np.int32)
+    n = 257
     for _, r in res:
-        assert (r["face"] == want).all()
-        assert (r["pt"] == want[:, None].astype(np.float64) * np.array([1.0, -1.0, 0.5])).all()
+        assert [k for k, _, _ in r["batches"]] == [0, 1, 2, 3, 4]
+        for k, face, pt in r["batches"]:
+            want = np.concatenate([np.arange(n) + 1000 * q + 100000 * k for q in range(world)]).astype(np.int32)
+            assert (face == want).all()
+            assert (pt == want[:, None].astype(np.float64) * np.array([1.0, -1.0, 0.5])).all()
         assert r["bad_shape_rejected"]
+
+
+# ---- the bench's N > 1 workload: one C3 stream, drawn whole on every rank, answered in contiguous shards ----
+def _worker_stream(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import workloads as W
+        from mesh_amd.distributed import gather_results
+        S = 10_007  # not a multiple of the world size: the shards differ by one row
+        q = W.c3_stream(S, "cpu")
+        mine, (a, b) = W.c3_shard(q, rank, world)
+        assert mine.is_contiguous() and mine.data_ptr() == q[a].data_ptr()
+        # every rank drew the same stream; the gathered shards reassemble it (and its N = 1 draw)
+        whole = gather_results(mine.clone(), S)
+        out_q.put((rank, (a, b), whole.numpy().copy(), W.c3_stream(S, "cpu").numpy()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_c3_stream_shards_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_stream, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(world)], key=lambda x: x[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import workloads as W
+    ref = W.c3_stream(10_007, "cpu").numpy()
+    assert [r[1] for r in res] == [(0, 5004), (5004, 10_007)]
+    for _, _, whole, own in res:
+        assert np.array_equal(whole, ref) and np.array_equal(own, ref)
+    assert ref.min() >= -1.1 and ref.max() <= 1.1

@@ -170,25 +170,33 @@ def test_c3_sample_both_leaf_paths(oracle, monkeypatch):
     assert np.array_equal(outs[0][2][rows], bpt)
 
 
-def test_entry_cut_bit_exact(oracle, monkeypatch):
-    # C3 mesh: walks from the entry cut (default grid with and without the cell hints, a coarse 8^3 grid) give
-    # the arrays of walks from the root (MESH_AMD_ENTRY_CUT=0), on uniform queries reaching past the grid (+-1.25 around the unit sphere),
-    # near-surface queries and queries on cell faces of the default grid; 2000 rows match brute force
+def _nearest_tree(t, q):
+    from mesh_amd import spatialsearch
+    face, part, pt = spatialsearch.aabbtree_nearest(t, np.ascontiguousarray(q, np.float64))
+    return face[0], part[0], pt
+
+
+def test_entry_cut_bit_exact(oracle):
+    # C3 mesh: walks from the entry cut (the default grid, a coarse 8^3 one) give the arrays of walks from the
+    # root (msh_tree_set_entry_cut(0)), on uniform queries reaching past the grid (+-1.25 around the unit
+    # sphere), near-surface queries and queries on cell faces of the default grid; 2000 rows match brute force
+    from mesh_amd import spatialsearch
     v, f = W.c3_mesh()
     rng = np.random.default_rng(41)
-    G = int(round(np.cbrt(2 * f.shape[0])))
+    G = int(round(np.cbrt(8 * f.shape[0])))
     lo, w = -1.25, 2.5 / G  # scene box +-1 (icosphere vertices on the unit sphere), widened by 1/4
     on_faces = rng.uniform(-1.2, 1.2, (20_000, 3))
     on_faces[np.arange(20_000), rng.integers(0, 3, 20_000)] = lo + rng.integers(0, G + 1, 20_000) * w
     surf, _ = W.surface_samples(v, f, 50_000, seed=42, sigma=0.003)
     q = np.concatenate([rng.uniform(-1.4, 1.4, (150_000, 3)), surf, on_faces])
+    t = spatialsearch.aabbtree_compute(v, f)
     outs = []
-    for cut, hint, g in (("0", "1", None), ("1", "1", None), ("1", "0", None), ("1", "1", "8")):
-        monkeypatch.setenv("MESH_AMD_ENTRY_CUT", cut)
-        monkeypatch.setenv("MESH_AMD_CUT_HINT", hint)  # unled slots hinted by their cell's centre answer
-        if g:
-            monkeypatch.setenv("MESH_AMD_CUT_G", g)
-        outs.append(_nearest(v, f, q))
+    for g in (0, -1, 8):
+        t.set_entry_cut(g)
+        outs.append(_nearest_tree(t, q))
+        info = t.entry_cut_info()
+        assert info["state"] == ("off" if g == 0 else "built"), info
+        assert info["G"] == (0 if g == 0 else (G if g < 0 else g))
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert np.array_equal(a, b)
@@ -196,6 +204,125 @@ def test_entry_cut_bit_exact(oracle, monkeypatch):
     bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[rows])
     assert np.array_equal(outs[1][0][rows], bf) and np.array_equal(outs[1][1][rows], bp)
     assert np.array_equal(outs[1][2][rows], bpt)
+
+
+def test_entry_cut_lazy_and_failure_fallback(oracle):
+    # The cut is built by the first closest-point query, never by the build, by rays or by the normals metric;
+    # a cut that cannot be built (here 4096^3 cells: more than one query call holds) is not an error: the handle
+    # records the failure and its queries start at the root with the same answers.
+    from mesh_amd import aabb_normals, spatialsearch
+    v, f = W.c2_mesh()  # 13,776 faces: above the 4096-face floor
+    q, _ = W.surface_samples(v, f, 20000, seed=51, sigma=0.02)
+    t = spatialsearch.aabbtree_compute(v, f)
+    assert t.entry_cut_info()["state"] == "pending"
+    nrm = np.tile([[0.0, 0.0, 1.0]], (q.shape[0], 1))
+    spatialsearch.aabbtree_nearest_alongnormal(t, q, nrm)
+    assert t.entry_cut_info()["state"] == "pending" and t.entry_cut_info()["bytes"] == 0
+    ref = _nearest_tree(t, q)
+    info = t.entry_cut_info()
+    assert info["state"] == "built" and info["bytes"] == info["G"] ** 3 * 68 and info["build_ms"] > 0
+    t.set_entry_cut(4096)
+    got = _nearest_tree(t, q)
+    info = t.entry_cut_info()
+    assert info["state"] == "failed" and info["bytes"] == 0 and info["G"] == 0
+    for a, b in zip(ref, got):
+        assert np.array_equal(a, b)
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[:2000])
+    assert np.array_equal(got[0][:2000], bf) and np.array_equal(got[1][:2000], bp) and np.array_equal(got[2][:2000], bpt)
+    # back to the automatic grid: rebuilt by the next query
+    t.set_entry_cut(-1)
+    assert t.entry_cut_info()["state"] == "pending"
+    again = _nearest_tree(t, q)
+    assert t.entry_cut_info()["state"] == "built"
+    for a, b in zip(ref, again):
+        assert np.array_equal(a, b)
+    h = aabb_normals.aabbtree_n_compute(v, f, 0.1)
+    aabb_normals.aabbtree_n_nearest(h, q, nrm)
+    assert h.entry_cut_info()["state"] == "off" and h.entry_cut_info()["bytes"] == 0
+    with pytest.raises(ValueError):
+        t.set_entry_cut(5000)
+
+
+def test_c3_replication_roundtrip():
+    # north_star's replication path on one GPU: the C3 tree packed into one device blob (what rank 0
+    # broadcasts), unpacked on the same device (what every other rank does), answers the C3 stream bit for
+    # bit like the source handle; the receiver builds its own entry cut on its first query
+    import torch
+    from mesh_amd import _native, spatialsearch
+    from mesh_amd.distributed import nearest_device
+    v, f = W.c3_mesh()
+    src = spatialsearch.aabbtree_compute(v, f)
+    blob = torch.empty(_native.blob_size(src), dtype=torch.uint8, device="cuda:0")
+    _native.blob_pack(src, blob.data_ptr())
+    torch.cuda.synchronize()
+    dst = _native.blob_unpack(blob.data_ptr(), blob.numel(), 0)
+    del blob
+    assert dst.entry_cut_info()["state"] == "pending"
+    a, b = src.info(), dst.info()
+    for k in ("n_points", "n_faces", "n_nodes", "bytes", "max_depth", "node_bytes", "leaf_bytes"):
+        assert getattr(a, k) == getattr(b, k), k
+    q = W.c3_stream(4_000_000, "cuda:0")
+    outs = []
+    for t in (src, dst):
+        o = (torch.empty(q.shape[0], dtype=torch.int32, device="cuda:0"),
+             torch.empty(q.shape[0], dtype=torch.int32, device="cuda:0"),
+             torch.empty((q.shape[0], 3), dtype=torch.float64, device="cuda:0"))
+        nearest_device(t, q, *o)
+        outs.append(o)
+    torch.cuda.synchronize()
+    assert dst.entry_cut_info()["state"] == "built"
+    assert dst.entry_cut_info()["G"] == src.entry_cut_info()["G"]
+    for x, y in zip(*outs):
+        assert torch.equal(x, y)
+
+
+def test_query_order_one_sweep_equals_radix():
+    # the one-sweep query sort gives the permutation of the 3-launch radix sort it replaced, on the C3 stream
+    # (100M rows: 24,415 tiles of look-back), a ragged size, a size below one tile and rows with NaN / inf
+    import torch
+    from mesh_amd import _native, spatialsearch
+    v, f = W.c3_mesh()
+    t = spatialsearch.aabbtree_compute(v, f)
+    q = W.c3_stream(100_000_000, "cuda:0")
+    bad = W.c3_stream(50_000, "cuda:0", seed=7)
+    bad[::7, 0] = float("nan")
+    bad[3::11, 2] = float("inf")
+    for x in (q, q[:12_345_677], q[:1000], bad):
+        perms = []
+        for sorter in (0, 1):
+            p = torch.empty(x.shape[0], dtype=torch.int32, device="cuda:0")
+            _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), x.shape[0], p.data_ptr(), sorter,
+                                                             None))
+            perms.append(p)
+        torch.cuda.synchronize()
+        assert torch.equal(perms[0], perms[1])
+        assert torch.equal(torch.sort(perms[0].long())[0], torch.arange(x.shape[0], device="cuda:0"))
+
+
+def test_c3_stream_shards_equal_whole():
+    # BASELINE configs[2] sharded as bench.py does for N = 8, on one GPU: each of the 8 contiguous shards of the
+    # 100M-query C3 stream answered by its own call (its own Morton sort, leader phases, entry cut walks and
+    # pass 2 at 12.5M queries) gives exactly the rows of the answer of the whole stream
+    import torch
+    from mesh_amd import spatialsearch
+    from mesh_amd.distributed import nearest_device
+    v, f = W.c3_mesh()
+    t = spatialsearch.aabbtree_compute(v, f)
+    S = 100_000_000
+    q = W.c3_stream(S, "cuda:0")
+
+    def slab(n):
+        return (torch.empty(n, dtype=torch.int32, device="cuda:0"), torch.empty(n, dtype=torch.int32, device="cuda:0"),
+                torch.empty((n, 3), dtype=torch.float64, device="cuda:0"))
+
+    whole, parts = slab(S), slab(S)
+    nearest_device(t, q, *whole)
+    for r in range(8):
+        qs, (a, b) = W.c3_shard(q, r, 8)
+        nearest_device(t, qs, parts[0][a:b], parts[1][a:b], parts[2][a:b])
+    torch.cuda.synchronize()
+    for x, y in zip(whole, parts):
+        assert torch.equal(x, y)
 
 
 def test_c3_full_size_properties(oracle):
@@ -236,9 +363,7 @@ def test_c3_headline_stream(oracle):
     from mesh_amd.distributed import nearest_device
     v, f = W.c3_mesh()
     S = 100_000_000
-    g = torch.Generator(device="cuda:0")
-    g.manual_seed(3)
-    dq = (torch.rand((S, 3), generator=g, dtype=torch.float64, device="cuda:0") * 2.2 - 1.1).contiguous()
+    dq = W.c3_stream(S, "cuda:0")
     t = spatialsearch.aabbtree_compute(v, f)
     df = torch.empty(S, dtype=torch.int32, device="cuda:0")
     dp = torch.empty(S, dtype=torch.int32, device="cuda:0")

@@ -144,6 +144,31 @@ def c3_mesh():
     return geodesic_icosphere(224)
 
 
+def c3_workload_name(freq, S):
+    """config.workload of bench.py (and the key its PMC profile is matched on): one C3 query stream of S
+    rows per step, sharded contiguously over the GPUs."""
+    return ("C3: geodesic icosphere freq %d (%d faces, %d vertices), %d uniform queries in [-1.1,1.1]^3 (seed 3) "
+            "per step, sharded contiguously over the GPUs" % (freq, 20 * freq ** 2, 10 * freq ** 2 + 2, S))
+
+
+def c3_stream(S, device, seed=3):
+    """The C3 query stream (BASELINE configs[2]): S rows uniform in [-1.1, 1.1]^3 drawn by torch's generator
+    for `device` with `seed` — the same rows on every device of one kind, so every rank can draw the whole
+    stream and keep its shard (c3_shard) instead of receiving it.  (S, 3) float64, contiguous."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    return (torch.rand((S, 3), generator=g, dtype=torch.float64, device=device) * 2.2 - 1.1).contiguous()
+
+
+def c3_shard(q, rank, world):
+    """Rank `rank`'s contiguous shard of the (S, 3) stream q (mesh_amd.distributed.shard_range) as a view
+    (rows of a C-contiguous array: contiguous), with its [start, stop)."""
+    from mesh_amd.distributed import shard_range
+    a, b = shard_range(q.shape[0], rank, world)
+    return q[a:b], (a, b)
+
+
 def c5_mesh():
     v, f = geodesic_icosphere(500)
     th = np.arccos(np.clip(v[:, 2], -1, 1))
