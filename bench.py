@@ -48,7 +48,8 @@ def parse():
                     help="queries per step: one C3 stream, sharded contiguously over the GPUs")
     ap.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling (100M per GPU) line")
     ap.add_argument("--freq", type=int, default=224, help="icosphere frequency (224 -> 1,003,520 faces)")
-    ap.add_argument("--cpu-seconds", type=float, default=24.0, help="CPU baseline time budget (both modes)")
+    ap.add_argument("--cpu-queries", type=int, default=24000,
+                    help="CPU baseline: fixed sample of queries per host thread (1 thread: ~12 s)")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
@@ -64,46 +65,43 @@ def host_threads():
         return os.cpu_count() or 1
 
 
-def cpu_baseline(v, f, budget_s):
-    """Oracle CGAL-tree restatement on the C3 query stream (seed 3, rank 0), timed as BASELINE.md §2
-    prescribes: 3 warm-up chunks, then the median rate of 10 timed chunks, in two modes:
+def cpu_baseline(v, f, per_thread):
+    """Oracle CGAL-tree restatement on the C3 query stream (seed 3, rank 0), in two modes:
       * 1 thread (the reference's aabbtree_nearest loop is serial: its omp pragma is compiled out,
         spatialsearchmodule.cpp:212-214) -> the reported `cpu_baseline`;
       * all host threads this process may use (OpenMP over queries) -> `cpu_baseline_allcores`.
-    The chunk size is chosen so the 13 chunks of the 1-thread mode take about 2/3 of budget_s and those of the
-    all-threads mode the rest: the reported (1-thread) chunks hold ~3k queries each, so the few costly queries
-    near the sphere's centre (equidistant from much of the mesh) weigh alike in every chunk."""
+    Each mode answers a FIXED sample — the same rows of the stream in every session (per_thread x threads
+    queries after 2,000 x threads warm-up rows) — and reports its total queries / total time, so the sample's
+    content (its few costly queries near the sphere's centre, equidistant from much of the mesh) is identical
+    from run to run and only the host's speed varies; 4 sub-chunks give the spread."""
     from oracle import oracle as O
     t0 = time.perf_counter()
     tree = O.CgalTree(v, f, hint=True)
     build_s = time.perf_counter() - t0
-    rng = np.random.default_rng(3)
-    pool = rng.uniform(-1.1, 1.1, (4_000_000, 3))
     out = {}
-    for mode, threads, share in (("1", 1, 2.0 / 3.0), ("all", host_threads(), 1.0 / 3.0)):
-        # calibrate: how many queries per second at this thread count
-        n = 4000 * threads
-        t0 = time.perf_counter()
-        tree.nearest(pool[:n], threads=threads)
-        rate0 = n / max(time.perf_counter() - t0, 1e-6)
-        chunk = int(min(max(rate0 * budget_s * share / 13, 500), pool.shape[0] // 13))
-        rates, off = [], 0
-        for k in range(13):
-            q = pool[off:off + chunk]
-            off += chunk
+    for mode, threads in (("1", 1), ("all", host_threads())):
+        n = per_thread * threads
+        warm = 2000 * threads
+        pool = np.random.default_rng(3).uniform(-1.1, 1.1, (warm + n, 3))
+        tree.nearest(pool[:warm], threads=threads)
+        chunk = n // 4
+        times = []
+        for k in range(4):
+            q = np.ascontiguousarray(pool[warm + k * chunk:warm + (k + 1) * chunk])
             t0 = time.perf_counter()
             tree.nearest(q, threads=threads)
-            dt = time.perf_counter() - t0
-            if k >= 3:
-                rates.append(chunk / dt)
-        out[mode] = (float(np.median(rates)), chunk, threads)
+            times.append(time.perf_counter() - t0)
+        rates = [chunk / t for t in times]
+        out[mode] = (4 * chunk / sum(times), 4 * chunk, threads, min(rates), max(rates))
+
     def obj(mode, label):
-        rate, chunk, threads = out[mode]
+        rate, n, threads, lo, hi = out[mode]
         return {"value": rate, "unit": "queries/s", "cores": threads, "kind": "port",
-                "sample": "median of 10 timed chunks of %d uniform C3 queries (seed 3; 3 warm-up chunks) on the "
+                "sample": "%d uniform C3 queries (the stream's rows after %d warm-up rows, seed 3; the same rows "
+                          "every session), total queries / total time (4 sub-chunks: %.0f-%.0f q/s) on the "
                           "1,003,520-face icosphere; CGAL-faithful restatement (median-split AABB tree + KD hint, "
                           "fp64, g++ -O3 -ffp-contract=off), %s; tree build %.2f s excluded"
-                          % (chunk, label, build_s)}
+                          % (n, 2000 * threads, lo, hi, label, build_s)}
     return (obj("1", "1 thread (the reference's aabbtree_nearest loop is serial, spatialsearchmodule.cpp:212-217)"),
             obj("all", "OpenMP over queries on %d host threads" % out["all"][2]))
 
@@ -337,7 +335,7 @@ def main():
         out["value_weak_100M_per_gpu"] = world * S * args.steps / elapsed_weak
         out["ms_per_step_weak"] = elapsed_weak / args.steps * 1e3
     if world == 1 and not args.no_cpu:
-        out["cpu_baseline"], out["cpu_baseline_allcores"] = cpu_baseline(v, f, args.cpu_seconds)
+        out["cpu_baseline"], out["cpu_baseline_allcores"] = cpu_baseline(v, f, args.cpu_queries)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

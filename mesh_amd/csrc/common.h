@@ -23,7 +23,10 @@
 namespace msh {
 
 constexpr int kBlock = 256;          // 4 waves of 64 lanes
-constexpr int kStack = 16;           // per-lane LDS stack entries; deeper entries spill to global memory
+#ifndef MSH_KSTACK
+#define MSH_KSTACK 16
+#endif
+constexpr int kStack = MSH_KSTACK;         // per-lane LDS stack entries; deeper entries spill to global memory
 constexpr double kSlack = 1.0 + 9.094947017729282e-13;  // 1 + 2^-40: fp64 rounding margin for culls
 
 // float index within a node:  0-5 frame (n0 t0 n1 t1 n2 t2: the (n_k, t_k) pairs are 8-B aligned, so

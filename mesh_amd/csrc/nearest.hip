@@ -371,7 +371,7 @@ __device__ inline D3 heidrich_bary(const D3& p, const D3& a, const D3& b, const 
 // Outputs of slot i from its policy (winner's leaf -> point / part recomputed exactly).
 template <int MODE, class Pol>
 __device__ inline void write_result(const KnnArgs& a, size_t i, const D3& q, const Pol& pol) {
-    const bool rec = a.res && (!a.direct || a.phase == 1 || a.phase == 3);  // slot-order record
+    const bool rec = a.res && (!a.direct || a.phase == 1 || a.phase == 3 || a.phase == 4);  // slot-order record
     const bool out = !a.res || a.direct;                                      // caller's arrays
     const size_t r = a.res ? (size_t)a.perm[i] : i;                           // caller's row
     if constexpr (MODE == 2) {
@@ -465,10 +465,11 @@ static_assert(kLead2 % kLead == 0 && kLead2 / kLead >= 2, "kLead2: a multiple of
 constexpr int kLeafQ = 4;
 constexpr int kLeafRound = 2;
 
-// slot of work unit k in the launch's phase: 3 super-leaders, 1 leaders (without the super-leaders), 2
-// followers, 0 every slot
+// slot of work unit k in the launch's phase: 3 super-leaders, 1 leaders (without the super-leaders), 4 every leader
+// (trees with cell hints: no super-leader launch), 2 followers, 0 every slot
 __device__ inline size_t slot_of(const KnnArgs& a, size_t k) {
     if (a.phase == 3) return k * kLead2;
+    if (a.phase == 4) return k * kLead;
     if (a.phase == 1) {
         constexpr size_t r = kLead2 / kLead;
         return kLead * (k + k / (r - 1) + 1);
@@ -509,6 +510,11 @@ __device__ inline int leader_leaf(const KnnArgs& a, size_t i, const D3& q, size_
     return leaf;
 }
 
+// number of set bits of m below this lane (v_mbcnt: no per-lane mask register)
+__device__ inline unsigned lanes_below(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
 // Wave leaf list (closest-point modes): lanes append the leaf children that survive their node's bound to a
 // ring of (leaf << 6 | owner lane) entries in LDS shared by the wave, and the wave evaluates them in rounds of
 // 64 — one entry per lane, every round full except when nobody can move — instead of per-lane queues flushed
@@ -517,6 +523,14 @@ __device__ inline int leader_leaf(const KnnArgs& a, size_t i, const D3& q, size_
 // (face << 32 | leaf) among the entries that reached it: the lexicographic (d2, face) rule.
 // kPend (C3, M q/s): 3: 1236, 4: 1346, 8: 1593, 16: 1677, 32: 1706, unbounded: 1689; per-lane queues 1541.
 constexpr int kPend = 32;
+#ifndef MSH_REFILL
+#define MSH_REFILL 0  // list path: persistent lanes that take new units as they finish (see k_knn)
+#endif
+#ifndef MSH_REFILL_LANES
+#define MSH_REFILL_LANES 32
+#endif
+[[maybe_unused]] constexpr int kRefill = MSH_REFILL_LANES;  // free lanes of a wave that trigger a refill
+
 constexpr unsigned kRing = 256;     // ring entries per wave: < 64 left after full rounds + <= 128 per step
 constexpr size_t kListMaxLeaves = (size_t)1 << 26;  // leaf index bits of a ring entry
 constexpr size_t kLeadMinLeaves = 4096;  // smaller trees skip the leader phases (C1: 0.56 -> 0.29 ms)
@@ -525,7 +539,10 @@ constexpr size_t kLeadMinLeaves = 4096;  // smaller trees skip the leader phases
 // step): the register budget drops from 139 to 128 VGPRs at the cost of a few spills of loop-invariant values
 // outside the node step (C3: +10 % over the compiler's 3 waves; 5 waves spill in the loop: -30 %; 5 waves also
 // need <= 32 KB of LDS per block).
-#define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 1 : 4)))
+#ifndef MSH_KNN_WAVES
+#define MSH_KNN_WAVES 4
+#endif
+#define MSH_KNN_ATTR __attribute__((amdgpu_waves_per_eu(MODE == 1 ? 1 : MSH_KNN_WAVES)))
 // Entry cut.  The grid cell of q (centre c, half-diagonal r) holds up to kCutK tree entries (node or ~leaf)
 // whose bound from c is within (d(c) + 2r)^2, d(c) = c's exact distance to the mesh, and which together cover
 // every such subtree; any other subtree lies farther than d(c) + 2r from c, so farther than d(c) + r >= d(q)
@@ -581,6 +598,232 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     unsigned long long u_trav_it = 0, u_trav_lanes = 0, u_leaf_it = 0, u_leaf_lanes = 0;  // STATS: wave iterations
     unsigned n_nodes = 0, n_leaves = 0;
     unsigned n_impr = 0, n_hinted = 0, n_hint_won = 0;  // STATS: improving leaf tests, hinted queries, hint = answer
+#if MSH_REFILL
+    // Persistent lanes (list path): a lane whose query is finished takes the phase's next unit instead of idling
+    // until the slowest lane of its tile is done.  Finished lanes wait until kRefill lanes of the wave are free
+    // (or nobody can move); then, together, they store their answers, take the next units of the wave's current
+    // tile (Morton-adjacent slots, in lane order; a new tile from the XCD-group counters when it runs out), append
+    // their hint leaves to the ring, the wave evaluates everything pending, and the new queries start their walks
+    // from their cells' entries with the hint's bound.
+    bool refill_done = false;
+    if constexpr (kList) {
+      if (a.T > 1) {
+        refill_done = true;
+        uint32_t* ring = lsh + (tid >> 6) * (kRing + 64 * 4);
+        unsigned long long* bd = reinterpret_cast<unsigned long long*>(ring + kRing);  // per owner: d2 bits
+        unsigned long long* bfl = bd + 64;                                              // (face << 32 | leaf)
+        const unsigned max_steps = (unsigned)min(a.T, (size_t)UINT_MAX);
+        bool has = false;  // the lane holds a (finite) query: traversing, or finished and waiting to store it
+        unsigned i = 0;  // slot (S < 2^32)
+        auto pol = make_pol<MODE>(a, 0, D3{0.0, 0.0, 0.0});
+        QF qf = make_qf(pol.q, a.org, a.tm);
+        Walker w{0, 0};
+        bool active = false, want_defer = false, deferred = false;
+        int nq = 0;
+        unsigned last_pos = 0, steps = 0, tot = 0;
+        int hint_leaf = -1;  // STATS
+        unsigned head = 0, tail = 0;
+        unsigned tile = 0, cursor = 64;  // wave-uniform: current tile, units of it dealt so far
+        bool exhausted = false;
+        auto run_rounds = [&](unsigned upto) {
+            while (head != upto) {
+                const unsigned n = min(64u, upto - head);
+                bd[lane] = (unsigned long long)__double_as_longlong(pol.best);
+                bfl[lane] = ~0ull;
+                const bool valid = (unsigned)lane < n;
+                const uint32_t en = ring[(head + (valid ? (unsigned)lane : 0u)) & (kRing - 1)];
+                const int src = (int)(en & 63u);
+                const int leaf = (int)(en >> 6);
+                const D3 x = D3{__shfl(pol.q.x, src), __shfl(pol.q.y, src), __shfl(pol.q.z, src)};
+                uint32_t f;
+                const double d2 = pol.eval(leaf, x, f);
+                const unsigned long long kb = (unsigned long long)__double_as_longlong(d2);
+                asm volatile("" ::: "memory");
+                if (valid) atomicMin(&bd[src], kb);
+                asm volatile("" ::: "memory");
+                if (valid && bd[src] == kb) atomicMin(&bfl[src], ((unsigned long long)f << 32) | (unsigned)leaf);
+                asm volatile("" ::: "memory");
+                const unsigned long long nb = bd[lane], nf = bfl[lane];
+                const double nd = __longlong_as_double((long long)nb);
+                const uint32_t nface = (uint32_t)(nf >> 32);
+                if (nf != ~0ull && (nd < pol.best || (nd == pol.best && nface < pol.best_face))) {
+                    pol.best = nd;
+                    pol.best_face = nface;
+                    pol.best_leaf = (int)(uint32_t)nf;
+                    pol.relim();
+                    if (STATS) ++n_impr;
+                }
+                asm volatile("" ::: "memory");
+                if (STATS) {
+                    if (valid) ++n_leaves;
+                    if (lane == 0) {
+                        ++u_leaf_it;
+                        u_leaf_lanes += n;
+                    }
+                }
+                head += n;
+            }
+            if ((int)(last_pos - head) < 0) nq = 0;  // every entry of this lane is evaluated
+        };
+        // appends leaf l (>= 0) of this lane to the ring, in lane order; at most one per lane per call
+        auto append1 = [&](int l) {
+            const unsigned long long m = __ballot(l >= 0);
+            if (l >= 0) {
+                const unsigned pos = tail + lanes_below(m);
+                ring[pos & (kRing - 1)] = ((uint32_t)l << 6) | (uint32_t)lane;
+                last_pos = pos;
+                ++nq;
+            }
+            tail += (unsigned)__popcll(m);
+        };
+        for (;;) {
+            // a lane past its budget defers once its own leaves are evaluated (pass 2 then owns the query)
+            if (want_defer && nq == 0) {
+                want_defer = false;
+                const unsigned dslot = atomicAdd(a.n_deferred, 1u);
+                if (dslot < a.max_deferred) {
+                    DeferRec r;
+                    r.slot = i;
+                    r.face = pol.best_face;
+                    r.leaf = pol.best_leaf;
+                    r.pad = 0;
+                    r.best = pol.best;
+                    r.pad2 = 0;
+                    a.deferred[dslot] = r;
+                    active = false;
+                    deferred = true;
+                }
+                // deferred list full: finish here without a budget
+            }
+            const bool done = has && !active && nq == 0 && !want_defer;
+            const bool can = has && active && !want_defer && nq < kPend;
+            const unsigned long long mcan = __ballot(can);
+            const int n_free = __popcll(__ballot(!has || done));
+            if (n_free >= kRefill || (mcan == 0ull && tail == head)) {
+                // ---- refill: store the finished lanes' answers, deal new units to the free lanes ----
+                if (done) {
+                    if (deferred) {
+                        if ((a.phase == 1 || a.phase == 3 || a.phase == 4) && a.res) {
+                            // later phases take hints from this slot before pass 2 answers it: publish the closest
+                            // point of the best face so far (a point on the mesh), or NO_FACE when it has none yet
+                            D3 o = D3{NAN, NAN, NAN};
+                            uint32_t f = MSH_NO_FACE;
+                            if (pol.best_leaf >= 0) {
+                                D3 ta, tb, tc;
+                                int part;
+                                load_tri(static_cast<const TriRec*>(a.leaves), pol.best_leaf, ta, tb, tc, f);
+                                closest_on_triangle(pol.q, ta, tb, tc, o, part);
+                            }
+                            store_qres(a.res + i, f, (uint32_t)pol.best_leaf, o.x, o.y, o.z);
+                        }
+                    } else if (!STATS || a.res) {
+                        write_result<MODE>(a, i, pol.q, pol);
+                    }
+                    if (STATS) {
+                        if (hint_leaf >= 0 && pol.best_leaf == hint_leaf) ++n_hint_won;
+                        atomicAdd(a.stats + 8 + 9 * (a.phase == 3 ? 0 : ((a.phase == 1 || a.phase == 4) ? 1 : 2)) + 2,
+                                  (unsigned long long)tot);
+                    }
+                    has = false;
+                }
+                bool fresh = false;  // this lane took a unit in this refill
+                for (;;) {
+                    const unsigned long long idle = __ballot(!has && !fresh);
+                    if (idle == 0ull || exhausted) break;
+                    if (cursor >= 64u) {
+                        unsigned t = 0;
+                        if (lane == 0) t = dequeue_tile(a.counters, a.ntiles, group);
+                        t = __shfl(t, 0);
+                        if (t >= a.ntiles) {
+                            exhausted = true;
+                            break;
+                        }
+                        tile = t;
+                        cursor = 0;
+                    }
+                    const unsigned r = lanes_below(idle);
+                    const unsigned n_take = min((unsigned)__popcll(idle), 64u - cursor);
+                    if (!has && !fresh && r < n_take) {
+                        fresh = true;
+                        const size_t k = (size_t)tile * 64 + cursor + r;
+                        bool live = k < a.nunits;
+                        if (live) {
+                            const size_t si = slot_of(a, k);
+                            live = si < a.S;
+                            i = (unsigned)si;
+                        }
+                        if (live) {
+                            const D3 q = load_q(a, i);
+                            if (a.inv_w && !a.direct) a.inv_w[a.qperm[i]] = (uint32_t)i;
+                            pol = make_pol<MODE>(a, i, q);
+                            if (!finite3(q)) {  // no distance is defined: NO_FACE / NaN, no traversal
+                                if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
+                            } else {
+                                has = true;
+                            }
+                        }
+                    }
+                    cursor += n_take;
+                }
+                const bool nw = fresh && has;  // a new query to start
+                if (__ballot(nw) != 0ull) {
+                    size_t cell = kNoCell;
+                    int lf = -1;
+                    if (nw) {
+                        const int root = query_root(a, i, pol.q, qf);
+                        w = Walker{root, 0};
+                        active = false;
+                        want_defer = false;
+                        deferred = false;
+                        steps = 0;
+                        if (STATS) tot = 0;
+                        cell = cut_cell(a, pol.q);
+                        if (a.cut_hint && cell != kNoCell && a.phase != 2) lf = a.cut_hint[cell];
+                        else if (a.phase == 2) lf = leader_leaf(a, i, pol.q, kFWin, kLead);
+                        else if (a.phase == 1) lf = leader_leaf(a, i, pol.q, kLWin * kLead2, kLead2);
+                        if (STATS) {
+                            hint_leaf = lf;
+                            if (lf >= 0) ++n_hinted;
+                        }
+                    }
+                    // the hints go through the ring with everything pending, so each walk starts with its bound
+                    append1(nw ? lf : -1);
+                    run_rounds(tail);
+                    if (nw) active = cell != kNoCell ? cut_start(a, cell, pol, w, lds, spill) : true;
+                }
+                if (__ballot(has) == 0ull && exhausted) break;
+                continue;
+            }
+            if (STATS) {
+                const int nt = __popcll(mcan);
+                if (lane == 0 && mcan) {
+                    ++u_trav_it;
+                    u_trav_lanes += nt;
+                }
+            }
+            int l0 = -1, l1 = -1;
+            if (can) {
+                active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, l0, l1, kPend - nq);
+                ++steps;
+                if (STATS) ++tot;
+                if (active && steps >= max_steps) active = false;  // each node is entered once: corrupt tree
+                if (active && steps == a.budget) want_defer = true;
+            }
+            // append this step's leaves (at most two per lane) to the ring, in lane order
+            if (l0 < 0) {
+                l0 = l1;
+                l1 = -1;
+            }
+            append1(l0);
+            append1(l1);
+            // full rounds while lanes can move; everything once nobody can
+            const unsigned upto = mcan ? head + ((tail - head) & ~63u) : tail;
+            if (upto != head) run_rounds(upto);
+        }
+      }
+    }
+    if (!refill_done)
+#endif
     for (;;) {
         unsigned tile = 0;
         if (lane == 0) tile = dequeue_tile(a.counters, a.ntiles, group);
@@ -698,47 +941,25 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 }
                 if ((int)(last_pos - head) < 0) nq = 0;  // every entry of this lane is evaluated
             };
+            unsigned dslot = 0;  // this lane's deferred-list slot (deferred)
             for (;;) {
-                // a lane past its budget defers once its own leaves are evaluated (pass 2 then owns the query)
+                // a lane past its budget defers once its own leaves are evaluated (pass 2 then owns the query); its
+                // records are written after the tile's loop, so the loop holds no copy of the construction
                 if (want_defer && nq == 0) {
                     want_defer = false;
-                    const unsigned slot = atomicAdd(a.n_deferred, 1u);
-                    if (slot < a.max_deferred) {
-                        if ((a.phase == 1 || a.phase == 3) && a.res) {
-                            // later phases take hints from this slot before pass 2 answers it: publish the closest
-                            // point of the best face so far (a point on the mesh), or NO_FACE when it has none yet
-                            D3 o = D3{NAN, NAN, NAN};
-                            uint32_t f = MSH_NO_FACE;
-                            if (pol.best_leaf >= 0) {
-                                D3 ta, tb, tc;
-                                int part;
-                                load_tri(static_cast<const TriRec*>(a.leaves), pol.best_leaf, ta, tb, tc, f);
-                                closest_on_triangle(q, ta, tb, tc, o, part);
-                            }
-                            store_qres(a.res + i, f, (uint32_t)pol.best_leaf, o.x, o.y, o.z);
-                        }
-                        DeferRec r;
-                        r.slot = (uint32_t)i;
-                        r.face = pol.best_face;
-                        r.leaf = pol.best_leaf;
-                        r.pad = 0;
-                        r.best = pol.best;
-                        r.pad2 = 0;
-                        a.deferred[slot] = r;
+                    dslot = atomicAdd(a.n_deferred, 1u);
+                    if (dslot < a.max_deferred) {
                         active = false;
                         deferred = true;
                     }
                     // deferred list full: finish here without a budget
                 }
                 const bool can = active && !want_defer && nq < kPend;
-                if (__ballot(can) == 0ull) {
-                    if (tail == head) break;  // nothing queued and nobody can move: the tile is done
-                    run_rounds(tail);
-                    continue;
-                }
+                const bool any = __ballot(can) != 0ull;
+                if (!any && tail == head) break;  // nothing queued and nobody can move: the tile is done
                 if (STATS) {
                     const int nt = __popcll(__ballot(can));
-                    if (lane == 0) {
+                    if (lane == 0 && any) {
                         ++u_trav_it;
                         u_trav_lanes += nt;
                     }
@@ -770,7 +991,32 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     ++nq;
                 }
                 tail += (unsigned)(__popcll(m1) + __popcll(m2));
-                if (tail - head >= 64u) run_rounds(head + ((tail - head) & ~63u));
+                // full rounds while lanes can move; everything once nobody can
+                const unsigned upto = any ? head + ((tail - head) & ~63u) : tail;
+                if (upto != head) run_rounds(upto);
+            }
+            if (deferred) {
+                if ((a.phase == 1 || a.phase == 3 || a.phase == 4) && a.res) {
+                    // later phases take hints from this slot before pass 2 answers it: publish the closest point of
+                    // the best face so far (a point on the mesh), or NO_FACE when it has none yet
+                    D3 o = D3{NAN, NAN, NAN};
+                    uint32_t f = MSH_NO_FACE;
+                    if (pol.best_leaf >= 0) {
+                        D3 ta, tb, tc;
+                        int part;
+                        load_tri(static_cast<const TriRec*>(a.leaves), pol.best_leaf, ta, tb, tc, f);
+                        closest_on_triangle(q, ta, tb, tc, o, part);
+                    }
+                    store_qres(a.res + i, f, (uint32_t)pol.best_leaf, o.x, o.y, o.z);
+                }
+                DeferRec r;
+                r.slot = (uint32_t)i;
+                r.face = pol.best_face;
+                r.leaf = pol.best_leaf;
+                r.pad = 0;
+                r.best = pol.best;
+                r.pad2 = 0;
+                a.deferred[dslot] = r;
             }
             if (STATS) {  // per-tile step profile of this phase (stats[8 + 9 * phase slot ...])
                 unsigned mx = tot, sm = tot;
@@ -778,7 +1024,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
                     sm += (unsigned)__shfl_xor((int)sm, o);
                 }
-                unsigned long long* h = a.stats + 8 + 9 * (a.phase == 3 ? 0 : (a.phase == 1 ? 1 : 2));
+                unsigned long long* h = a.stats + 8 + 9 * (a.phase == 3 ? 0 : ((a.phase == 1 || a.phase == 4) ? 1 : 2));
                 if (lane == 0) {
                     atomicAdd(h + 0, 1ull);
                     atomicAdd(h + 1, (unsigned long long)mx);
@@ -917,7 +1163,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         if (slot < a.max_deferred) {
                             if (STATS) n_leaves += nq;
                             test_queue(kLeafQ);
-                            if ((a.phase == 1 || a.phase == 3) && a.res) {
+                            if ((a.phase == 1 || a.phase == 3 || a.phase == 4) && a.res) {
                                 // later phases take hints from this slot before pass 2 answers it: publish the
                                 // closest point of the best face so far (a point on the mesh, so a valid upper
                                 // bound for its neighbours), or NO_FACE when it has none yet
@@ -956,7 +1202,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     mx = max(mx, (unsigned)__shfl_xor((int)mx, o));
                     sm += (unsigned)__shfl_xor((int)sm, o);
                 }
-                unsigned long long* h = a.stats + 8 + 9 * (a.phase == 3 ? 0 : (a.phase == 1 ? 1 : 2));
+                unsigned long long* h = a.stats + 8 + 9 * (a.phase == 3 ? 0 : ((a.phase == 1 || a.phase == 4) ? 1 : 2));
                 if (lane == 0) {
                     atomicAdd(h + 0, 1ull);
                     atomicAdd(h + 1, (unsigned long long)mx);
@@ -1289,7 +1535,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     a.deferred = dbuf.as<DeferRec>();
     auto pass1 = [&](int phase, size_t nunits, const char* name) -> int {
         a.phase = phase;
-        a.budget = phase == 3 ? kBudget3 : (phase == 1 ? kBudget1 : kBudget);
+        a.budget = phase == 3 ? kBudget3 : ((phase == 1 || phase == 4) ? kBudget1 : kBudget);
         // small trees: a query that walks T/16 nodes (the centre of a coarse closed mesh) goes to the
         // wave-cooperative pass 2 instead of holding its tile for up to T serial steps (C1, 840 faces:
         // traversal 1.15 -> 0.56 ms; with no leader phases below, 0.29 ms)
@@ -1311,7 +1557,12 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         {
             TimedLaunch t1(STATS ? "knn_pass1_stats" : "knn_pass1", s);
             if (lead) {
-                if (kLead2 > 0) {
+                if (a.list && a.cut_hint) {
+                    // cell hints serve every leader inside the entry cut's grid, so the super-leaders would only
+                    // hint leaders outside it: one leader launch over every leader slot (phase 4; outside the
+                    // grid unhinted) instead of a super-leader launch the chip cannot fill
+                    MSH_TRY(pass1(4, n_lead, STATS ? "knn_lead_stats" : "knn_lead"));
+                } else if (kLead2 > 0) {
                     constexpr size_t l2 = kLead2 ? kLead2 : 1;
                     const size_t n_super = (a.S + l2 - 1) / l2;
                     MSH_TRY(pass1(3, n_super, STATS ? "knn_lead2_stats" : "knn_lead2"));

@@ -20,6 +20,51 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+def pmc_of(target, kernel, units):
+    """Measured fabric bytes of `kernel` in this config from profiles/pmc_configs.json (scripts/pmc_configs.py),
+    only when that profile was taken of the loaded library (same msh_build_id); `units` = rays or queries per
+    dispatch, to express them per unit.  None (with the reason) otherwise."""
+    from mesh_amd import _native
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_configs.json")) as fh:
+            prof = json.load(fh).get(target)
+    except (OSError, ValueError):
+        prof = None
+    if not prof:
+        return {"note": "no PMC profile of %s" % target}
+    if prof.get("build_id") != _native.build_id():
+        return {"note": "PMC profile of %s is of build %s, not of the loaded build %s" % (
+            target, prof.get("build_id"), _native.build_id())}
+    k = prof["kernels"].get(kernel)
+    if not k or not k.get("hbm_bytes_per_dispatch"):
+        return {"note": "kernel %s not in the PMC profile" % kernel}
+    return {"hbm_bytes_per_unit": k["hbm_bytes_per_dispatch"] / units, "hbm_GBps": k["hbm_GBps"],
+            "l2_hit_rate": k["l2_hit_rate"], "pmc_ms_per_dispatch": k["ms_per_dispatch"],
+            "build_id": prof["build_id"], "code": prof["code"],
+            "note": "bytes leaving L2 (Infinity Cache hits included; DRAM traffic is at most this), "
+                    "(2 FETCH_SIZE + WRITE_SIZE) KB per dispatch, gfx950 correction"}
+
+
+def pmc_traversal(target, S):
+    """Measured fabric bytes per query of the closest-point traversal (pass-1 launches + pass 2) in a config's
+    PMC profile: every dispatch's bytes over (traversals x S), the profile's traversals = pass-2 dispatches (the
+    entry cut's traversal dropped by pmc_configs.py --skip 1)."""
+    k1, k2 = "msh::k_knn<0, false, true>", "msh::k_knn_coop<0, false>"
+    a, b = pmc_of(target, k1, 1), pmc_of(target, k2, 1)
+    if "hbm_bytes_per_unit" not in a or "hbm_bytes_per_unit" not in b:
+        return a if "hbm_bytes_per_unit" not in a else b
+    with open(os.path.join(ROOT, "profiles", "pmc_configs.json")) as fh:
+        ks = json.load(fh)[target]["kernels"]
+    n_trav = ks[k2]["dispatches"]
+    tot = ks[k1]["hbm_bytes_total"] + ks[k2]["hbm_bytes_total"]
+    hit = [ks[k]["counters_per_dispatch"] for k in (k1, k2)]
+    h = sum(c.get("TCC_HIT_sum", 0.0) * ks[k]["dispatches"] for c, k in zip(hit, (k1, k2)))
+    m = sum(c.get("TCC_MISS_sum", 0.0) * ks[k]["dispatches"] for c, k in zip(hit, (k1, k2)))
+    return {"hbm_bytes_per_query": tot / (n_trav * S), "traversals": n_trav,
+            "l2_hit_rate": h / (h + m) if h + m > 0 else None, "build_id": a["build_id"], "code": a["code"],
+            "note": a["note"]}
+
+
 def timed(fn, reps):
     from mesh_amd import _native
     # warm-up (allocations, code objects): two calls, the second held like the loop's previous result, so
@@ -126,11 +171,12 @@ def c2(reps):
     part = torch.empty(S, dtype=torch.int32, device="cuda")
     pt = torch.empty((S, 3), dtype=torch.float64, device="cuda")
     wall_d = _device_timed(lambda: nearest_device(tree, dq, face, part, pt), reps)
-    c1t, cmt, th = cpu_rates(v, f, q)
+    c1t, cmt, th = cpu_rates(v, f, q) if os.environ.get("MESH_AMD_NO_CPU") != "1" else (None, None, None)
     return {"config": "C2 SMPL-topology stand-in (6,890 v / 13,776 f), 10M near-surface queries",
             "queries_per_s_device": S / wall_d, "ms_traversal_kernel": kernel_ms("nearest"),
             "queries_per_s_numpy_api": S / wall, "ms_numpy_api": wall * 1e3,
             "build_ms_gpu": tree.info().build_ms, "build_ms_wall": build_wall * 1e3,
+            "measured": pmc_traversal("c2", S),
             "cpu_ref_1t_qps": c1t, "cpu_ref_omp_qps": cmt, "cpu_threads": th}
 
 
@@ -265,11 +311,17 @@ def c5(reps):
             "alongnormal": {"rays_per_s_device": S / wall_r, "kernel_ms": k_r, "wall_ms_device": wall_r * 1e3,
                             "rays_per_s_numpy_api": S / wall_np, "nodes_per_ray": nn_r, "leaves_per_ray": nl_r,
                             "bytes_per_ray": b_r, "achieved_GBps": S * b_r / (k_r / 1e3) / 1e9,
-                            "frac_of_8TBps": S * b_r / (k_r / 1e3) / 8e12},
+                            "frac_of_8TBps": S * b_r / (k_r / 1e3) / 8e12,
+                            "frac_note": "byte model (SURVEY 8d): every node and leaf request priced at full size, "
+                                         "cache-served re-reads included",
+                            "measured": pmc_of("c5", "msh::k_rays<0, false>", S)},
             "visibility": {"rays_per_s_device": R / wall_v, "kernel_ms": k_v, "wall_ms_device": wall_v * 1e3,
                            "nodes_per_ray": nn_v, "leaves_per_ray": nl_v, "bytes_per_ray": b_v,
                            "achieved_GBps": R * b_v / (k_v / 1e3) / 1e9,
                            "frac_of_8TBps": R * b_v / (k_v / 1e3) / 8e12,
+                           "frac_note": "byte model (SURVEY 8d): above 1 because L2 and the Infinity Cache serve the "
+                                        "node re-reads (cache-served, not HBM); `measured` holds the fabric bytes",
+                           "measured": pmc_of("c5", "msh::k_rays<1, false>", R),
                            "visible_fraction": float(vis.double().mean().item())},
             "build_ms_gpu": info.build_ms, **cpu}
 

@@ -14,6 +14,8 @@ ok() {  # rc 0 = pass, 1 = test failures (no fault) -> continue; anything else -
 STAGES=${STAGES:-"smoke pytest bench prof"}
 for s in $STAGES; do
   case $s in
+    sortdbg) timeout -k 10 300 python scripts/sort_debug.py ${SORT_SIZES:-} > gpurun_out/sortdbg.log 2>&1; ok sortdbg $? ;;
+    pytest_rest) timeout -k 10 1200 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread ${DESELECT:-} > gpurun_out/pytest_gpu.log 2>&1; ok pytest_rest $? ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; ok smoke $? ;;
     pytest) timeout -k 10 1200 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; ok pytest $? ;;
     bench_small) timeout -k 10 600 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_small.log 2>&1; ok bench_small $? ;;
@@ -21,6 +23,11 @@ for s in $STAGES; do
       for so in build/variants/*.so; do
         n=$(basename $so .so)
         MESH_AMD_LIB=$PWD/$so timeout -k 10 300 python bench.py --queries ${VQ:-10000000} --steps ${VSTEPS:-5} --warmup 2 --no-cpu > gpurun_out/var_$n.log 2>&1; ok var_$n $?
+      done ;;
+    variants_check)  # closest-point parity tests through every build/variants/*.so (env MESH_AMD_LIB)
+      for so in build/variants/*.so; do
+        n=$(basename $so .so)
+        MESH_AMD_LIB=$PWD/$so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -k "c1 or c2 or non_finite or c3_sample or entry_cut or c3_stream_shards or c3_headline or tiny or degenerate or far_and or on_vertices or cooperative or deep_tree or tied or batch_bit or barycentric or device_api" > gpurun_out/varchk_$n.log 2>&1; ok varchk_$n $?
       done ;;
     variants_c5)  # the same sweep through the C5 ray workloads
       for so in build/variants/*.so; do

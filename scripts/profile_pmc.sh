@@ -2,15 +2,23 @@
 # rocprofv3 passes on the bench (C3 workload): kernel-trace --stats (CSV), then one PMC pass per counter
 # group (FETCH_SIZE / WRITE_SIZE / TCC_HIT_sum+TCC_MISS_sum cannot share a pass on gfx950).  Run on the
 # GPU box from the repo root; outputs under gpurun_out/pmc/.  Stops at the first failing step.
+# TARGET=c5 (or c2, c4 ...): the same passes over one scripts/bench_configs.py config instead, into
+# gpurun_out/pmc_<TARGET>/ (scripts/pmc_configs.py summarises them).
 set -u
 R=$(cd "$(dirname "$0")/.." && pwd)
+TARGET=${TARGET:-c3}
 OUT=$R/gpurun_out/pmc
+[ "$TARGET" = c3 ] || OUT=$R/gpurun_out/pmc_$TARGET
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 Q=${Q:-100000000}
 run() {
   local name=$1; shift
-  timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 "$R/bench.py" --queries $Q --steps 2 --warmup 1 --no-cpu > "$OUT/$name.log" 2>&1
+  if [ "$TARGET" = c3 ]; then
+    timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 "$R/bench.py" --queries $Q --steps 2 --warmup 1 --no-cpu > "$OUT/$name.log" 2>&1
+  else
+    MESH_AMD_NO_CPU=1 timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 "$R/scripts/bench_configs.py" --configs $TARGET --reps 1 > "$OUT/$name.log" 2>&1
+  fi
   local rc=$?
   echo "$name rc=$rc" | tee -a "$OUT/status.txt"
   [ $rc -eq 0 ] || exit $rc
