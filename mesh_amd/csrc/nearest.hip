@@ -523,13 +523,6 @@ __device__ inline unsigned lanes_below(unsigned long long m) {
 // (face << 32 | leaf) among the entries that reached it: the lexicographic (d2, face) rule.
 // kPend (C3, M q/s): 3: 1236, 4: 1346, 8: 1593, 16: 1677, 32: 1706, unbounded: 1689; per-lane queues 1541.
 constexpr int kPend = 32;
-#ifndef MSH_REFILL
-#define MSH_REFILL 0  // list path: persistent lanes that take new units as they finish (see k_knn)
-#endif
-#ifndef MSH_REFILL_LANES
-#define MSH_REFILL_LANES 32
-#endif
-[[maybe_unused]] constexpr int kRefill = MSH_REFILL_LANES;  // free lanes of a wave that trigger a refill
 
 constexpr unsigned kRing = 256;     // ring entries per wave: < 64 left after full rounds + <= 128 per step
 constexpr size_t kListMaxLeaves = (size_t)1 << 26;  // leaf index bits of a ring entry
@@ -598,232 +591,6 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     unsigned long long u_trav_it = 0, u_trav_lanes = 0, u_leaf_it = 0, u_leaf_lanes = 0;  // STATS: wave iterations
     unsigned n_nodes = 0, n_leaves = 0;
     unsigned n_impr = 0, n_hinted = 0, n_hint_won = 0;  // STATS: improving leaf tests, hinted queries, hint = answer
-#if MSH_REFILL
-    // Persistent lanes (list path): a lane whose query is finished takes the phase's next unit instead of idling
-    // until the slowest lane of its tile is done.  Finished lanes wait until kRefill lanes of the wave are free
-    // (or nobody can move); then, together, they store their answers, take the next units of the wave's current
-    // tile (Morton-adjacent slots, in lane order; a new tile from the XCD-group counters when it runs out), append
-    // their hint leaves to the ring, the wave evaluates everything pending, and the new queries start their walks
-    // from their cells' entries with the hint's bound.
-    bool refill_done = false;
-    if constexpr (kList) {
-      if (a.T > 1) {
-        refill_done = true;
-        uint32_t* ring = lsh + (tid >> 6) * (kRing + 64 * 4);
-        unsigned long long* bd = reinterpret_cast<unsigned long long*>(ring + kRing);  // per owner: d2 bits
-        unsigned long long* bfl = bd + 64;                                              // (face << 32 | leaf)
-        const unsigned max_steps = (unsigned)min(a.T, (size_t)UINT_MAX);
-        bool has = false;  // the lane holds a (finite) query: traversing, or finished and waiting to store it
-        unsigned i = 0;  // slot (S < 2^32)
-        auto pol = make_pol<MODE>(a, 0, D3{0.0, 0.0, 0.0});
-        QF qf = make_qf(pol.q, a.org, a.tm);
-        Walker w{0, 0};
-        bool active = false, want_defer = false, deferred = false;
-        int nq = 0;
-        unsigned last_pos = 0, steps = 0, tot = 0;
-        int hint_leaf = -1;  // STATS
-        unsigned head = 0, tail = 0;
-        unsigned tile = 0, cursor = 64;  // wave-uniform: current tile, units of it dealt so far
-        bool exhausted = false;
-        auto run_rounds = [&](unsigned upto) {
-            while (head != upto) {
-                const unsigned n = min(64u, upto - head);
-                bd[lane] = (unsigned long long)__double_as_longlong(pol.best);
-                bfl[lane] = ~0ull;
-                const bool valid = (unsigned)lane < n;
-                const uint32_t en = ring[(head + (valid ? (unsigned)lane : 0u)) & (kRing - 1)];
-                const int src = (int)(en & 63u);
-                const int leaf = (int)(en >> 6);
-                const D3 x = D3{__shfl(pol.q.x, src), __shfl(pol.q.y, src), __shfl(pol.q.z, src)};
-                uint32_t f;
-                const double d2 = pol.eval(leaf, x, f);
-                const unsigned long long kb = (unsigned long long)__double_as_longlong(d2);
-                asm volatile("" ::: "memory");
-                if (valid) atomicMin(&bd[src], kb);
-                asm volatile("" ::: "memory");
-                if (valid && bd[src] == kb) atomicMin(&bfl[src], ((unsigned long long)f << 32) | (unsigned)leaf);
-                asm volatile("" ::: "memory");
-                const unsigned long long nb = bd[lane], nf = bfl[lane];
-                const double nd = __longlong_as_double((long long)nb);
-                const uint32_t nface = (uint32_t)(nf >> 32);
-                if (nf != ~0ull && (nd < pol.best || (nd == pol.best && nface < pol.best_face))) {
-                    pol.best = nd;
-                    pol.best_face = nface;
-                    pol.best_leaf = (int)(uint32_t)nf;
-                    pol.relim();
-                    if (STATS) ++n_impr;
-                }
-                asm volatile("" ::: "memory");
-                if (STATS) {
-                    if (valid) ++n_leaves;
-                    if (lane == 0) {
-                        ++u_leaf_it;
-                        u_leaf_lanes += n;
-                    }
-                }
-                head += n;
-            }
-            if ((int)(last_pos - head) < 0) nq = 0;  // every entry of this lane is evaluated
-        };
-        // appends leaf l (>= 0) of this lane to the ring, in lane order; at most one per lane per call
-        auto append1 = [&](int l) {
-            const unsigned long long m = __ballot(l >= 0);
-            if (l >= 0) {
-                const unsigned pos = tail + lanes_below(m);
-                ring[pos & (kRing - 1)] = ((uint32_t)l << 6) | (uint32_t)lane;
-                last_pos = pos;
-                ++nq;
-            }
-            tail += (unsigned)__popcll(m);
-        };
-        for (;;) {
-            // a lane past its budget defers once its own leaves are evaluated (pass 2 then owns the query)
-            if (want_defer && nq == 0) {
-                want_defer = false;
-                const unsigned dslot = atomicAdd(a.n_deferred, 1u);
-                if (dslot < a.max_deferred) {
-                    DeferRec r;
-                    r.slot = i;
-                    r.face = pol.best_face;
-                    r.leaf = pol.best_leaf;
-                    r.pad = 0;
-                    r.best = pol.best;
-                    r.pad2 = 0;
-                    a.deferred[dslot] = r;
-                    active = false;
-                    deferred = true;
-                }
-                // deferred list full: finish here without a budget
-            }
-            const bool done = has && !active && nq == 0 && !want_defer;
-            const bool can = has && active && !want_defer && nq < kPend;
-            const unsigned long long mcan = __ballot(can);
-            const int n_free = __popcll(__ballot(!has || done));
-            if (n_free >= kRefill || (mcan == 0ull && tail == head)) {
-                // ---- refill: store the finished lanes' answers, deal new units to the free lanes ----
-                if (done) {
-                    if (deferred) {
-                        if ((a.phase == 1 || a.phase == 3 || a.phase == 4) && a.res) {
-                            // later phases take hints from this slot before pass 2 answers it: publish the closest
-                            // point of the best face so far (a point on the mesh), or NO_FACE when it has none yet
-                            D3 o = D3{NAN, NAN, NAN};
-                            uint32_t f = MSH_NO_FACE;
-                            if (pol.best_leaf >= 0) {
-                                D3 ta, tb, tc;
-                                int part;
-                                load_tri(static_cast<const TriRec*>(a.leaves), pol.best_leaf, ta, tb, tc, f);
-                                closest_on_triangle(pol.q, ta, tb, tc, o, part);
-                            }
-                            store_qres(a.res + i, f, (uint32_t)pol.best_leaf, o.x, o.y, o.z);
-                        }
-                    } else if (!STATS || a.res) {
-                        write_result<MODE>(a, i, pol.q, pol);
-                    }
-                    if (STATS) {
-                        if (hint_leaf >= 0 && pol.best_leaf == hint_leaf) ++n_hint_won;
-                        atomicAdd(a.stats + 8 + 9 * (a.phase == 3 ? 0 : ((a.phase == 1 || a.phase == 4) ? 1 : 2)) + 2,
-                                  (unsigned long long)tot);
-                    }
-                    has = false;
-                }
-                bool fresh = false;  // this lane took a unit in this refill
-                for (;;) {
-                    const unsigned long long idle = __ballot(!has && !fresh);
-                    if (idle == 0ull || exhausted) break;
-                    if (cursor >= 64u) {
-                        unsigned t = 0;
-                        if (lane == 0) t = dequeue_tile(a.counters, a.ntiles, group);
-                        t = __shfl(t, 0);
-                        if (t >= a.ntiles) {
-                            exhausted = true;
-                            break;
-                        }
-                        tile = t;
-                        cursor = 0;
-                    }
-                    const unsigned r = lanes_below(idle);
-                    const unsigned n_take = min((unsigned)__popcll(idle), 64u - cursor);
-                    if (!has && !fresh && r < n_take) {
-                        fresh = true;
-                        const size_t k = (size_t)tile * 64 + cursor + r;
-                        bool live = k < a.nunits;
-                        if (live) {
-                            const size_t si = slot_of(a, k);
-                            live = si < a.S;
-                            i = (unsigned)si;
-                        }
-                        if (live) {
-                            const D3 q = load_q(a, i);
-                            if (a.inv_w && !a.direct) a.inv_w[a.qperm[i]] = (uint32_t)i;
-                            pol = make_pol<MODE>(a, i, q);
-                            if (!finite3(q)) {  // no distance is defined: NO_FACE / NaN, no traversal
-                                if (!STATS || a.res) write_result<MODE>(a, i, q, pol);
-                            } else {
-                                has = true;
-                            }
-                        }
-                    }
-                    cursor += n_take;
-                }
-                const bool nw = fresh && has;  // a new query to start
-                if (__ballot(nw) != 0ull) {
-                    size_t cell = kNoCell;
-                    int lf = -1;
-                    if (nw) {
-                        const int root = query_root(a, i, pol.q, qf);
-                        w = Walker{root, 0};
-                        active = false;
-                        want_defer = false;
-                        deferred = false;
-                        steps = 0;
-                        if (STATS) tot = 0;
-                        cell = cut_cell(a, pol.q);
-                        if (a.cut_hint && cell != kNoCell && a.phase != 2) lf = a.cut_hint[cell];
-                        else if (a.phase == 2) lf = leader_leaf(a, i, pol.q, kFWin, kLead);
-                        else if (a.phase == 1) lf = leader_leaf(a, i, pol.q, kLWin * kLead2, kLead2);
-                        if (STATS) {
-                            hint_leaf = lf;
-                            if (lf >= 0) ++n_hinted;
-                        }
-                    }
-                    // the hints go through the ring with everything pending, so each walk starts with its bound
-                    append1(nw ? lf : -1);
-                    run_rounds(tail);
-                    if (nw) active = cell != kNoCell ? cut_start(a, cell, pol, w, lds, spill) : true;
-                }
-                if (__ballot(has) == 0ull && exhausted) break;
-                continue;
-            }
-            if (STATS) {
-                const int nt = __popcll(mcan);
-                if (lane == 0 && mcan) {
-                    ++u_trav_it;
-                    u_trav_lanes += nt;
-                }
-            }
-            int l0 = -1, l1 = -1;
-            if (can) {
-                active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, l0, l1, kPend - nq);
-                ++steps;
-                if (STATS) ++tot;
-                if (active && steps >= max_steps) active = false;  // each node is entered once: corrupt tree
-                if (active && steps == a.budget) want_defer = true;
-            }
-            // append this step's leaves (at most two per lane) to the ring, in lane order
-            if (l0 < 0) {
-                l0 = l1;
-                l1 = -1;
-            }
-            append1(l0);
-            append1(l1);
-            // full rounds while lanes can move; everything once nobody can
-            const unsigned upto = mcan ? head + ((tail - head) & ~63u) : tail;
-            if (upto != head) run_rounds(upto);
-        }
-      }
-    }
-    if (!refill_done)
-#endif
     for (;;) {
         unsigned tile = 0;
         if (lane == 0) tile = dequeue_tile(a.counters, a.ntiles, group);
@@ -890,7 +657,6 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             uint32_t* ring = lsh + (tid >> 6) * (kRing + 64 * 4);
             unsigned long long* bd = reinterpret_cast<unsigned long long*>(ring + kRing);  // per owner: d2 bits
             unsigned long long* bfl = bd + 64;                                              // (face << 32 | leaf)
-            const unsigned long long lt = (1ull << lane) - 1ull;
             bool active = start, want_defer = false, deferred = false;
             int nq = 0;              // this lane's leaves appended since all of them were last evaluated (a bound)
             unsigned last_pos = 0;   // ring counter of this lane's newest entry
@@ -979,7 +745,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     l1 = -1;
                 }
                 const unsigned long long m1 = __ballot(l0 >= 0), m2 = __ballot(l1 >= 0);
-                const unsigned pos = tail + (unsigned)(__popcll(m1 & lt) + __popcll(m2 & lt));
+                const unsigned pos = tail + lanes_below(m1) + lanes_below(m2);
                 if (l0 >= 0) {
                     ring[pos & (kRing - 1)] = ((uint32_t)l0 << 6) | (uint32_t)lane;
                     last_pos = pos;

@@ -14,6 +14,7 @@ ok() {  # rc 0 = pass, 1 = test failures (no fault) -> continue; anything else -
 STAGES=${STAGES:-"smoke pytest bench prof"}
 for s in $STAGES; do
   case $s in
+    sorttest) timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -k one_sweep > gpurun_out/sorttest.log 2>&1; ok sorttest $? ;;
     sortdbg) timeout -k 10 300 python scripts/sort_debug.py ${SORT_SIZES:-} > gpurun_out/sortdbg.log 2>&1; ok sortdbg $? ;;
     pytest_rest) timeout -k 10 1200 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread ${DESELECT:-} > gpurun_out/pytest_gpu.log 2>&1; ok pytest_rest $? ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; ok smoke $? ;;
@@ -22,7 +23,7 @@ for s in $STAGES; do
     variants)  # tuning sweep: every build/variants/*.so through the 10M-query bench (env MESH_AMD_LIB)
       for so in build/variants/*.so; do
         n=$(basename $so .so)
-        MESH_AMD_LIB=$PWD/$so timeout -k 10 300 python bench.py --queries ${VQ:-10000000} --steps ${VSTEPS:-5} --warmup 2 --no-cpu > gpurun_out/var_$n.log 2>&1; ok var_$n $?
+        MESH_AMD_LIB=$PWD/$so timeout -k 10 ${VTIMEOUT:-300} python bench.py --queries ${VQ:-10000000} --steps ${VSTEPS:-5} --warmup 2 --no-cpu > gpurun_out/var_$n.log 2>&1; ok var_$n $?
       done ;;
     variants_check)  # closest-point parity tests through every build/variants/*.so (env MESH_AMD_LIB)
       for so in build/variants/*.so; do
@@ -40,6 +41,8 @@ for s in $STAGES; do
     c5)     timeout -k 10 900 python scripts/bench_configs.py --configs c5 --reps 3 > gpurun_out/bench_c5.log 2>&1; ok c5 $? ;;
     configs) timeout -k 10 900 python scripts/bench_configs.py > gpurun_out/bench_configs.log 2>&1; ok configs $? ;;
     bench)  timeout -k 10 900 python bench.py > gpurun_out/bench.log 2>&1; ok bench $? ;;
+    pmc)    PASSES="${PMC_PASSES:-stats fetch write tcc sq valu valu2 sq2}" TARGET=${PMC_TARGET:-c3} bash scripts/profile_pmc.sh > gpurun_out/pmc_${PMC_TARGET:-c3}.log 2>&1; ok pmc_${PMC_TARGET:-c3} $? ;;
+    pmc_cfg) for t in ${PMC_CFGS:-c5 c2}; do PASSES="stats fetch write tcc" TARGET=$t bash scripts/profile_pmc.sh > gpurun_out/pmc_$t.log 2>&1; ok pmc_$t $?; done ;;
     repl)   timeout -k 10 300 python scripts/replication_timing.py > gpurun_out/repl.log 2>&1; ok repl $? ;;
     bench_stats) MESH_AMD_STATS_DUMP=1 timeout -k 10 600 python bench.py --steps 2 --warmup 1 --no-cpu > gpurun_out/bench_stats.log 2>&1; ok bench_stats $? ;;
     prof_small) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof_small" -o run -- python3 "$OLDPWD/bench.py" --queries 10000000 --steps 2 --warmup 1 --no-cpu > "$OLDPWD/gpurun_out/prof_small.log" 2>&1); ok prof_small $? ;;

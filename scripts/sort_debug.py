@@ -18,7 +18,7 @@ def keys24(q, lo, hi):
     for k in range(3):
         e = f(hi[k]) - f(lo[k])
         n = (q[:, k].astype(f) - f(lo[k])) / e
-        n = np.minimum(np.maximum(n * f(1024.0), f(0.0)), f(1023.0)).astype(np.uint32)
+        n = np.fmin(np.fmax(n * f(1024.0), f(0.0)), f(1023.0)).astype(np.uint32)  # C fminf / fmaxf: NaN -> 0
         v = n.copy()
         v = (v * np.uint32(0x00010001)) & np.uint32(0xFF0000FF)
         v = (v * np.uint32(0x00000101)) & np.uint32(0x0F00F00F)
