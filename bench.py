@@ -12,7 +12,9 @@ timed region).  `value` = 100M x steps / max-over-ranks wall time (strong scalin
 `value_without_allgather` (the same steps without the exchange) and `value_weak_100M_per_gpu` (every rank
 answers the whole 100M stream and the N x 100M answers are all-gathered: the round-3 weak-scaling line).
 The BVH build is setup (reported as build_ms); for N > 1 it is built on rank 0 and replicated with one RCCL
-broadcast.  The entry cut is built by the first (warm-up) query, its time reported as entry_cut_ms.
+broadcast.  For N > 1 (or --secondary on) two more lines ride along, beside `value` and never as it:
+`c5_visibility_sharded` (BASELINE configs[4]: 160M visibility rays per step, vertex ranges sharded) and
+`c4_batch_sharded` (configs[3]: 4096 meshes x 10k scan points per step, mesh ranges sharded), see secondary().  The entry cut is built by the first (warm-up) query, its time reported as entry_cut_ms.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--queries Q]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
@@ -51,6 +53,9 @@ def parse():
     ap.add_argument("--cpu-queries", type=int, default=24000,
                     help="CPU baseline: fixed sample of queries per host thread (1 thread: ~12 s)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--secondary", choices=("auto", "on", "off"), default="auto",
+                    help="C5 visibility and C4 batch lines beside value (auto: when N > 1, the configs north_star "
+                         "shards across GPUs)")
     return ap.parse_args()
 
 
@@ -104,6 +109,64 @@ def cpu_baseline(v, f, per_thread):
                           % (n, 2000 * threads, lo, hi, label, build_s)}
     return (obj("1", "1 thread (the reference's aabbtree_nearest loop is serial, spatialsearchmodule.cpp:212-217)"),
             obj("all", "OpenMP over queries on %d host threads" % out["all"][2]))
+
+
+def secondary(timed, world, rank, dev, steps):
+    """BASELINE configs[4] and [3] through their multi-GPU splits (north_star: C5 rays sharded across the GPUs,
+    C4 meshes split by range), reported beside `value`, never as it.  Each is timed like the headline (barrier +
+    sync around K steps, max over ranks), after one untimed step:
+      * C5 visibility: 64 Fibonacci cameras x the 2.5M vertices of the 5M-face bumped icosphere (160M rays); the
+        tree is built on rank 0 and replicated by RCCL broadcast; every rank casts its vertex range for all
+        cameras (visibility_device), and `with_gather` adds the all-gather that assembles the (C, P) outputs on
+        every rank (visibility_sharded; reference loop visibility.cpp:136-173);
+      * C4: 4096 meshes of one topology x 10k scan points; every rank generates only its mesh range, builds its
+        batched tree and answers (batched build + query through the numpy API, then the mesh-slab all-gather:
+        batch_nearest_sharded; the reference builds one AabbTree per mesh, spatialsearchmodule.cpp:272-321)."""
+    import torch
+    from mesh_amd import spatialsearch
+    from mesh_amd.distributed import (batch_nearest_sharded, replicate_tree, shard_range, visibility_device,
+                                      visibility_sharded)
+    from mesh_amd.mesh import Mesh
+    import workloads as W
+    out = {}
+    v5, f5 = W.c5_mesh()
+    t5 = spatialsearch.aabbtree_compute(v5, f5) if rank == 0 else None
+    if world > 1:
+        t5 = replicate_tree(t5, src=0)
+    vn = torch.from_numpy(Mesh(v=v5, f=f5).estimate_vertex_normals()).to(dev)
+    cams = torch.from_numpy(W.fibonacci_cameras(64, 3.0)).to(dev)
+    P, C = v5.shape[0], 64
+    a0, a1 = shard_range(P, rank, world)
+    vis = torch.empty((C, a1 - a0), dtype=torch.int32, device=dev)
+    ndc = torch.empty((C, a1 - a0), dtype=torch.float64, device=dev)
+    local = lambda: visibility_device(t5, cams, vis, ndc, vn, None, 1e-3, a0, a1 - a0)  # noqa: E731
+    gathered = lambda: visibility_sharded(t5, cams, vn)  # noqa: E731
+    local()
+    gathered()
+    el_l = timed(local, steps)
+    el_g = timed(gathered, steps)
+    out["c5_visibility_sharded"] = {
+        "workload": "C5: bumped icosphere (5,000,000 faces / 2,500,002 v), visibility of every vertex from 64 "
+                    "Fibonacci cameras (160M rays) per step, vertex ranges sharded over the GPUs",
+        "rays_per_s": C * P * steps / el_l, "ms_per_step": el_l / steps * 1e3,
+        "rays_per_s_with_gather": C * P * steps / el_g, "ms_per_step_with_gather": el_g / steps * 1e3,
+        "rays_per_gpu": C * (a1 - a0)}
+    del t5, vn, vis, ndc, v5, f5
+    torch.cuda.empty_cache()
+    B, S = 4096, 10_000
+    b0, b1 = shard_range(B, rank, world)
+    t0 = time.perf_counter()
+    v4, f4, q4 = W.c4_batch_range(b0, b1, B, S)
+    gen_s = time.perf_counter() - t0
+    step4 = lambda: batch_nearest_sharded(v4, f4, q4, device=dev)  # noqa: E731
+    step4()
+    el4 = timed(step4, steps)
+    out["c4_batch_sharded"] = {
+        "workload": "C4: 4096 meshes (5,042 v / 10,080 f, one topology) x 10k scan points per step, mesh ranges "
+                    "sharded over the GPUs: batched build + query (numpy API) + mesh-slab all-gather",
+        "queries_per_s": B * S * steps / el4, "ms_per_step": el4 / steps * 1e3, "meshes_per_gpu": b1 - b0,
+        "input_generation_s": gen_s}
+    return out
 
 
 def load_traffic(workload, S, build_id):
@@ -253,6 +316,10 @@ def main():
             del wring, wslabs, wg
             torch.cuda.empty_cache()
 
+    sec = None
+    if args.secondary == "on" or (args.secondary == "auto" and world > 1):
+        sec = secondary(timed, world, rank, dev, args.steps)
+
     # ---- instrumented traversal (untimed): algorithmic bytes of this rank's shard ----
     nodes, leaves = _native.ctypes.c_uint64(0), _native.ctypes.c_uint64(0)
     _native.check(_native.lib().msh_tree_nearest_stats(tree.ptr, q.data_ptr(), S_loc, _native.ctypes.byref(nodes),
@@ -334,6 +401,8 @@ def main():
     if elapsed_weak is not None:
         out["value_weak_100M_per_gpu"] = world * S * args.steps / elapsed_weak
         out["ms_per_step_weak"] = elapsed_weak / args.steps * 1e3
+    if sec:
+        out.update(sec)
     if world == 1 and not args.no_cpu:
         out["cpu_baseline"], out["cpu_baseline_allcores"] = cpu_baseline(v, f, args.cpu_queries)
     print(json.dumps(out), flush=True)

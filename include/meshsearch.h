@@ -113,10 +113,10 @@ int msh_tree_nearest_bary_device(msh_tree* tree, const double* d_q, size_t S, ui
                                  double* d_w, void* stream);
 
 /* The order in which the closest-point path visits the S query rows (d_perm[slot] = row): stable by the top
- * 24 bits of their 30-bit Morton codes in the tree's scene box widened by 10 %.  sorter 0 = the path's own
- * sort (one-sweep, decoupled look-back, for calls of < 2^30 rows), 1 = the 3-launch-per-pass radix sort it
- * replaced (and that larger calls use); both give the same permutation.  Asynchronous on `stream`. */
-int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_perm, int sorter, void* stream);
+ * 24 bits of their 30-bit Morton codes in the tree's scene box widened by 10 % (query Morton codes + the LDS radix
+ * sort, 3 passes of 8 bits).  No reference counterpart (test and diagnostic entry point).  Asynchronous on
+ * `stream`. */
+int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_perm, void* stream);
 
 /* Entry cut of a triangle tree (no reference counterpart: derived acceleration data).  A grid
  * of G^3 cells over the scene box widened by 1/4, 68 B per cell (8 start entries + a hint leaf), from which

@@ -404,8 +404,6 @@ static const size_t kSortMin = 4096;  // below this the query Morton sort costs 
 // C3's 100M queries put ~6 in a cell, and the traversal runs the same node counts as with the full code
 // (sort 3.44 -> 3.08 ms, traversal unchanged).  The order within a cell is the caller's (stable sort).
 constexpr int kQuerySortLo = 6;
-// calls of up to 2^30 - 1 queries take the one-sweep sort (query_sort); larger ones the 3-launch-per-pass radix sort
-constexpr size_t kOneSweepMax = ((size_t)1 << 30) - 1;
 static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_t S, hipStream_t s,
                         QueryOrder* ord, bool allow_lazy = false) {
     *ord = QueryOrder{d_q, d_n, nullptr, nullptr};
@@ -417,14 +415,9 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
     MSH_TRY(ws.vals_alt.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.inv.reserve(S * sizeof(uint32_t)));
     bool in_alt = false;
-    if (S <= kOneSweepMax) {
-        MSH_TRY(query_order(t, d_q, S, kQuerySortLo, ws.keys.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
-                            ws.vals.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), ws, s, &in_alt));
-    } else {
-        MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
-        MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
-                                 ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
-    }
+    MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
+    MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
+                             ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
     if (in_alt) {  // odd pass count: the sorted pairs are in the alt buffers; swap roles instead of copying
         std::swap(ws.keys, ws.keys_alt);
         std::swap(ws.vals, ws.vals_alt);
@@ -745,6 +738,40 @@ static PinnedPool& pinned_pool() {
     return *p;
 }
 
+// Row ranges (first row, rows) of the staged pipeline's chunks, none longer than `chunk`.  With ramp, the first
+// and the last chunks grow and shrink geometrically (chunk/8, chunk/4, chunk/2 ...): the GPU starts after a small
+// first upload instead of a full chunk's host copy and upload, and the call ends a small chunk's kernels and
+// download after the previous one instead of a full one's; the middle rows go in equal chunks of at most `chunk`.
+static std::vector<std::pair<size_t, size_t>> chunk_plan(size_t S, size_t chunk, bool ramp) {
+    std::vector<std::pair<size_t, size_t>> plan;
+    std::vector<size_t> up;
+    if (ramp)
+        for (size_t c = chunk / 8; c >= ((size_t)1 << 20) && c < chunk; c *= 2) up.push_back(c);
+    size_t ends = 0;
+    for (size_t c : up) ends += 2 * c;
+    while (!up.empty() && ends + chunk / 2 > S) {  // too few rows for the ramps: drop their largest steps
+        ends -= 2 * up.back();
+        up.pop_back();
+    }
+    size_t r = 0;
+    for (size_t c : up) {
+        plan.push_back({r, c});
+        r += c;
+    }
+    const size_t mid = S - ends;
+    const size_t nmid = (mid + chunk - 1) / chunk;
+    for (size_t k = 0; k < nmid; ++k) {
+        const size_t n = mid / nmid + (k < mid % nmid ? 1 : 0);
+        plan.push_back({r, n});
+        r += n;
+    }
+    for (size_t j = up.size(); j-- > 0;) {
+        plan.push_back({r, up[j]});
+        r += up[j];
+    }
+    return plan;
+}
+
 // pipelined() over caller arrays that are page-locked in place: per chunk an H2D copy of the input rows into a
 // device slab (copy stream `up`), the kernels (handle stream), a D2H copy of the output rows straight into
 // the caller's arrays (stream `down`); two device slabs alternate, so chunk k uploads while k - 1 computes and
@@ -844,7 +871,9 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
         }
         return st;
     }
-    const size_t nch = (S + chunk - 1) / chunk;
+    const char* re = getenv("MESH_AMD_HOST_RAMP");  // A/B switch (measurement)
+    const std::vector<std::pair<size_t, size_t>> plan = chunk_plan(S, chunk, re && atoi(re) != 0);
+    const size_t nch = plan.size();
     // Optionally (host_register_enabled) page-lock the caller's arrays in place (hipHostRegister): the copy
     // engines then move the rows straight between the caller's memory and HBM, with no pageable <-> pinned
     // staging copies on the host.  Any registration failure falls back to staging.
@@ -882,7 +911,7 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
     //   chunk k's upload (copy stream), kernels (handle stream) and download (second copy stream).
     auto outs_of = [&](size_t kk, std::vector<CopyTask>& tasks) {
         const int b = (int)(kk & 1);
-        const size_t r0 = kk * chunk, n = std::min(chunk, S - r0);
+        const size_t r0 = plan[kk].first, n = plan[kk].second;
         size_t off = 0;
         for (const HostArr& a : arrs) {
             if (a.out)
@@ -905,7 +934,7 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
                 }
             }
             const bool have = k < nch;
-            const size_t r0 = k * chunk, n = have ? std::min(chunk, S - r0) : 0;
+            const size_t r0 = have ? plan[k].first : 0, n = have ? plan[k].second : 0;
             if (have) {
                 size_t off = 0;
                 for (const HostArr& a : arrs) {
@@ -1099,10 +1128,9 @@ int msh_points_build(const double* v, size_t P, msh_tree** out) {
 
 void msh_tree_free(msh_tree* tree) { free_tree(tree); }
 
-int msh_tree_query_order(msh_tree* t, const double* d_q, size_t S, uint32_t* d_perm, int sorter, void* stream) {
+int msh_tree_query_order(msh_tree* t, const double* d_q, size_t S, uint32_t* d_perm, void* stream) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_query_order"));
     MSH_TRY(check_count(S, "msh_tree_query_order"));
-    if (sorter != 0 && sorter != 1) { set_error("msh_tree_query_order: sorter %d (0 or 1)", sorter); return MSH_EINVAL; }
     if (S == 0) return MSH_OK;
     if (!d_q || !d_perm) { set_error("msh_tree_query_order: null argument"); return MSH_EINVAL; }
     hipStream_t s = pick(t, stream);
@@ -1113,14 +1141,9 @@ int msh_tree_query_order(msh_tree* t, const double* d_q, size_t S, uint32_t* d_p
     MSH_TRY(ws.keys_alt.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.vals_alt.reserve(S * sizeof(uint32_t)));
     bool in_alt = false;
-    if (sorter == 0 && S <= kOneSweepMax) {
-        MSH_TRY(query_order(t, d_q, S, kQuerySortLo, ws.keys.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
-                            ws.vals.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), ws, s, &in_alt));
-    } else {
-        MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
-        MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
-                                 ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
-    }
+    MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
+    MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
+                             ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
     MSH_HIP(hipMemcpyAsync(d_perm, in_alt ? ws.vals_alt.ptr : ws.vals.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     return MSH_OK;
 }

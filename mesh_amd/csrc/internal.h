@@ -139,11 +139,6 @@ namespace msh {
 // passes, in keys_alt/vals_alt (*in_alt = true) without the copy back.  lo_bit: first key bit sorted.
 int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, size_t n, int bits,
                      Workspace& ws, hipStream_t s, int lo_bit = 0, bool* in_alt = nullptr);
-// Query order of the closest-point path: the permutation that sorts the (n,3) query rows by bits
-// [lo_bit, lo_bit + 24) of their 30-bit Morton codes in the box [lo, hi], stably (one-sweep, 3 passes; n < 2^30).
-// keys/keys_alt: n scratch words each; the permutation ends in perm_alt (*in_alt = true) — perm is scratch.
-int query_sort(const double* d_q, size_t n, const float* lo, const float* hi, int lo_bit, uint32_t* keys,
-               uint32_t* keys_alt, uint32_t* perm, uint32_t* perm_alt, Workspace& ws, hipStream_t s, bool* in_alt);
 // exclusive scan of u32 (in place), n elements
 int exclusive_scan_u32(uint32_t* data, size_t n, Workspace& ws, hipStream_t s);
 
@@ -182,9 +177,6 @@ int point_bounds(const double* d_v, size_t P, double* d_lo, double* d_hi, hipStr
 // ---- queries (nearest.hip) ----
 // 30-bit Morton codes of query points in the tree's scene box + iota values.
 int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* keys, uint32_t* vals, hipStream_t s);
-// query_sort over the cells of query_morton (the tree's scene box widened by 10 % per side)
-int query_order(const msh_tree* tree, const double* d_q, size_t S, int lo_bit, uint32_t* keys, uint32_t* keys_alt,
-                uint32_t* perm, uint32_t* perm_alt, Workspace& ws, hipStream_t s, bool* in_alt);
 // slot i <- rows perm[i] of a (and b when non-null); inv[perm[i]] = i
 int gather_rows(const double* d_a, const double* d_b, const uint32_t* d_perm, size_t S, double* d_as, double* d_bs,
                 uint32_t* d_inv, hipStream_t s);

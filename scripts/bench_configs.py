@@ -246,6 +246,30 @@ def c4(reps):
             "cpu_note": "median over 8 sampled meshes of one CGAL-restatement tree each; tree builds excluded"}
 
 
+def facade(reps):
+    """Mesh.closest_faces_and_points end to end (the reference builds one AabbTree per call, mesh.py:454-455):
+    build + query through the numpy API, on C2 (10M near-surface queries) and C3 (100M uniform queries).  The
+    facade's tree goes without the entry cut (one batch does not pay for it); the same call on a tree that
+    builds its cut on the first query is timed beside it."""
+    from mesh_amd.mesh import Mesh
+    from mesh_amd import search
+    import workloads as W
+    out = {"config": "Mesh.closest_faces_and_points end to end (tree build + entry cut policy + query, numpy API)"}
+    for name, (v, f), q in (("c2", W.c2_mesh(), W.c2_queries()),
+                            ("c3", W.c3_mesh(), np.random.default_rng(3).uniform(-1.1, 1.1, (100_000_000, 3)))):
+        m = Mesh(v=v, f=f)
+        _, wall = timed(lambda: m.closest_faces_and_points(q), reps)
+
+        def with_cut():
+            t = search.AabbTree(m)
+            r = t.nearest(q)
+            return r, t.cpp_handle.entry_cut_info()["build_ms"], t.cpp_handle.info().build_ms
+        (_, cut_ms, build_ms), wall_cut = timed(with_cut, reps)
+        out[name] = {"queries": q.shape[0], "ms_facade": wall * 1e3, "queries_per_s_facade": q.shape[0] / wall,
+                     "ms_with_entry_cut": wall_cut * 1e3, "entry_cut_build_ms": cut_ms, "tree_build_ms_gpu": build_ms}
+    return out
+
+
 def _device_timed(fn, reps):
     import torch
     from mesh_amd import _native
@@ -357,7 +381,7 @@ def main():
     args = ap.parse_args()
     from mesh_amd import _native
     _native.set_device(0)
-    fns = {"c1": c1, "c2": c2, "c3np": c3np, "c4": c4, "c5": c5}
+    fns = {"c1": c1, "c2": c2, "c3np": c3np, "c4": c4, "c5": c5, "facade": facade}
     for name in args.configs.split(","):
         r = fns[name](args.reps)
         r["name"] = name

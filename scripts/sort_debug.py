@@ -1,7 +1,8 @@
-"""Development check of the query order (msh_tree_query_order): both sorters against a numpy stable argsort of
-the same 24-bit Morton keys (computed here with the kernels' fp32 arithmetic), on C3-stream prefixes.
+"""The closest-point path's query order (msh_tree_query_order) against numpy's stable argsort of the same 24-bit
+Morton keys, computed here with the kernel's fp32 arithmetic (k_query_morton / common.h query_morton30), on prefixes
+of the C3 stream.  tests/test_gpu_parity.py uses keys24 and sort_box.
 
-    python scripts/sort_debug.py
+    python scripts/sort_debug.py [n1,n2,...]
 """
 import os
 import sys
@@ -28,39 +29,34 @@ def keys24(q, lo, hi):
     return (out >> np.uint32(6)) & np.uint32(0xFFFFFF)
 
 
+def sort_box(info):
+    """The cells of query_morton: the tree's scene box widened by 10 % of its extent per side, in fp32."""
+    lo, hi = [], []
+    for k in range(3):
+        e = np.float32(info.scene_hi[k]) - np.float32(info.scene_lo[k])
+        lo.append(np.float32(info.scene_lo[k]) - np.float32(0.1) * e)
+        hi.append(np.float32(info.scene_hi[k]) + np.float32(0.1) * e)
+    return lo, hi
+
+
 def main():
     import torch
     from mesh_amd import _native, spatialsearch
     import workloads as W
     v, f = W.c3_mesh()
     t = spatialsearch.aabbtree_compute(v, f)
-    info = t.info()
-    lo, hi = [], []
-    for k in range(3):
-        e = np.float32(info.scene_hi[k]) - np.float32(info.scene_lo[k])
-        lo.append(np.float32(info.scene_lo[k]) - np.float32(0.1) * e)
-        hi.append(np.float32(info.scene_hi[k]) + np.float32(0.1) * e)
+    lo, hi = sort_box(t.info())
     sizes = [int(x) for x in (sys.argv[1].split(",") if len(sys.argv) > 1 else
                               ["1000", "4096", "4097", "12345", "100000", "1000000", "4000000"])]
     qa = W.c3_stream(max(sizes), "cuda:0")
     for n in sizes:
         x = qa[:n].contiguous()
-        perms = []
-        for sorter in (0, 1):
-            p = torch.empty(n, dtype=torch.int32, device="cuda:0")
-            _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), n, p.data_ptr(), sorter, None))
-            torch.cuda.synchronize()
-            perms.append(p.cpu().numpy().astype(np.int64))
-        kk = keys24(x.cpu().numpy(), lo, hi)
-        ref = np.argsort(kk, kind="stable")
-        res = []
-        for s, p in enumerate(perms):
-            ok = np.array_equal(p, ref)
-            isperm = np.array_equal(np.sort(p), np.arange(n))
-            sorted_keys = bool(np.all(np.diff(kk[p].astype(np.int64)) >= 0)) if isperm else False
-            first = int(np.argmax(p != ref)) if not ok else -1
-            res.append(dict(sorter=s, equal_ref=ok, is_perm=isperm, keys_sorted=sorted_keys, first_diff=first))
-        print(n, res, flush=True)
+        p = torch.empty(n, dtype=torch.int32, device="cuda:0")
+        _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), n, p.data_ptr(), None))
+        torch.cuda.synchronize()
+        p = p.cpu().numpy().astype(np.int64)
+        ref = np.argsort(keys24(x.cpu().numpy(), lo, hi), kind="stable")
+        print(n, "equal to the stable argsort:", bool(np.array_equal(p, ref)), flush=True)
 
 
 if __name__ == "__main__":

@@ -276,37 +276,26 @@ def test_c3_replication_roundtrip():
         assert torch.equal(x, y)
 
 
-def test_query_order_one_sweep_equals_radix():
-    # the one-sweep query sort gives the permutation of the 3-launch radix sort it replaced, and both equal numpy's
-    # stable argsort of the same 24-bit Morton keys (scripts/sort_debug.keys24, the kernels' fp32 arithmetic): on the
-    # C3 stream (100M rows: 24,415 tiles of look-back), a ragged size, a size below one tile and rows with NaN / inf.
-    # The two sorts run back to back on the tree's stream (no host synchronisation between them).
+def test_query_order_equals_stable_argsort():
+    # the closest-point path's query order (msh_tree_query_order: Morton codes + the 3-pass LDS radix sort) equals
+    # numpy's stable argsort of the same 24-bit Morton keys (scripts/sort_debug.keys24, the kernel's fp32
+    # arithmetic): on the C3 stream (100M rows), a ragged size, a size below one tile and rows with NaN / inf
     import torch
     from mesh_amd import _native, spatialsearch
-    from scripts.sort_debug import keys24
+    from scripts.sort_debug import keys24, sort_box
     v, f = W.c3_mesh()
     t = spatialsearch.aabbtree_compute(v, f)
-    info = t.info()
-    lo = [np.float32(info.scene_lo[k]) - np.float32(0.1) * (np.float32(info.scene_hi[k]) - np.float32(info.scene_lo[k]))
-          for k in range(3)]
-    hi = [np.float32(info.scene_hi[k]) + np.float32(0.1) * (np.float32(info.scene_hi[k]) - np.float32(info.scene_lo[k]))
-          for k in range(3)]
+    lo, hi = sort_box(t.info())
     q = W.c3_stream(100_000_000, "cuda:0")
     bad = W.c3_stream(50_000, "cuda:0", seed=7)
     bad[::7, 0] = float("nan")
     bad[3::11, 2] = float("inf")
     for x in (q, q[:12_345_677], q[:1000], bad):
-        perms = []
-        for sorter in (0, 1):
-            p = torch.empty(x.shape[0], dtype=torch.int32, device="cuda:0")
-            _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), x.shape[0], p.data_ptr(), sorter,
-                                                             None))
-            perms.append(p)
+        p = torch.empty(x.shape[0], dtype=torch.int32, device="cuda:0")
+        _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), x.shape[0], p.data_ptr(), None))
         torch.cuda.synchronize()
-        ps = [p.cpu().numpy().astype(np.int64) for p in perms]
         ref = np.argsort(keys24(x.cpu().numpy(), lo, hi), kind="stable")
-        ok = [bool(np.array_equal(p, ref)) for p in ps]
-        assert ok == [True, True], "rows %d: one-sweep == reference %s, radix == reference %s" % (x.shape[0], *ok)
+        assert np.array_equal(p.cpu().numpy().astype(np.int64), ref), "rows %d" % x.shape[0]
 
 
 def test_c3_stream_shards_equal_whole():

@@ -197,6 +197,20 @@ def c4_batch(B=4096, S=10_000, seed=4):
     return v, f, q
 
 
+def c4_batch_range(lo, hi, B=4096, S=10_000, seed=4):
+    """Meshes [lo, hi) of c4_batch(B, S, seed), each identical to its row there, inside full-size (B, ...) arrays
+    whose other rows are left unset: a rank of C4's mesh-range split generates only its own meshes."""
+    f = c4_mesh(0)[1]
+    P = c4_mesh(0)[0].shape[0]
+    v = np.empty((B, P, 3))
+    q = np.empty((B, S, 3))
+    for i in range(lo, hi):
+        v[i] = c4_mesh(i)[0]
+        diag = float(np.linalg.norm(v[i].max(0) - v[i].min(0)))
+        q[i] = surface_samples(v[i], f, S, seed=seed * 100003 + i, sigma=0.005 * diag)[0]
+    return v, f, q
+
+
 def fibonacci_cameras(C=64, radius=3.0):
     """C5 cameras: C points of a Fibonacci sphere of the given radius."""
     k = np.arange(C) + 0.5
