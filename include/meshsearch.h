@@ -268,7 +268,8 @@ int msh_timing_reset(void);
  *    cap (MESH_AMD_PINNED_POOL_MB, default 16384; 0 disables the pool) even after releasing its free
  *    blocks: the caller then allocates ordinary pageable arrays.
  *  - msh_host_free: returns a block (any pointer msh_host_alloc gave) to the pool; NULL is ignored.
- *  - msh_host_pool_trim: releases every free block; msh_host_pool_bytes: bytes held (live + free).
+ *  - msh_host_pool_trim: releases every free block, and the idle staging slabs the host-array entry points
+ *    share between handles; msh_host_pool_bytes: bytes held (live + free).
  * Host-buffer entry points recognise output arrays that lie inside one live block. */
 int msh_host_alloc(size_t bytes, void** out);
 void msh_host_free(void* p);

@@ -610,10 +610,108 @@ static void release_stage(msh_tree* t, bool host, bool dev) {
 }
 static void release_stage(msh_tree* t) { release_stage(t, true, true); }
 
+// Staging slabs shared by the handles of a device: a pipelined call leases one set (two pinned host slabs and two
+// device slabs) into its handle and hands it back when it returns, so a caller that builds a tree per call (the
+// reference's Mesh.closest_faces_and_points, mesh.py:454-455) pays the page-locking of ~1.5 GB of host slabs
+// once per process instead of once per tree.  At most kStageKeep idle sets are kept per device.
+struct StageSet {
+    void* h[2] = {nullptr, nullptr};
+    void* d[2] = {nullptr, nullptr};
+    size_t hbytes = 0, dbytes = 0;
+};
+class StagePool {
+  public:
+    StageSet take(int dev) {
+        std::lock_guard<std::mutex> g(mu_);
+        std::vector<StageSet>& v = idle_[dev];
+        if (v.empty()) return StageSet{};
+        StageSet s = v.back();
+        v.pop_back();
+        return s;
+    }
+    void give(int dev, const StageSet& s) {
+        constexpr size_t kStageKeep = 2;
+        std::lock_guard<std::mutex> g(mu_);
+        std::vector<StageSet>& v = idle_[dev];
+        if (v.size() < kStageKeep) {
+            v.push_back(s);
+            return;
+        }
+        for (int b = 0; b < 2; ++b) {  // an extra set (concurrent calls): freed
+            if (s.h[b]) (void)hipHostFree(s.h[b]);
+            if (s.d[b]) (void)hipFree(s.d[b]);
+        }
+    }
+
+    void trim() {
+        std::lock_guard<std::mutex> g(mu_);
+        for (auto& kv : idle_) {
+            for (const StageSet& s : kv.second)
+                for (int b = 0; b < 2; ++b) {
+                    if (s.h[b]) (void)hipHostFree(s.h[b]);
+                    if (s.d[b]) (void)hipFree(s.d[b]);
+                }
+            kv.second.clear();
+        }
+    }
+
+  private:
+    std::mutex mu_;
+    std::map<int, std::vector<StageSet>> idle_;
+};
+static StagePool& stage_pool() {
+    static StagePool* p = new StagePool;  // never destroyed: the runtime may be gone at static destruction
+    return *p;
+}
+// the handle holds the leased set for one call (stage_setup grows it in place)
+struct StageLease {
+    msh_tree* t;
+    explicit StageLease(msh_tree* tree) : t(tree) {
+        const StageSet s = stage_pool().take(t->device);
+        for (int b = 0; b < 2; ++b) {
+            t->h_stage[b] = s.h[b];
+            t->d_stage[b] = s.d[b];
+        }
+        t->hstage_bytes = s.hbytes;
+        t->stage_bytes = s.dbytes;
+    }
+    ~StageLease() {
+        StageSet s;
+        for (int b = 0; b < 2; ++b) {
+            s.h[b] = t->h_stage[b];
+            s.d[b] = t->d_stage[b];
+            t->h_stage[b] = nullptr;
+            t->d_stage[b] = nullptr;
+        }
+        s.hbytes = t->hstage_bytes;
+        s.dbytes = t->stage_bytes;
+        t->hstage_bytes = t->stage_bytes = 0;
+        stage_pool().give(t->device, s);
+    }
+};
+
 // copy streams, events, and two host slabs of >= host_bytes and two device slabs of >= dev_bytes (grow-only)
 static int stage_setup(msh_tree* t, size_t host_bytes, size_t dev_bytes) {
     if (!t->s_up) MSH_HIP(hipStreamCreateWithFlags(&t->s_up, hipStreamNonBlocking));
-    if (!t->s_down) MSH_HIP(hipStreamCreateWithFlags(&t->s_down, hipStreamNonBlocking));
+    if (!t->s_down) {
+        // The runtime moves device -> host copies with blit kernels, which otherwise spread over every CU and
+        // starve the next chunk's sort and traversal launches; MESH_AMD_D2H_CUS = n keeps them on n CUs spread
+        // over the device (A/B switch)
+        const char* e = getenv("MESH_AMD_D2H_CUS");
+        const int n = e ? atoi(e) : 0;
+        hipDeviceProp_t prop;
+        if (n > 0 && hipGetDeviceProperties(&prop, t->device) == hipSuccess && n < prop.multiProcessorCount) {
+            const int ncu = prop.multiProcessorCount;
+            std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+            for (int k = 0; k < n; ++k) {
+                const int cu = (int)((long long)k * ncu / n);
+                mask[cu / 32] |= 1u << (cu % 32);
+            }
+            MSH_HIP(hipExtStreamCreateWithCUMask(&t->s_down, (uint32_t)mask.size(), mask.data()));
+        } else {
+            MSH_HIP(hipStreamCreateWithFlags(&t->s_down, hipStreamNonBlocking));
+        }
+    }
     for (int b = 0; b < 2; ++b) {
         if (!t->e_up[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_up[b], hipEventDisableTiming));
         if (!t->e_run[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_run[b], hipEventDisableTiming));
@@ -738,40 +836,6 @@ static PinnedPool& pinned_pool() {
     return *p;
 }
 
-// Row ranges (first row, rows) of the staged pipeline's chunks, none longer than `chunk`.  With ramp, the first
-// and the last chunks grow and shrink geometrically (chunk/8, chunk/4, chunk/2 ...): the GPU starts after a small
-// first upload instead of a full chunk's host copy and upload, and the call ends a small chunk's kernels and
-// download after the previous one instead of a full one's; the middle rows go in equal chunks of at most `chunk`.
-static std::vector<std::pair<size_t, size_t>> chunk_plan(size_t S, size_t chunk, bool ramp) {
-    std::vector<std::pair<size_t, size_t>> plan;
-    std::vector<size_t> up;
-    if (ramp)
-        for (size_t c = chunk / 8; c >= ((size_t)1 << 20) && c < chunk; c *= 2) up.push_back(c);
-    size_t ends = 0;
-    for (size_t c : up) ends += 2 * c;
-    while (!up.empty() && ends + chunk / 2 > S) {  // too few rows for the ramps: drop their largest steps
-        ends -= 2 * up.back();
-        up.pop_back();
-    }
-    size_t r = 0;
-    for (size_t c : up) {
-        plan.push_back({r, c});
-        r += c;
-    }
-    const size_t mid = S - ends;
-    const size_t nmid = (mid + chunk - 1) / chunk;
-    for (size_t k = 0; k < nmid; ++k) {
-        const size_t n = mid / nmid + (k < mid % nmid ? 1 : 0);
-        plan.push_back({r, n});
-        r += n;
-    }
-    for (size_t j = up.size(); j-- > 0;) {
-        plan.push_back({r, up[j]});
-        r += up[j];
-    }
-    return plan;
-}
-
 // pipelined() over caller arrays that are page-locked in place: per chunk an H2D copy of the input rows into a
 // device slab (copy stream `up`), the kernels (handle stream), a D2H copy of the output rows straight into
 // the caller's arrays (stream `down`); two device slabs alternate, so chunk k uploads while k - 1 computes and
@@ -871,9 +935,8 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
         }
         return st;
     }
-    const char* re = getenv("MESH_AMD_HOST_RAMP");  // A/B switch (measurement)
-    const std::vector<std::pair<size_t, size_t>> plan = chunk_plan(S, chunk, re && atoi(re) != 0);
-    const size_t nch = plan.size();
+    const size_t nch = (S + chunk - 1) / chunk;
+    StageLease lease(t);  // every stream is synchronised before pipelined returns, so the slabs are idle then
     // Optionally (host_register_enabled) page-lock the caller's arrays in place (hipHostRegister): the copy
     // engines then move the rows straight between the caller's memory and HBM, with no pageable <-> pinned
     // staging copies on the host.  Any registration failure falls back to staging.
@@ -911,7 +974,7 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
     //   chunk k's upload (copy stream), kernels (handle stream) and download (second copy stream).
     auto outs_of = [&](size_t kk, std::vector<CopyTask>& tasks) {
         const int b = (int)(kk & 1);
-        const size_t r0 = plan[kk].first, n = plan[kk].second;
+        const size_t r0 = kk * chunk, n = std::min(chunk, S - r0);
         size_t off = 0;
         for (const HostArr& a : arrs) {
             if (a.out)
@@ -934,7 +997,7 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
                 }
             }
             const bool have = k < nch;
-            const size_t r0 = have ? plan[k].first : 0, n = have ? plan[k].second : 0;
+            const size_t r0 = k * chunk, n = have ? std::min(chunk, S - r0) : 0;
             if (have) {
                 size_t off = 0;
                 for (const HostArr& a : arrs) {
@@ -1796,7 +1859,10 @@ void msh_host_free(void* p) {
     if (p) pinned_pool().release(p);
 }
 
-int msh_host_pool_trim(void) { return pinned_pool().trim(); }
+int msh_host_pool_trim(void) {
+    stage_pool().trim();
+    return pinned_pool().trim();
+}
 
 size_t msh_host_pool_bytes(void) { return pinned_pool().bytes(); }
 

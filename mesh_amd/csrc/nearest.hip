@@ -41,10 +41,6 @@
 
 #include "internal.h"
 
-#ifndef MSH_FASTSTACK
-#define MSH_FASTSTACK 0  // list path: LDS-only push / pop while no lane of the wave reaches the spill area
-#endif
-
 
 namespace msh {
 
@@ -269,20 +265,6 @@ struct Walker {
         }
         return false;
     }
-    // pop() whose loop reads LDS only, when no lane of the wave has stack entries in the spill area
-    template <class Pol>
-    __device__ inline bool pop_lds(const Pol& pol, uint2* __restrict__ lds, uint2* __restrict__ spill) {
-        if (__ballot(sp > kStack) != 0ull) return pop(pol, lds, spill);
-        while (sp > 0) {
-            --sp;
-            const uint2 e = lds[sp * kBlock];
-            if (__uint_as_float(e.y) <= pol.limf) {
-                node = (int)e.x;
-                return true;
-            }
-        }
-        return false;
-    }
     // Visit `node`: bound its two children by their fp32 oriented boxes (node_child_bounds), test leaf
     // children, descend into the nearer internal child and push the farther one.  Returns false when the
     // traversal is complete.
@@ -358,20 +340,7 @@ struct Walker {
             } else {
                 if (l0) p0 = ~c0;
                 if (l1) p0 = ~c1;
-#if MSH_FASTSTACK
-                // the farther internal child is pushed: every lane writes its candidate entry to slot sp (above the
-                // top, so harmless, where it pushes nothing) and only the pushing lanes advance sp; the spill path
-                // runs only when some lane of the wave is at the LDS stack's end
-                const uint2 e = make_uint2((unsigned)(first1 ? c0 : c1), __float_as_uint(first1 ? d0 : d1));
-                if (__ballot(sp >= kStack) != 0ull) {
-                    if (i0 && i1) push(e, lds, spill);
-                } else {
-                    lds[sp * kBlock] = e;
-                    sp += (i0 && i1) ? 1 : 0;
-                }
-#else
                 if (i0 && i1) push(make_uint2((unsigned)(first1 ? c0 : c1), __float_as_uint(first1 ? d0 : d1)), lds, spill);
-#endif
                 if (i0 || i1) {
                     node = (i0 && i1) ? (first1 ? c1 : c0) : (i0 ? c0 : c1);
                     more = true;
@@ -379,11 +348,7 @@ struct Walker {
             }
         }
         if (more) return true;
-#if MSH_FASTSTACK
-        return pop_lds(pol, lds, spill);
-#else
         return pop(pol, lds, spill);
-#endif
     }
 };
 

@@ -52,7 +52,8 @@ def main():
     for n in sizes:
         x = qa[:n].contiguous()
         p = torch.empty(n, dtype=torch.int32, device="cuda:0")
-        _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), n, p.data_ptr(), None))
+        _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), n, p.data_ptr(),
+                                                         torch.cuda.current_stream().cuda_stream))
         torch.cuda.synchronize()
         p = p.cpu().numpy().astype(np.int64)
         ref = np.argsort(keys24(x.cpu().numpy(), lo, hi), kind="stable")

@@ -238,9 +238,11 @@ def test_vertex_normals_device_bad_index():
     dv = torch.from_numpy(v).cuda()
     df = torch.from_numpy(f.view(np.int32)).cuda()
     dn = torch.empty_like(dv)
-    st = N.lib().msh_vertex_normals_device(dv.data_ptr(), v.shape[0], df.data_ptr(), f.shape[0], dn.data_ptr(), None)
+    st = N.lib().msh_vertex_normals_device(dv.data_ptr(), v.shape[0], df.data_ptr(), f.shape[0], dn.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream)
     assert st == N.MSH_EINVAL and b"out of range" in N.lib().msh_last_error()
     f[5, 1] = 0  # a valid mesh on the same buffers still works
     df.copy_(torch.from_numpy(f.view(np.int32)))
-    st = N.lib().msh_vertex_normals_device(dv.data_ptr(), v.shape[0], df.data_ptr(), f.shape[0], dn.data_ptr(), None)
+    st = N.lib().msh_vertex_normals_device(dv.data_ptr(), v.shape[0], df.data_ptr(), f.shape[0], dn.data_ptr(),
+                                           torch.cuda.current_stream().cuda_stream)
     assert st == 0

@@ -292,7 +292,10 @@ def test_query_order_equals_stable_argsort():
     bad[3::11, 2] = float("inf")
     for x in (q, q[:12_345_677], q[:1000], bad):
         p = torch.empty(x.shape[0], dtype=torch.int32, device="cuda:0")
-        _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), x.shape[0], p.data_ptr(), None))
+        # on torch's stream: the rows come from torch's generator, whose kernels the tree's own (non-blocking)
+        # stream would not wait for
+        _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), x.shape[0], p.data_ptr(),
+                                                         torch.cuda.current_stream().cuda_stream))
         torch.cuda.synchronize()
         ref = np.argsort(keys24(x.cpu().numpy(), lo, hi), kind="stable")
         assert np.array_equal(p.cpu().numpy().astype(np.int64), ref), "rows %d" % x.shape[0]
