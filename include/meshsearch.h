@@ -16,7 +16,9 @@
  *    (spatialsearchmodule.cpp:82-97 ValueError; cgal_error_emulation.hpp:19-33 RuntimeError).
  *  - Host-buffer entry points (no _device suffix) copy inputs to HBM, run the HIP kernels and copy
  *    results back; they are synchronous.  *_device entry points take HBM pointers and a hipStream_t
- *    (passed as void*, NULL = the handle's own stream) and are asynchronous on that stream.
+ *    (passed as void*, NULL = the handle's own stream, a blocking stream that orders with the legacy default
+ *    stream — so NULL also serves a caller whose work is queued on the default stream) and are asynchronous
+ *    on that stream.
  *  - A handle owns device copies of the mesh and its BVH (the reference's TreeAndTri owns host
  *    copies, nearest_triangle.hpp:28-32); input arrays are not retained.  Calls on one handle must be
  *    serialised by the caller (host threads); on the device, launches that share a handle's scratch

@@ -188,7 +188,11 @@ static int new_tree(int kind, msh_tree** out) {
     msh_tree* t = new msh_tree();
     t->device = dev;
     t->kind = kind;
-    hipError_t e = hipStreamCreateWithFlags(&t->stream, hipStreamNonBlocking);
+    // A blocking stream: it orders with the legacy default stream, so a caller that queues its inputs there (torch's
+    // default stream is handle 0, which the *_device entry points read as "the handle's own stream") and then
+    // passes NULL sees its writes before the handle's kernels read them, and its later default-stream work after
+    // them.  (A non-blocking stream here let the C3 query order read rows torch's generator was still writing.)
+    hipError_t e = hipStreamCreateWithFlags(&t->stream, hipStreamDefault);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->ws_done, hipEventDisableTiming);
     if (e != hipSuccess) {
         set_error("hipStreamCreate / hipEventCreate failed on device %d: %s", dev, hipGetErrorString(e));
@@ -693,25 +697,7 @@ struct StageLease {
 // copy streams, events, and two host slabs of >= host_bytes and two device slabs of >= dev_bytes (grow-only)
 static int stage_setup(msh_tree* t, size_t host_bytes, size_t dev_bytes) {
     if (!t->s_up) MSH_HIP(hipStreamCreateWithFlags(&t->s_up, hipStreamNonBlocking));
-    if (!t->s_down) {
-        // The runtime moves device -> host copies with blit kernels, which otherwise spread over every CU and
-        // starve the next chunk's sort and traversal launches; MESH_AMD_D2H_CUS = n keeps them on n CUs spread
-        // over the device (A/B switch)
-        const char* e = getenv("MESH_AMD_D2H_CUS");
-        const int n = e ? atoi(e) : 0;
-        hipDeviceProp_t prop;
-        if (n > 0 && hipGetDeviceProperties(&prop, t->device) == hipSuccess && n < prop.multiProcessorCount) {
-            const int ncu = prop.multiProcessorCount;
-            std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-            for (int k = 0; k < n; ++k) {
-                const int cu = (int)((long long)k * ncu / n);
-                mask[cu / 32] |= 1u << (cu % 32);
-            }
-            MSH_HIP(hipExtStreamCreateWithCUMask(&t->s_down, (uint32_t)mask.size(), mask.data()));
-        } else {
-            MSH_HIP(hipStreamCreateWithFlags(&t->s_down, hipStreamNonBlocking));
-        }
-    }
+    if (!t->s_down) MSH_HIP(hipStreamCreateWithFlags(&t->s_down, hipStreamNonBlocking));
     for (int b = 0; b < 2; ++b) {
         if (!t->e_up[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_up[b], hipEventDisableTiming));
         if (!t->e_run[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_run[b], hipEventDisableTiming));
