@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <chrono>
 #include <map>
 #include <atomic>
 #include <condition_variable>
@@ -89,6 +90,16 @@ TimedLaunch::~TimedLaunch() {
     (void)hipEventRecord(b, s);
     std::lock_guard<std::mutex> g(g_tmu);
     g_pending.push_back(Pending{name, a, b});
+}
+
+// host-side intervals under the same names (msh_timing_get): the host pipeline's copies and waits
+static void host_time(const char* name, std::chrono::steady_clock::time_point t0) {
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    std::lock_guard<std::mutex> g(g_tmu);
+    if (!g_timing) return;
+    auto& t = g_times[name];
+    t.first += ms;
+    t.second += 1;
 }
 
 static void resolve_pending() {
@@ -975,12 +986,14 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
             const int b = (int)(k & 1);
             std::vector<CopyTask> tasks;
             if (k >= 2) {
+                const auto tw = std::chrono::steady_clock::now();
                 if (direct_out) {
                     if ((e = hipEventSynchronize(e_up[b])) != hipSuccess) { fail(e, "upload"); break; }
                 } else {
                     if ((e = hipEventSynchronize(e_down[b])) != hipSuccess) { fail(e, "kernels / download"); break; }
                     outs_of(k - 2, tasks);
                 }
+                host_time("host_wait", tw);
             }
             const bool have = k < nch;
             const size_t r0 = k * chunk, n = have ? std::min(chunk, S - r0) : 0;
@@ -993,7 +1006,9 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
                     off += a.row_bytes;
                 }
             }
+            const auto tc = std::chrono::steady_clock::now();
             copy_pool().run(tasks);
+            host_time("host_copy", tc);
             if (!have) continue;
             // the device slab's previous chunk (k - 2) must have been downloaded before it is overwritten
             if (direct_out && k >= 2 && (e = hipStreamWaitEvent(up, e_down[b], 0)) != hipSuccess) { fail(e, "upload"); break; }

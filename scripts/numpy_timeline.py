@@ -29,10 +29,16 @@ def run(n, calls):
     tree = spatialsearch.aabbtree_compute(v, f)
     outs = []
     for k in range(calls):
+        _native.timing_reset()
+        _native.timing_enable(True)
         t0 = time.perf_counter()
         outs.append(spatialsearch.aabbtree_nearest(tree, q))
         outs = outs[-2:]  # a caller holding its previous result while it asks for the next
-        print("call %d: %.1f ms" % (k, (time.perf_counter() - t0) * 1e3), flush=True)
+        wall = (time.perf_counter() - t0) * 1e3
+        _native.timing_enable(False)
+        parts = {name: _native.timing_get(name) for name in ("host_copy", "host_wait", "nearest", "sort")}
+        print("call %d: %.1f ms  %s" % (k, wall, "  ".join("%s %.1f ms / %d" % (n, ms, c) for n, (ms, c) in
+                                                              parts.items())), flush=True)
 
 
 def parse(d):
