@@ -178,8 +178,8 @@ static void free_tree(msh_tree* t) {
     if (t->d_vorder_shard) (void)hipFree(t->d_vorder_shard);
     if (t->d_cut) (void)hipFree(t->d_cut);
     if (t->d_cut_hint) (void)hipFree(t->d_cut_hint);
-    for (int b = 0; b < 2; ++b) {
-        if (t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
+    for (int b = 0; b < 3; ++b) {
+        if (b < 2 && t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
         if (t->d_stage[b]) (void)hipFree(t->d_stage[b]);
         if (t->e_up[b]) (void)hipEventDestroy(t->e_up[b]);
         if (t->e_run[b]) (void)hipEventDestroy(t->e_run[b]);
@@ -614,10 +614,10 @@ struct HostArr {
 };
 
 static void release_stage(msh_tree* t, bool host, bool dev) {
-    for (int b = 0; b < 2; ++b) {
-        if (host && t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
+    for (int b = 0; b < 3; ++b) {
+        if (host && b < 2 && t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
         if (dev && t->d_stage[b]) (void)hipFree(t->d_stage[b]);
-        if (host) t->h_stage[b] = nullptr;
+        if (host && b < 2) t->h_stage[b] = nullptr;
         if (dev) t->d_stage[b] = nullptr;
     }
     if (host) t->hstage_bytes = 0;
@@ -631,7 +631,7 @@ static void release_stage(msh_tree* t) { release_stage(t, true, true); }
 // once per process instead of once per tree.  At most kStageKeep idle sets are kept per device.
 struct StageSet {
     void* h[2] = {nullptr, nullptr};
-    void* d[2] = {nullptr, nullptr};
+    void* d[3] = {nullptr, nullptr, nullptr};
     size_t hbytes = 0, dbytes = 0;
 };
 class StagePool {
@@ -652,8 +652,8 @@ class StagePool {
             v.push_back(s);
             return;
         }
-        for (int b = 0; b < 2; ++b) {  // an extra set (concurrent calls): freed
-            if (s.h[b]) (void)hipHostFree(s.h[b]);
+        for (int b = 0; b < 3; ++b) {  // an extra set (concurrent calls): freed
+            if (b < 2 && s.h[b]) (void)hipHostFree(s.h[b]);
             if (s.d[b]) (void)hipFree(s.d[b]);
         }
     }
@@ -662,8 +662,8 @@ class StagePool {
         std::lock_guard<std::mutex> g(mu_);
         for (auto& kv : idle_) {
             for (const StageSet& s : kv.second)
-                for (int b = 0; b < 2; ++b) {
-                    if (s.h[b]) (void)hipHostFree(s.h[b]);
+                for (int b = 0; b < 3; ++b) {
+                    if (b < 2 && s.h[b]) (void)hipHostFree(s.h[b]);
                     if (s.d[b]) (void)hipFree(s.d[b]);
                 }
             kv.second.clear();
@@ -683,8 +683,8 @@ struct StageLease {
     msh_tree* t;
     explicit StageLease(msh_tree* tree) : t(tree) {
         const StageSet s = stage_pool().take(t->device);
-        for (int b = 0; b < 2; ++b) {
-            t->h_stage[b] = s.h[b];
+        for (int b = 0; b < 3; ++b) {
+            if (b < 2) t->h_stage[b] = s.h[b];
             t->d_stage[b] = s.d[b];
         }
         t->hstage_bytes = s.hbytes;
@@ -692,10 +692,12 @@ struct StageLease {
     }
     ~StageLease() {
         StageSet s;
-        for (int b = 0; b < 2; ++b) {
-            s.h[b] = t->h_stage[b];
+        for (int b = 0; b < 3; ++b) {
+            if (b < 2) {
+                s.h[b] = t->h_stage[b];
+                t->h_stage[b] = nullptr;
+            }
             s.d[b] = t->d_stage[b];
-            t->h_stage[b] = nullptr;
             t->d_stage[b] = nullptr;
         }
         s.hbytes = t->hstage_bytes;
@@ -709,7 +711,7 @@ struct StageLease {
 static int stage_setup(msh_tree* t, size_t host_bytes, size_t dev_bytes) {
     if (!t->s_up) MSH_HIP(hipStreamCreateWithFlags(&t->s_up, hipStreamNonBlocking));
     if (!t->s_down) MSH_HIP(hipStreamCreateWithFlags(&t->s_down, hipStreamNonBlocking));
-    for (int b = 0; b < 2; ++b) {
+    for (int b = 0; b < 3; ++b) {
         if (!t->e_up[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_up[b], hipEventDisableTiming));
         if (!t->e_run[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_run[b], hipEventDisableTiming));
         if (!t->e_down[b]) MSH_HIP(hipEventCreateWithFlags(&t->e_down[b], hipEventDisableTiming));
@@ -721,7 +723,7 @@ static int stage_setup(msh_tree* t, size_t host_bytes, size_t dev_bytes) {
     }
     if (t->stage_bytes < dev_bytes) {
         release_stage(t, false, true);
-        for (int b = 0; b < 2; ++b) MSH_HIP(hipMalloc(&t->d_stage[b], dev_bytes));
+        for (int b = 0; b < 3; ++b) MSH_HIP(hipMalloc(&t->d_stage[b], dev_bytes));
         t->stage_bytes = dev_bytes;
     }
     return MSH_OK;
@@ -965,10 +967,14 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
         set_error("%s: %s", what, hipGetErrorString(e));
         st = e == hipErrorOutOfMemory ? MSH_ENOMEM : MSH_EDEVICE;
     };
-    // Step k (slab b = k & 1; a slab holds one chunk's input rows and, after them, its output rows):
-    //   wait for chunk k - 2's download, then copy chunk k - 2's outputs out of slab b AND chunk k's inputs into
-    //   it, on all copy workers at once, while the GPU works on chunk k - 1 in the other slab; then enqueue
-    //   chunk k's upload (copy stream), kernels (handle stream) and download (second copy stream).
+    // Step k (host slab b = k & 1, device slab db = k % 3; a slab holds one chunk's input rows and, after them,
+    // its output rows; events are per device slab):
+    //   wait for chunk k - 2's upload (direct_out) or download (staged outputs, copied out of host slab b here),
+    //   then copy chunk k's inputs into host slab b, on all copy workers at once, while the GPU works on earlier
+    //   chunks; then enqueue chunk k's upload (copy stream; into device slab db once chunk k - 3's download has
+    //   left it), kernels (handle stream) and download (second copy stream).  Three device slabs let chunk k's
+    //   upload run while chunk k - 2 is still downloading (with two, each upload waited for the download of the
+    //   chunk before: C3 numpy API 112 ms per 100M queries).
     auto outs_of = [&](size_t kk, std::vector<CopyTask>& tasks) {
         const int b = (int)(kk & 1);
         const size_t r0 = kk * chunk, n = std::min(chunk, S - r0);
@@ -983,14 +989,14 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
     do {
         hipError_t e = hipSuccess;
         for (size_t k = 0; k < nch + 2 && st == MSH_OK; ++k) {
-            const int b = (int)(k & 1);
+            const int b = (int)(k & 1), db = (int)(k % 3), pb = (int)((k + 1) % 3);  // pb: chunk k - 2's slab
             std::vector<CopyTask> tasks;
             if (k >= 2) {
                 const auto tw = std::chrono::steady_clock::now();
                 if (direct_out) {
-                    if ((e = hipEventSynchronize(e_up[b])) != hipSuccess) { fail(e, "upload"); break; }
+                    if ((e = hipEventSynchronize(e_up[pb])) != hipSuccess) { fail(e, "upload"); break; }
                 } else {
-                    if ((e = hipEventSynchronize(e_down[b])) != hipSuccess) { fail(e, "kernels / download"); break; }
+                    if ((e = hipEventSynchronize(e_down[pb])) != hipSuccess) { fail(e, "kernels / download"); break; }
                     outs_of(k - 2, tasks);
                 }
                 host_time("host_wait", tw);
@@ -1010,27 +1016,28 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
             copy_pool().run(tasks);
             host_time("host_copy", tc);
             if (!have) continue;
-            // the device slab's previous chunk (k - 2) must have been downloaded before it is overwritten
-            if (direct_out && k >= 2 && (e = hipStreamWaitEvent(up, e_down[b], 0)) != hipSuccess) { fail(e, "upload"); break; }
+            // the device slab's previous chunk (k - 3) must have been downloaded before it is overwritten (staged
+            // outputs: the host waited for chunk k - 2's download above, which the in-order download stream implies)
+            if (direct_out && k >= 3 && (e = hipStreamWaitEvent(up, e_down[db], 0)) != hipSuccess) { fail(e, "upload"); break; }
             size_t off = 0;
             for (const HostArr& a : arrs) {
-                if (a.in && (e = hipMemcpyAsync(static_cast<char*>(dev[b]) + off * chunk,
+                if (a.in && (e = hipMemcpyAsync(static_cast<char*>(dev[db]) + off * chunk,
                                                 static_cast<char*>(host[b]) + off * chunk, n * a.row_bytes,
                                                 hipMemcpyHostToDevice, up)) != hipSuccess)
                     break;
                 off += a.row_bytes;
             }
-            if (e == hipSuccess) e = hipEventRecord(e_up[b], up);
-            if (e == hipSuccess) e = hipStreamWaitEvent(sc, e_up[b], 0);
+            if (e == hipSuccess) e = hipEventRecord(e_up[db], up);
+            if (e == hipSuccess) e = hipStreamWaitEvent(sc, e_up[db], 0);
             if (e != hipSuccess) { fail(e, "upload"); break; }
             std::vector<char*> slabs;
             off = 0;
             for (const HostArr& a : arrs) {
-                slabs.push_back(static_cast<char*>(dev[b]) + off * chunk);
+                slabs.push_back(static_cast<char*>(dev[db]) + off * chunk);
                 off += a.row_bytes;
             }
             if ((st = run(r0, n, slabs)) != MSH_OK) break;
-            if ((e = hipEventRecord(e_run[b], sc)) != hipSuccess || (e = hipStreamWaitEvent(down, e_run[b], 0)) != hipSuccess) {
+            if ((e = hipEventRecord(e_run[db], sc)) != hipSuccess || (e = hipStreamWaitEvent(down, e_run[db], 0)) != hipSuccess) {
                 fail(e, "launch");
                 break;
             }
@@ -1039,13 +1046,13 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
                 if (a.out) {
                     char* dst = direct_out ? static_cast<char*>(a.out) + r0 * a.row_bytes
                                            : static_cast<char*>(host[b]) + off * chunk;
-                    if ((e = hipMemcpyAsync(dst, static_cast<char*>(dev[b]) + off * chunk, n * a.row_bytes,
+                    if ((e = hipMemcpyAsync(dst, static_cast<char*>(dev[db]) + off * chunk, n * a.row_bytes,
                                             hipMemcpyDeviceToHost, down)) != hipSuccess)
                         break;
                 }
                 off += a.row_bytes;
             }
-            if (e == hipSuccess) e = hipEventRecord(e_down[b], down);
+            if (e == hipSuccess) e = hipEventRecord(e_down[db], down);
             if (e != hipSuccess) { fail(e, "download"); break; }
         }
     } while (0);

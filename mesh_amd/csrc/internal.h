@@ -111,11 +111,12 @@ struct msh_tree {
     // host-call staging (lazily created, grow-only): two pinned host slabs, two device slabs, copy
     // streams and their events (api.cpp pipelined())
     void* h_stage[2] = {nullptr, nullptr};
-    void* d_stage[2] = {nullptr, nullptr};
+    void* d_stage[3] = {nullptr, nullptr, nullptr};  // device slabs: a ring of 3 (pipelined)
     size_t stage_bytes = 0;   // device slabs
     size_t hstage_bytes = 0;  // host slabs (inputs only when results go straight into pinned arrays)
     hipStream_t s_up = nullptr, s_down = nullptr;
-    hipEvent_t e_up[2] = {nullptr, nullptr}, e_run[2] = {nullptr, nullptr}, e_down[2] = {nullptr, nullptr};
+    hipEvent_t e_up[3] = {nullptr, nullptr, nullptr}, e_run[3] = {nullptr, nullptr, nullptr},
+               e_down[3] = {nullptr, nullptr, nullptr};
     double build_ms = 0.0;
     int max_depth = 0;             // bound of the deepest leaf (root children = 1): k_karras prefix lengths
     // entry cut (single triangle trees; nearest.hip build_entry_cut): a G^3 grid over the scene box widened by

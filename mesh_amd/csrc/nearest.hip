@@ -41,10 +41,6 @@
 
 #include "internal.h"
 
-#ifndef MSH_TOPREG
-#define MSH_TOPREG 0  // Walker: the stack's top entry in registers
-#endif
-
 
 namespace msh {
 
@@ -252,29 +248,6 @@ struct PtPol {
 struct Walker {
     int node;
     int sp;
-#if MSH_TOPREG
-    // The top entry lives in registers (entries 0 .. sp - 2 in the stack): a pop takes it at once and reloads
-    // the next one from LDS, whose latency the following node load and test cover.
-    uint2 top;
-    __device__ inline void push(uint2 e, uint2* __restrict__ lds, uint2* __restrict__ spill) {
-        if (sp > 0) stack_put(lds, spill, sp - 1, top);
-        top = e;
-        ++sp;
-    }
-    template <class Pol>
-    __device__ inline bool pop(const Pol& pol, uint2* __restrict__ lds, uint2* __restrict__ spill) {
-        while (sp > 0) {
-            const uint2 e = top;
-            --sp;
-            if (sp > 0) top = stack_get(lds, spill, sp - 1);
-            if (__uint_as_float(e.y) <= pol.limf) {
-                node = (int)e.x;
-                return true;
-            }
-        }
-        return false;
-    }
-#else
     __device__ inline void push(uint2 e, uint2* __restrict__ lds, uint2* __restrict__ spill) {
         stack_put(lds, spill, sp, e);
         ++sp;
@@ -292,7 +265,6 @@ struct Walker {
         }
         return false;
     }
-#endif
     // Visit `node`: bound its two children by their fp32 oriented boxes (node_child_bounds), test leaf
     // children, descend into the nearer internal child and push the farther one.  Returns false when the
     // traversal is complete.
@@ -550,10 +522,7 @@ __device__ inline unsigned lanes_below(unsigned long long m) {
 // owners through LDS: an atomic min of the squared distance's bits per owner, then an atomic min of
 // (face << 32 | leaf) among the entries that reached it: the lexicographic (d2, face) rule.
 // kPend (C3, M q/s): 3: 1236, 4: 1346, 8: 1593, 16: 1677, 32: 1706, unbounded: 1689; per-lane queues 1541.
-#ifndef MSH_KPEND
-#define MSH_KPEND 32
-#endif
-constexpr int kPend = MSH_KPEND;
+constexpr int kPend = 32;
 
 constexpr unsigned kRing = 256;     // ring entries per wave: < 64 left after full rounds + <= 128 per step
 constexpr size_t kListMaxLeaves = (size_t)1 << 26;  // leaf index bits of a ring entry
