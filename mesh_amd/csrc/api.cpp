@@ -736,14 +736,35 @@ static bool host_register_enabled() {
     return e && atoi(e) != 0;
 }
 
-// Rows per pipelined chunk (MESH_AMD_HOST_CHUNK overrides).  Larger chunks keep the sorted traversal coherent
-// and cut per-chunk launch tails; measured on C3 (100M queries): staging 4M 155 ms, 8M 137, 16M 134, 32M 150;
-// results in pinned pool arrays 4M 197 ms, 16M 145, 32M 125.
-static size_t host_chunk(bool direct_out) {
-    const char* e = getenv("MESH_AMD_HOST_CHUNK");
-    const long long c = e ? atoll(e) : 0;
-    if (c > 0) return (size_t)c;
-    return direct_out ? ((size_t)32 << 20) : ((size_t)16 << 20);
+// Chunk plan of a pipelined call: the rows of each chunk, the last entry repeated.  Larger chunks keep the sorted
+// traversal coherent and cut per-chunk launch tails; a small first chunk lets the first download start early.
+// The host link moves both directions at ~57 GB/s combined (scripts/pcie_probe.py), and a C3 call moves 2.4 GB
+// up and 3.2 GB down per 100M queries, so a call is bound by its copies once they overlap the kernels.
+// Measured on C3 (100M queries, results in pinned pool arrays, three device slabs; profiles/r04_c3np_plan_ab.json):
+// 32M chunks 98 ms, 24M 94-96, 16M 120, 6M + 30M 96, 4M + 12M + 28M 94-96, 8M + 16M + 32M 92-94, 12M + 28M 91,
+// 8M + 24M 89-91, 8M + 20M 86-89.  Staged outputs (caller arrays outside the pool): 16M chunks (4M 155 ms, 8M 137,
+// 16M 134, 32M 150).  Overrides: MESH_AMD_HOST_CHUNK = rows (uniform chunks), MESH_AMD_HOST_PLAN = "a,b,..." in
+// units of 2^20 rows.
+static std::vector<size_t> host_plan(bool direct_out) {
+    if (const char* e = getenv("MESH_AMD_HOST_CHUNK")) {
+        const long long c = atoll(e);
+        if (c > 0) return {(size_t)c};
+    }
+    std::vector<size_t> plan;
+    if (const char* e = getenv("MESH_AMD_HOST_PLAN")) {
+        for (const char* p = e; *p;) {
+            char* q = nullptr;
+            const double v = strtod(p, &q);
+            if (q == p) break;
+            if (v > 0) plan.push_back(std::max<size_t>(64, (size_t)(v * (double)(1 << 20))));
+            p = *q ? q + 1 : q;
+        }
+    }
+    if (plan.empty()) {
+        if (direct_out) plan = {(size_t)8 << 20, (size_t)20 << 20};
+        else plan = {(size_t)16 << 20};
+    }
+    return plan;
 }
 
 // Page-locked result pool (msh_host_alloc / msh_host_free, meshsearch.h).  Blocks are hipHostMalloc'd in 2-MB
@@ -903,7 +924,6 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
     bool direct_out = true;
     for (const HostArr& a : arrs)
         if (a.out && !pinned_pool().contains(a.out, S * a.row_bytes)) direct_out = false;
-    const size_t chunk = std::min(S, host_chunk(direct_out));
     hipStream_t sc = t->stream;
     int st = MSH_OK;
     if (S * row <= ((size_t)16 << 20)) {  // small call: one pageable round trip through device scratch
@@ -934,7 +954,19 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
         }
         return st;
     }
-    const size_t nch = (S + chunk - 1) / chunk;
+    // chunks (host_plan): first rows c0s[k], rows cns[k]; slabs are sized for the largest
+    std::vector<size_t> c0s, cns;
+    {
+        const std::vector<size_t> plan = host_plan(direct_out);
+        for (size_t r = 0, j = 0; r < S; ++j) {
+            const size_t n = std::min(plan[std::min(j, plan.size() - 1)], S - r);
+            c0s.push_back(r);
+            cns.push_back(n);
+            r += n;
+        }
+    }
+    const size_t chunk = *std::max_element(cns.begin(), cns.end());
+    const size_t nch = cns.size();
     StageLease lease(t);  // every stream is synchronised before pipelined returns, so the slabs are idle then
     // Optionally (host_register_enabled) page-lock the caller's arrays in place (hipHostRegister): the copy
     // engines then move the rows straight between the caller's memory and HBM, with no pageable <-> pinned
@@ -977,7 +1009,7 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
     //   chunk before: C3 numpy API 112 ms per 100M queries).
     auto outs_of = [&](size_t kk, std::vector<CopyTask>& tasks) {
         const int b = (int)(kk & 1);
-        const size_t r0 = kk * chunk, n = std::min(chunk, S - r0);
+        const size_t r0 = c0s[kk], n = cns[kk];
         size_t off = 0;
         for (const HostArr& a : arrs) {
             if (a.out)
@@ -1002,7 +1034,7 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
                 host_time("host_wait", tw);
             }
             const bool have = k < nch;
-            const size_t r0 = k * chunk, n = have ? std::min(chunk, S - r0) : 0;
+            const size_t r0 = have ? c0s[k] : S, n = have ? cns[k] : 0;
             if (have) {
                 size_t off = 0;
                 for (const HostArr& a : arrs) {
