@@ -363,7 +363,7 @@ def main():
                                   "broadcast, answers all-gathered)" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "k_knn<0,false,true> + k_knn_coop<0,false> (pass 1 + pass 2: traversal + fp64 refinement)",
+                     "kernel": "k_knn<0,false,true,true> + k_knn_coop<0,false> (pass 1 + pass 2: traversal + fp64 refinement)",
                      "kernel_ms": avg_kernel_s * 1e3, "queries_per_launch": S_loc, "bytes_per_query": bytes_per_query,
                      "node_bytes": node_b, "leaf_bytes": leaf_b,
                      "nodes_per_query": n_node, "leaves_per_query": n_leaf,

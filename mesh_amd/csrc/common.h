@@ -466,6 +466,21 @@ __device__ inline uint2 stack_get(const uint2* __restrict__ lds, const uint2* __
     const unsigned long long v = __builtin_nontemporal_load(p);
     return make_uint2((unsigned)v, (unsigned)(v >> 32));
 }
+// 4-B entries (compact stacks, trees of <= 2^20 leaves): the same placement; the spill side takes a 64-bit slot
+// like the 8-B stack's (a 32-bit access let the compiler merge both sides into one flat access)
+__device__ inline void stack_put(uint32_t* __restrict__ lds, uint2* __restrict__ spill, int sp, uint32_t e) {
+    if (sp < kStack) {
+        lds[sp * kBlock] = e;
+    } else {
+        __builtin_nontemporal_store((unsigned long long)e,
+                                    reinterpret_cast<unsigned long long*>(spill + (size_t)(sp - kStack) * kBlock));
+    }
+}
+__device__ inline uint32_t stack_get(const uint32_t* __restrict__ lds, const uint2* __restrict__ spill, int sp) {
+    if (sp < kStack) return lds[sp * kBlock];
+    return (uint32_t)__builtin_nontemporal_load(
+        reinterpret_cast<const unsigned long long*>(spill + (size_t)(sp - kStack) * kBlock));
+}
 
 // 30-bit Morton code of a query point in the box [l, h] (fp32 cell coordinates, 1024 cells per axis, clamped)
 __device__ inline uint32_t query_morton30(double x, double y, double z, float lx, float ly, float lz, float hx, float hy,

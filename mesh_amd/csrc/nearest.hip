@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <type_traits>
 
 #include "internal.h"
 
@@ -244,22 +245,61 @@ struct PtPol {
     }
 };
 
+// Stack entries (node or ~leaf ref, fp32 bound bits): 8 B, or 4 B for trees of <= 2^20 leaves — the bound's top
+// 11 bits (sign 0, exponent, 2 mantissa bits: the bound truncated, so still a lower bound; a pop it fails to prune
+// only visits a node whose children are then bounded exactly) over the ref's 21 bits, one v_bfi to pack, a v_and
+// and a v_bfe to unpack.
+struct Ent8 {
+    typedef uint2 T;
+    __device__ static T make(uint32_t ref, uint32_t bb) { return make_uint2(ref, bb); }
+    __device__ static int ref(T e) { return (int)e.x; }
+    __device__ static float bound(T e) { return __uint_as_float(e.y); }
+};
+struct Ent4 {
+    typedef uint32_t T;
+    __device__ static T make(uint32_t ref, uint32_t bb) { return (bb & 0xFFE00000u) | (ref & 0x001FFFFFu); }
+    __device__ static int ref(T e) { return __builtin_amdgcn_sbfe((int)e, 0, 21); }
+    __device__ static float bound(T e) { return __uint_as_float(e & 0xFFE00000u); }
+};
+constexpr size_t kEnt4MaxLeaves = (size_t)1 << 20;  // refs in [-2^20, 2^20): 21 bits
+
+// A node's 64 B loaded into LDS ahead of its step (global_load_lds: no registers hold it while the lane appends
+// leaves or runs leaf rounds).  The wave's slot array holds 4 x 64 float4 (piece k of lane l at k * 64 + l); wsl =
+// its LDS byte address (wave-uniform: M0), nb = this lane's first piece.
+__device__ inline void node_prefetch(const BNode* __restrict__ nodes, int i, uint32_t wsl) {
+    const float4* g = reinterpret_cast<const float4*>(nodes + i);
+    typedef __attribute__((address_space(3))) void* LP;
+    // (no immediate offsets: the instruction's offset moves the LDS destination too)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) __builtin_amdgcn_global_load_lds(g + k, (LP)(size_t)(wsl + 1024 * k), 16, 0, 0);
+}
+__device__ inline NodeV node_from_lds(const float4* nb) {
+    // the compiler does not order LDS reads after an LDS DMA: wait for it (vmcnt counts the DMA in issue order)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    NodeV n;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) n.q[k] = nb[k * 64];
+    return n;
+}
+
 // Per-lane depth-first walker.  lds: this lane's column of the LDS stack (stride kBlock).
-struct Walker {
+template <class E = Ent8>
+struct WalkerT {
+    typedef typename E::T Ent;
     int node;
     int sp;
-    __device__ inline void push(uint2 e, uint2* __restrict__ lds, uint2* __restrict__ spill) {
-        stack_put(lds, spill, sp, e);
+    __device__ inline void push(uint32_t ref, uint32_t bb, Ent* __restrict__ lds, uint2* __restrict__ spill) {
+        stack_put(lds, spill, sp, E::make(ref, bb));
         ++sp;
     }
     // pop until an entry survives the current limit; false when the stack is exhausted
     template <class Pol>
-    __device__ inline bool pop(const Pol& pol, uint2* __restrict__ lds, uint2* __restrict__ spill) {
+    __device__ inline bool pop(const Pol& pol, Ent* __restrict__ lds, uint2* __restrict__ spill) {
         while (sp > 0) {
             --sp;
-            const uint2 e = stack_get(lds, spill, sp);
-            if (__uint_as_float(e.y) <= pol.limf) {
-                node = (int)e.x;
+            const Ent e = stack_get(lds, spill, sp);
+            if (E::bound(e) <= pol.limf) {
+                node = E::ref(e);
                 return true;
             }
         }
@@ -269,7 +309,7 @@ struct Walker {
     // children, descend into the nearer internal child and push the farther one.  Returns false when the
     // traversal is complete.
     template <class Pol, bool STATS>
-    __device__ inline bool step(const BNode* __restrict__ nodes, const QF& qf, Pol& pol, uint2* __restrict__ lds,
+    __device__ inline bool step(const BNode* __restrict__ nodes, const QF& qf, Pol& pol, Ent* __restrict__ lds,
                                 uint2* __restrict__ spill, unsigned& n_nodes, unsigned& n_leaves) {
         const NodeV nd = load_node(nodes, node);
         if (STATS) ++n_nodes;
@@ -293,7 +333,7 @@ struct Walker {
             int nearc = c0, farc = c1;
             float dfar = d1;
             if (d1 < d0) { nearc = c1; farc = c0; dfar = d0; }
-            push(make_uint2((unsigned)farc, __float_as_uint(dfar)), lds, spill);
+            push((unsigned)farc, __float_as_uint(dfar), lds, spill);
             node = nearc;
             return true;
         }
@@ -310,15 +350,17 @@ struct Walker {
     // One push site and one pop site (each is a divergent loop or branch in the wave-synchronous caller, so
     // every extra copy runs serially for the lanes that take it); a parked leaf goes straight to `node`,
     // since the stack entry it would get is the one the following pop returns.
-    template <class Pol, bool STATS>
+    // PF: the node was prefetched into this lane's LDS slot (nb; node_prefetch), and the next one is prefetched
+    // before returning
+    template <class Pol, bool STATS, bool PF = false>
     __device__ inline bool step_collect(const BNode* __restrict__ nodes, const QF& qf, const Pol& pol,
-                                        uint2* __restrict__ lds, uint2* __restrict__ spill, unsigned& n_nodes, int& p0,
-                                        int& p1, int room = 2) {
+                                        Ent* __restrict__ lds, uint2* __restrict__ spill, unsigned& n_nodes, int& p0,
+                                        int& p1, int room = 2, const float4* nb = nullptr, uint32_t wsl = 0) {
         bool more = false;  // `node` holds the next entry; otherwise pop
         if (node < 0) {
             p0 = ~node;
         } else {
-            const NodeV nd = load_node(nodes, node);
+            const NodeV nd = PF ? node_from_lds(nb) : load_node(nodes, node);
             if (STATS) ++n_nodes;
             float d0, d1;
             node_child_bounds(nd, qf, d0, d1);
@@ -340,17 +382,19 @@ struct Walker {
             } else {
                 if (l0) p0 = ~c0;
                 if (l1) p0 = ~c1;
-                if (i0 && i1) push(make_uint2((unsigned)(first1 ? c0 : c1), __float_as_uint(first1 ? d0 : d1)), lds, spill);
+                if (i0 && i1) push((unsigned)(first1 ? c0 : c1), __float_as_uint(first1 ? d0 : d1), lds, spill);
                 if (i0 || i1) {
                     node = (i0 && i1) ? (first1 ? c1 : c0) : (i0 ? c0 : c1);
                     more = true;
                 }
             }
         }
-        if (more) return true;
-        return pop(pol, lds, spill);
+        const bool r = more || pop(pol, lds, spill);
+        if (PF && r && node >= 0) node_prefetch(nodes, node, wsl);
+        return r;
     }
 };
+typedef WalkerT<Ent8> Walker;
 
 // Heidrich's barycentric coordinates of p's projection into triangle (a, b, c), with the operation
 // order of the reference's numpy code (barycentric_coordinates_of_projection.py:31-47, called with
@@ -554,8 +598,8 @@ __device__ inline size_t cut_cell(const KnnArgs& a, const D3& q) {
     if (!(ux >= 0.0 && ux < G && uy >= 0.0 && uy < G && uz >= 0.0 && uz < G)) return kNoCell;
     return ((size_t)(unsigned)uz * (size_t)a.cut_G + (unsigned)uy) * (size_t)a.cut_G + (unsigned)ux;
 }
-template <class Pol>
-__device__ inline bool cut_start(const KnnArgs& a, size_t cell, const Pol& pol, Walker& w, uint2* __restrict__ lds,
+template <class Pol, class W>
+__device__ inline bool cut_start(const KnnArgs& a, size_t cell, const Pol& pol, W& w, typename W::Ent* __restrict__ lds,
                                  uint2* __restrict__ spill) {
     const uint4* c = reinterpret_cast<const uint4*>(a.cut + cell * kCutK);
     uint4 e[kCutK / 2];
@@ -563,7 +607,7 @@ __device__ inline bool cut_start(const KnnArgs& a, size_t cell, const Pol& pol, 
     for (int j = 0; j < kCutK / 2; ++j) e[j] = c[j];
     auto put = [&](uint32_t ref, uint32_t sb) {
         if (ref == kCutEmpty) return;
-        w.push(make_uint2(ref, sb), lds, spill);
+        w.push(ref, sb, lds, spill);
     };
 #pragma unroll
     for (int j = kCutK / 2 - 1; j >= 0; --j) {
@@ -573,18 +617,29 @@ __device__ inline bool cut_start(const KnnArgs& a, size_t cell, const Pol& pol, 
     return w.pop(pol, lds, spill);
 }
 
-template <int MODE, bool STATS, bool LIST>
+// PF (list path, trees of <= 2^20 leaves): 4-B stack entries (Ent4) and each lane's next node prefetched into LDS
+// (node_prefetch); the 16 KB the node slots take per block come out of the stack.  C3: 1889 -> 1945 M q/s in one
+// session, wave-cycles waiting on memory 55.7 -> 46.7 % at +10 VALU instructions per query
+// (profiles/r04_c3_node_prefetch_lds_ab.jsonl).
+template <int MODE, bool STATS, bool LIST, bool PF>
 __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
-    __shared__ uint2 stk[kStack * kBlock];
     constexpr bool kCompact = MODE == 0 || MODE == 3;  // per-lane queues dealt to the wave (else: per-lane rounds)
     constexpr bool kList = (MODE == 0 || MODE == 3) && LIST;  // a separate instantiation: its own registers
+    constexpr bool kPF = kList && PF;  // 4-B stack entries and nodes prefetched into LDS
+    typedef typename std::conditional<kPF, Ent4, Ent8>::type E;
+    __shared__ typename E::T stk[kStack * kBlock];
+    __shared__ float4 nbuf[kPF ? 4 * kBlock : 1];
     // compacted leaf phases: kLeafQ entries per lane; the wave leaf list shares this space (a.list)
     constexpr size_t kEntWords = kCompact && !kList ? (size_t)kBlock * kLeafQ * 2 : 1;
     constexpr size_t kListWords = kList ? 4 * (kRing + 64 * 4) : 1;  // per wave: ring + bd/bfl (u64 per lane each)
     __shared__ uint32_t lsh[kEntWords > kListWords ? kEntWords : kListWords];
     uint2* lent = reinterpret_cast<uint2*>(lsh);
     const int tid = threadIdx.x, lane = tid & 63;
-    uint2* lds = stk + tid;
+    typename E::T* lds = stk + tid;
+    // the wave's node slots (kPF): LDS byte address from a wave-uniform wave index, so M0 is set by scalar code
+    const int wv_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t wsl = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)(nbuf + (kPF ? wv_u * 256 : 0));
+    const float4* nb = nbuf + (kPF ? (tid >> 6) * 256 + lane : 0);
     uint2* ent = lent + (kCompact ? (tid >> 6) * 64 * kLeafQ : 0);
     uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
     const unsigned group = blockIdx.x & 7u;
@@ -651,9 +706,10 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
           {
             QF qf;
             const int root = query_root(a, i, q, qf);
-            Walker w{root, 0};
+            WalkerT<E> w{root, 0};
             bool start = fin;
             if (cell != kNoCell) start = cut_start(a, cell, pol, w, lds, spill);
+            if (kPF && start && w.node >= 0) node_prefetch(a.nodes, w.node, wsl);
             uint32_t* ring = lsh + (tid >> 6) * (kRing + 64 * 4);
             unsigned long long* bd = reinterpret_cast<unsigned long long*>(ring + kRing);  // per owner: d2 bits
             unsigned long long* bfl = bd + 64;                                              // (face << 32 | leaf)
@@ -732,8 +788,8 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 }
                 int l0 = -1, l1 = -1;
                 if (can) {
-                    active = w.step_collect<decltype(pol), STATS>(a.nodes, qf, pol, lds, spill, n_nodes, l0, l1,
-                                                                  kPend - nq);
+                    active = w.template step_collect<decltype(pol), STATS, kPF>(a.nodes, qf, pol, lds, spill, n_nodes,
+                                                                                  l0, l1, kPend - nq, nb, wsl);
                     ++steps;
                     if (STATS) ++tot;
                     if (active && steps >= max_steps) active = false;  // each node is entered once: corrupt tree
@@ -987,6 +1043,9 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         if (fin && (!STATS || a.res)) write_result<MODE>(a, i, q, pol);
         }
     }
+    // a lane that stopped (deferred) may still have a node prefetch in flight: it lands before the block's LDS is
+    // released
+    if constexpr (kPF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (STATS) {
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
         atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
@@ -1102,7 +1161,7 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         const int n = top;
         Walker w{0, 0};
         if (lane < n)
-            for (int j = lane + ((n - 1 - lane) / 64) * 64; j >= lane; j -= 64) w.push(W[j], lds, spill);
+            for (int j = lane + ((n - 1 - lane) / 64) * 64; j >= lane; j -= 64) w.push(W[j].x, W[j].y, lds, spill);
         bool active = w.pop(pol, lds, spill);
         while (__any(active)) {
             if (active) active = w.step<decltype(pol), false>(a.nodes, qf, pol, lds, spill, n_nodes, n_leaves);
@@ -1280,9 +1339,14 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         a.spill = ws.spill.as<uint2>();
     }
     a.budget = kBudget;
+    bool list_pf = false;  // list path with the LDS node prefetch and 4-B stack entries (k_knn PF)
     {
-        const char* e = getenv("MESH_AMD_LEAF_LIST");  // 0: per-lane leaf queues (the path of larger trees)
-        a.list = (MODE == 0 || MODE == 3) && !(e && atoi(e) == 0) && tree->B * tree->T < kListMaxLeaves;
+        // test hook: 0 per-lane leaf queues (the path of trees of >= 2^26 leaves), 2 the list without the node
+        // prefetch (the path of trees of more than 2^20 leaves)
+        const char* e = getenv("MESH_AMD_LEAF_LIST");
+        const int hook = e ? atoi(e) : 1;
+        a.list = (MODE == 0 || MODE == 3) && hook != 0 && tree->B * tree->T < kListMaxLeaves;
+        list_pf = a.list && hook != 2 && tree->B * tree->T <= kEnt4MaxLeaves;
     }
     a.max_deferred = (unsigned)std::min<size_t>(a.S, (a.S / 16) + 65536);
     DevBuf& dbuf = ws.flags;
@@ -1301,9 +1365,12 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         if (nblk == 0) return MSH_OK;
         TimedLaunch t1(name, s);
         if (a.list)
-            k_knn<MODE, STATS, (MODE == 0 || MODE == 3)><<<nblk, kBlock, 0, s>>>(a);
+            if (list_pf)
+                k_knn<MODE, STATS, (MODE == 0 || MODE == 3), (MODE == 0 || MODE == 3)><<<nblk, kBlock, 0, s>>>(a);
+            else
+                k_knn<MODE, STATS, (MODE == 0 || MODE == 3), false><<<nblk, kBlock, 0, s>>>(a);
         else
-            k_knn<MODE, STATS, false><<<nblk, kBlock, 0, s>>>(a);
+            k_knn<MODE, STATS, false, false><<<nblk, kBlock, 0, s>>>(a);
         MSH_HIP(hipGetLastError());
         return MSH_OK;
     };

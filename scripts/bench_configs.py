@@ -49,7 +49,7 @@ def pmc_traversal(target, S):
     """Measured fabric bytes per query of the closest-point traversal (pass-1 launches + pass 2) in a config's
     PMC profile: every dispatch's bytes over (traversals x S), the profile's traversals = pass-2 dispatches (the
     entry cut's traversal dropped by pmc_configs.py --skip 1)."""
-    k1, k2 = "msh::k_knn<0, false, true>", "msh::k_knn_coop<0, false>"
+    k1, k2 = "msh::k_knn<0, false, true, true>", "msh::k_knn_coop<0, false>"
     a, b = pmc_of(target, k1, 1), pmc_of(target, k2, 1)
     if "hbm_bytes_per_unit" not in a or "hbm_bytes_per_unit" not in b:
         return a if "hbm_bytes_per_unit" not in a else b

@@ -2,7 +2,7 @@
 """Register-pressure check of the closest-point traversal kernel (CPU only, no GPU needed).
 
 Compiles mesh_amd/csrc/nearest.hip to gfx950 assembly (optionally with extra -D flags) and reports, for
-k_knn<MODE, false>, the VGPR count, the spill count and how many scratch (spill) instructions sit inside
+k_knn<MODE, false, LIST, PF>, the VGPR count, the spill count and how many scratch (spill) instructions sit inside
 the tile's traversal loop (LLVM's block annotations "in Loop: ... Depth=N", N >= 2).  A spill reload
 inside that loop costs a memory round trip per iteration: A/B runs showed -13 % for two such reloads, so a
 variant with loop spills is not worth a GPU session.
@@ -31,7 +31,7 @@ def compile_asm(flags):
 
 
 def report(s, mode):
-    name = f"_ZN3msh5k_knnILi{mode}ELb0ELb{int(LIST)}EEEvNS_7KnnArgsE"
+    name = f"_ZN3msh5k_knnILi{mode}ELb0ELb{int(LIST)}ELb{int(PF)}EEEvNS_7KnnArgsE"
     meta = s[re.search(r"\.name:\s+" + name + r"\n", s).start():][:1500]
     vgpr = int(re.search(r"\.vgpr_count:\s+(\d+)", meta).group(1))
     spill = int(re.search(r"\.vgpr_spill_count:\s+(\d+)", meta).group(1))
@@ -51,16 +51,17 @@ def report(s, mode):
     return dict(mode=mode, vgpr=vgpr, vgpr_spill=spill, scratch_ops=total, scratch_in_loop=in_loop, lds=lds)
 
 
-LIST = True  # the wave-leaf-list instantiation k_knn<MODE, false, true> (the closest-point path)
+LIST = True  # the wave-leaf-list instantiation k_knn<MODE, false, true, PF> (the closest-point path)
+PF = True    # with LDS node prefetch and 4-B stack entries (trees of <= 2^20 leaves)
 
 
 def main():
-    global LIST
+    global LIST, PF
     flags = sys.argv[1:]
     s = compile_asm(flags)
-    for LIST in (True, False):
+    for LIST, PF in ((True, True), (True, False), (False, False)):
         for mode in (0, 3):
-            print(dict(report(s, mode), list=LIST))
+            print(dict(report(s, mode), list=LIST, prefetch=PF))
 
 
 if __name__ == "__main__":

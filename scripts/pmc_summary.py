@@ -23,7 +23,7 @@ import re
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TRAVERSAL = ("msh::k_knn<0, false, true>", "msh::k_knn_coop<0, false>")
+TRAVERSAL = ("msh::k_knn<0, false, true, true>", "msh::k_knn_coop<0, false>")
 
 
 def sys_path_root():

@@ -7,7 +7,7 @@ import csv
 import sqlite3
 import sys
 
-TRAVERSAL = ("k_knn<0, false, true>", "k_knn_coop<0, false>")
+TRAVERSAL = ("k_knn<0, false, true, true>", "k_knn_coop<0, false>")
 
 con = sqlite3.connect(sys.argv[1])
 with open(sys.argv[2], "w", newline="") as fh:

@@ -122,9 +122,10 @@ def test_c1_sphere_bit_exact(oracle, meshes):
     assert np.all(np.abs(dg - dc) <= 1e-9 * diag)
 
 
-@pytest.mark.parametrize("leaf_list", ["1", "0"])
+@pytest.mark.parametrize("leaf_list", ["1", "2", "0"])
 def test_c2_near_surface_bit_exact(oracle, monkeypatch, leaf_list):
-    # leaf_list 0: the per-lane leaf queues that trees of >= 2^26 leaves use instead of the wave leaf list
+    # leaf_list 1: the wave leaf list with the LDS node prefetch (trees of <= 2^20 leaves); 2: the list without it
+    # (larger trees); 0: the per-lane leaf queues that trees of >= 2^26 leaves use instead of the wave leaf list
     monkeypatch.setenv("MESH_AMD_LEAF_LIST", leaf_list)
     v, f = W.c2_mesh()
     q, _ = W.surface_samples(v, f, 20000, seed=9, sigma=0.01)
@@ -132,7 +133,7 @@ def test_c2_near_surface_bit_exact(oracle, monkeypatch, leaf_list):
     _assert_bit_exact_vs_brute(oracle, v, f, q)
 
 
-@pytest.mark.parametrize("leaf_list", ["1", "0"])
+@pytest.mark.parametrize("leaf_list", ["1", "2", "0"])
 def test_non_finite_queries(oracle, monkeypatch, leaf_list):
     # NaN / inf rows (documented deviation: the reference's CGAL call is undefined for them) answer NO_FACE,
     # part 0 and a NaN point; they sit among finite rows of a sorted launch with leader phases (C2 mesh: 13,776
@@ -154,16 +155,17 @@ def test_non_finite_queries(oracle, monkeypatch, leaf_list):
 
 
 def test_c3_sample_both_leaf_paths(oracle, monkeypatch):
-    # C3 mesh, 200k uniform queries (leader phases on): the wave leaf list and the per-lane queues give the
-    # same arrays, and both match brute force on a 2000-row sample
+    # C3 mesh, 200k uniform queries (leader phases on): the wave leaf list with and without the LDS node prefetch
+    # and the per-lane queues give the same arrays, and they match brute force on a 2000-row sample
     v, f = W.c3_mesh()
     q = np.random.default_rng(31).uniform(-1.1, 1.1, (200_000, 3))
     outs = []
-    for leaf_list in ("1", "0"):
+    for leaf_list in ("1", "2", "0"):
         monkeypatch.setenv("MESH_AMD_LEAF_LIST", leaf_list)
         outs.append(_nearest(v, f, q))
-    for a, b in zip(*outs):
-        assert np.array_equal(a, b)
+    for other in outs[1:]:
+        for a, b in zip(outs[0], other):
+            assert np.array_equal(a, b)
     rows = np.random.default_rng(32).choice(q.shape[0], 2000, replace=False)
     bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[rows])
     assert np.array_equal(outs[0][0][rows], bf) and np.array_equal(outs[0][1][rows], bp)
