@@ -266,12 +266,41 @@ constexpr size_t kEnt4MaxLeaves = (size_t)1 << 20;  // refs in [-2^20, 2^20): 21
 // A node's 64 B loaded into LDS ahead of its step (global_load_lds: no registers hold it while the lane appends
 // leaves or runs leaf rounds).  The wave's slot array holds 4 x 64 float4 (piece k of lane l at k * 64 + l); wsl =
 // its LDS byte address (wave-uniform: M0), nb = this lane's first piece.
+#ifndef MSH_PF_ASM
+#define MSH_PF_ASM 0
+#endif
+#ifndef MSH_PF_ASM_STEP
+#define MSH_PF_ASM_STEP 1008
+#endif
 __device__ inline void node_prefetch(const BNode* __restrict__ nodes, int i, uint32_t wsl) {
     const float4* g = reinterpret_cast<const float4*>(nodes + i);
+#if MSH_PF_ASM
+    // one address register and M0 stepped by scalar adds (the immediate offset also moves the LDS destination)
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_add_u32 m0, m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off offset:16\n\t"
+        "s_add_u32 m0, m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off offset:32\n\t"
+        "s_add_u32 m0, m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off offset:48\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(wsl), "i"(MSH_PF_ASM_STEP)
+        : "memory", "scc");
+#else
     typedef __attribute__((address_space(3))) void* LP;
     // (no immediate offsets: the instruction's offset moves the LDS destination too)
 #pragma unroll
     for (int k = 0; k < 4; ++k) __builtin_amdgcn_global_load_lds(g + k, (LP)(size_t)(wsl + 1024 * k), 16, 0, 0);
+#endif
 }
 __device__ inline NodeV node_from_lds(const float4* nb) {
     // the compiler does not order LDS reads after an LDS DMA: wait for it (vmcnt counts the DMA in issue order)
