@@ -266,41 +266,33 @@ constexpr size_t kEnt4MaxLeaves = (size_t)1 << 20;  // refs in [-2^20, 2^20): 21
 // A node's 64 B loaded into LDS ahead of its step (global_load_lds: no registers hold it while the lane appends
 // leaves or runs leaf rounds).  The wave's slot array holds 4 x 64 float4 (piece k of lane l at k * 64 + l); wsl =
 // its LDS byte address (wave-uniform: M0), nb = this lane's first piece.
-#ifndef MSH_PF_ASM
-#define MSH_PF_ASM 0
-#endif
-#ifndef MSH_PF_ASM_STEP
-#define MSH_PF_ASM_STEP 1008
-#endif
 __device__ inline void node_prefetch(const BNode* __restrict__ nodes, int i, uint32_t wsl) {
     const float4* g = reinterpret_cast<const float4*>(nodes + i);
-#if MSH_PF_ASM
-    // one address register and M0 stepped by scalar adds (the immediate offset also moves the LDS destination)
+    // One address register for the four pieces (immediate offsets 0, 16, 32, 48) and M0 stepped by scalar adds of
+    // 1024 - 16: the immediate offset moves the LDS destination too (tools/glds_offset_probe.hip: a lane's 16 B
+    // land at M0 + offset + 16 lane).  The builtin form (__builtin_amdgcn_global_load_lds per piece, no offsets)
+    // computed three more 64-bit addresses and reloaded three spilled M0 values per step: C3 0.6-0.7 % slower
+    // (profiles/r04_c3_prefetch_asm_lead_ab.jsonl).  The compiler does not see these loads; node_from_lds waits
+    // for them explicitly, and its own vmcnt waits stay conservative (the loads only add younger operations).
     uint32_t keep;
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %2\n\t"
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %1, off\n\t"
-        "s_add_u32 m0, m0, %3\n\t"
+        "s_add_u32 m0, m0, 0x3f0\n\t"
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %1, off offset:16\n\t"
-        "s_add_u32 m0, m0, %3\n\t"
+        "s_add_u32 m0, m0, 0x3f0\n\t"
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %1, off offset:32\n\t"
-        "s_add_u32 m0, m0, %3\n\t"
+        "s_add_u32 m0, m0, 0x3f0\n\t"
         "s_nop 0\n\t"
         "global_load_lds_dwordx4 %1, off offset:48\n\t"
         "s_mov_b32 m0, %0"
         : "=&s"(keep)
-        : "v"(g), "s"(wsl), "i"(MSH_PF_ASM_STEP)
+        : "v"(g), "s"(wsl)
         : "memory", "scc");
-#else
-    typedef __attribute__((address_space(3))) void* LP;
-    // (no immediate offsets: the instruction's offset moves the LDS destination too)
-#pragma unroll
-    for (int k = 0; k < 4; ++k) __builtin_amdgcn_global_load_lds(g + k, (LP)(size_t)(wsl + 1024 * k), 16, 0, 0);
-#endif
 }
 __device__ inline NodeV node_from_lds(const float4* nb) {
     // the compiler does not order LDS reads after an LDS DMA: wait for it (vmcnt counts the DMA in issue order)
@@ -523,12 +515,19 @@ __device__ inline D3 load_q(const KnnArgs& a, size_t i) {
 }
 
 // ---- pass-1 constants (each measured on C3 100M; A/B records in profiles/r02_*_ab.jsonl, r03_*_ab.jsonl) ----
-// Leader ordering: one leader slot per kLead slots (4: -4 %, 16: -1 %, none: -22 %), one super-leader per kLead2
+// Leader ordering: one leader slot per kLead slots (4: -4 %, 16: -1 %, none: -22 %; with the entry cut and the node
+// prefetch, 16: -1.5 %, 16 with 128-slot follower windows: -1.5 to -2 %, profiles/r04_c3_prefetch_asm_lead_ab.jsonl), one super-leader per kLead2
 // slots; super-leaders run first and unhinted, leaders take their hint from the kLWin super-leaders of their
 // window (4: -1.1 %), followers from the leaders of their kFWin-slot window (32: +-0, 128: -3 %).
-constexpr unsigned kLead = 8;
+#ifndef MSH_KLEAD
+#define MSH_KLEAD 8
+#endif
+#ifndef MSH_KFWIN
+#define MSH_KFWIN 64
+#endif
+constexpr unsigned kLead = MSH_KLEAD;
 constexpr unsigned kLead2 = 256;
-constexpr size_t kFWin = 64;
+constexpr size_t kFWin = MSH_KFWIN;
 constexpr size_t kLWin = 8;
 static_assert(kLead2 % kLead == 0 && kLead2 / kLead >= 2, "kLead2: a multiple of kLead");
 // Per-lane leaf queues (the path of trees with >= 2^26 leaves, and of the normals-metric and point modes): up
