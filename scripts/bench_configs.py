@@ -201,7 +201,7 @@ def c3np(reps):
     return {"config": "C3 icosphere (1,003,520 faces), 100M uniform host queries, aabbtree_nearest (numpy API)",
             "queries_per_s_numpy_api": q.shape[0] / res["0"][0], "ms_numpy_api": res["0"][0] * 1e3,
             "host_path": "results carved from the library's pinned pool (downloaded in place), inputs through pinned "
-                         "staging slabs filled by the library's copy workers, 32M-row chunks",
+                         "staging slabs filled by the library's copy workers, an 8M-row chunk then 20M-row chunks (host_plan)",
             "queries_per_s_numpy_api_registered": q.shape[0] / res["1"][0], "ms_numpy_api_registered": res["1"][0] * 1e3,
             "registered_equals_staged": bool(same),
             "ms_traversal_kernel": res["0"][1], "pcie_bytes_per_query": 56}
