@@ -65,6 +65,37 @@ void Workspace::release() {
     for (DevBuf* b : all) b->release();
 }
 
+// Query workspaces handed from a freed triangle tree to the next one built on the device.  A caller that builds a
+// tree per query batch — the reference's Mesh.closest_faces_and_points (mesh.py:454-455) — otherwise allocated and
+// freed the whole query workspace per call (~8 GB of device buffers at 100M queries).  free_tree gives the
+// workspace back only after the tree's work has finished; one idle workspace is kept per device, others are freed.
+class WsPool {
+  public:
+    void give(int dev, Workspace& ws) {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = idle_.find(dev);
+        if (it != idle_.end()) it->second.release();  // keep the newest
+        idle_[dev] = ws;
+        ws = Workspace{};
+    }
+    void take(int dev, Workspace& ws) {
+        std::lock_guard<std::mutex> g(mu_);
+        auto it = idle_.find(dev);
+        if (it == idle_.end()) return;
+        ws.release();
+        ws = it->second;
+        idle_.erase(it);
+    }
+
+  private:
+    std::mutex mu_;
+    std::map<int, Workspace> idle_;
+};
+static WsPool& ws_pool() {
+    static WsPool* p = new WsPool;  // never destroyed: the runtime may be gone at static destruction
+    return *p;
+}
+
 // ---- kernel timing ----
 struct Pending {
     std::string name;
@@ -168,6 +199,7 @@ static void free_tree(msh_tree* t) {
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     if (t->ws_done) (void)hipEventSynchronize(t->ws_done);
+    if (t->kind == kTriangles && t->B == 1) ws_pool().give(t->device, t->ws);
     t->ws.release();
     if (t->d_v) (void)hipFree(t->d_v);
     if (t->d_nodes) (void)hipFree(t->d_nodes);
@@ -403,6 +435,7 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
     (void)hipStreamSynchronize(s);
     dF.release(); dLo.release(); dHi.release(); dOrder.release();
     t->ws.release();  // build scratch (sort buffers, parents, ranges) is not needed by queries
+    if (st == MSH_OK) ws_pool().take(t->device, t->ws);  // a freed tree's query workspace, if one is idle
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return st;

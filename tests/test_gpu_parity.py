@@ -172,6 +172,31 @@ def test_c3_sample_both_leaf_paths(oracle, monkeypatch):
     assert np.array_equal(outs[0][2][rows], bpt)
 
 
+def test_workspace_handoff_between_trees(oracle, meshes):
+    # a freed triangle tree hands its query workspace to the next tree built on the device (api.cpp WsPool), as
+    # a tree per call (Mesh.closest_faces_and_points) does: trees built and freed in turn on two meshes answer
+    # the same arrays every round, and match brute force
+    import gc
+    vs, fs = meshes["sphere_v"], meshes["sphere_f"]
+    v2, f2 = W.c2_mesh()
+    qs = W.c1_queries(50000)
+    q2, _ = W.surface_samples(v2, f2, 300000, seed=52, sigma=0.01)  # > kSortMin rows: the sorted path
+    rounds = []
+    for _ in range(2):
+        a = _nearest(v2, f2, q2)
+        gc.collect()
+        b = _nearest(vs, fs, qs)
+        gc.collect()
+        rounds.append((a, b))
+    for x, y in zip(rounds[0][0] + rounds[0][1], rounds[1][0] + rounds[1][1]):
+        assert np.array_equal(x, y)
+    bf, bp, bpt, _ = oracle.brute_nearest(vs, fs, qs)
+    assert np.array_equal(rounds[1][1][0], bf) and np.array_equal(rounds[1][1][2], bpt)
+    rows = np.random.default_rng(53).choice(q2.shape[0], 2000, replace=False)
+    bf, bp, bpt, _ = oracle.brute_nearest(v2, f2, q2[rows])
+    assert np.array_equal(rounds[1][0][0][rows], bf) and np.array_equal(rounds[1][0][2][rows], bpt)
+
+
 def _nearest_tree(t, q):
     from mesh_amd import spatialsearch
     face, part, pt = spatialsearch.aabbtree_nearest(t, np.ascontiguousarray(q, np.float64))
