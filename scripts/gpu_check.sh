@@ -14,7 +14,6 @@ ok() {  # rc 0 = pass, 1 = test failures (no fault) -> continue; anything else -
 STAGES=${STAGES:-"smoke pytest bench prof"}
 for s in $STAGES; do
   case $s in
-    sorttest) timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -k one_sweep > gpurun_out/sorttest.log 2>&1; ok sorttest $? ;;
     sortdbg) timeout -k 10 300 python scripts/sort_debug.py ${SORT_SIZES:-} > gpurun_out/sortdbg.log 2>&1; ok sortdbg $? ;;
     pytest_rest) timeout -k 10 1200 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread ${DESELECT:-} > gpurun_out/pytest_gpu.log 2>&1; ok pytest_rest $? ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; ok smoke $? ;;
@@ -35,7 +34,6 @@ for s in $STAGES; do
         n=$(basename $so .so)
         MESH_AMD_LIB=$PWD/$so timeout -k 10 600 python scripts/bench_configs.py --configs c5 --reps 3 > gpurun_out/varc5_$n.log 2>&1; ok varc5_$n $?
       done ;;
-    bench_wide) MESH_AMD_TRAVERSAL=wide timeout -k 10 600 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_wide.log 2>&1; ok bench_wide $? ;;
     split)  MESH_AMD_STATS_DUMP=1 timeout -k 10 600 python scripts/c3_split.py > gpurun_out/split.log 2>&1; ok split $? ;;
     pytest_quick) timeout -k 10 600 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread -k "spill or cooperative or c1 or c2 or c3 or rays or alongnormal or visibility" > gpurun_out/pytest_quick.log 2>&1; ok pytest_quick $? ;;
     c5)     timeout -k 10 900 python scripts/bench_configs.py --configs c5 --reps 3 > gpurun_out/bench_c5.log 2>&1; ok c5 $? ;;
