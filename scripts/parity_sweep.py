@@ -31,6 +31,7 @@ def sweep_c3(args):
     g = torch.Generator(device="cuda:0")
     g.manual_seed(3)
     dq = (torch.rand((S, 3), generator=g, dtype=torch.float64, device="cuda:0") * 2.2 - 1.1).contiguous()
+    print("c3: stream generated", file=sys.stderr, flush=True)
     t = spatialsearch.aabbtree_compute(v, f)
     df = torch.empty(S, dtype=torch.int32, device="cuda:0")
     dp = torch.empty(S, dtype=torch.int32, device="cuda:0")
@@ -47,9 +48,9 @@ def sweep_c3(args):
                           np.argpartition(r, args.centre)[:args.centre]])
     t0 = time.perf_counter()
     chunks = []
-    for c0 in range(0, idx.size, 10000):  # progress lines: a long silent brute force looks hung on the GPU box
-        chunks.append(O.brute_nearest(v, f, q[idx[c0:c0 + 10000]]))
-        print("c3 brute force: %d / %d rows" % (min(c0 + 10000, idx.size), idx.size), file=sys.stderr, flush=True)
+    for c0 in range(0, idx.size, 2000):  # progress lines: a long silent brute force looks hung on the GPU box
+        chunks.append(O.brute_nearest(v, f, q[idx[c0:c0 + 2000]]))
+        print("c3 brute force: %d / %d rows" % (min(c0 + 2000, idx.size), idx.size), file=sys.stderr, flush=True)
     bf, bp, bpt = (np.concatenate([c[k] for c in chunks]) for k in range(3))
     bad = np.nonzero((face[idx] != bf) | (part[idx] != bp) | np.any(pt[idx] != bpt, axis=1))[0]
     return dict(workload="C3 headline stream (100M uniform queries, seed 3, device entry point)",
@@ -67,7 +68,11 @@ def sweep_c2(args):
     face, part, pt = spatialsearch.aabbtree_nearest(spatialsearch.aabbtree_compute(v, f), q)
     idx = np.random.default_rng(12).choice(q.shape[0], 5 * args.rows, replace=False)
     t0 = time.perf_counter()
-    bf, bp, bpt, _ = O.brute_nearest(v, f, q[idx])
+    chunks = []
+    for c0 in range(0, idx.size, 20000):  # progress lines (a silent minute looks hung on the GPU box)
+        chunks.append(O.brute_nearest(v, f, q[idx[c0:c0 + 20000]]))
+        print("c2 brute force: %d / %d rows" % (min(c0 + 20000, idx.size), idx.size), file=sys.stderr, flush=True)
+    bf, bp, bpt = (np.concatenate([c[k] for c in chunks]) for k in range(3))
     bad = np.nonzero((face[0][idx] != bf) | (part[0][idx] != bp) | np.any(pt[idx] != bpt, axis=1))[0]
     return dict(workload="C2 10M near-surface queries (numpy entry point aabbtree_nearest)", rows_checked=int(idx.size),
                 mismatches=int(bad.size), first_mismatch_rows=idx[bad[:10]].tolist(), brute_force_s=time.perf_counter() - t0,
