@@ -123,9 +123,11 @@ int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* 
 /* Entry cut of a triangle tree (no reference counterpart: derived acceleration data).  A grid
  * of G^3 cells over the scene box widened by 1/4, 68 B per cell (8 start entries + a hint leaf), from which
  * closest-point queries start their walks instead of the root; it changes where a walk starts, never an
- * answer.  It is built lazily, on the first closest-point query of the handle (msh_tree_nearest*,
+ * answer.  It is built lazily, on the first non-empty closest-point query of the handle (msh_tree_nearest*,
  * msh_tree_nearest_bary*, msh_tree_nearest_stats), so trees used only for rays, visibility or the normals
- * metric never hold it.  Trees of < 4096 faces never get one.
+ * metric never hold it.  Trees of < 4096 faces never get one.  That first call is synchronous, also for the
+ * *_device entry points (the cut's build waits for its own cell-centre queries): a caller that captures
+ * *_device calls in a graph or needs them asynchronous makes one small query first (or sets G = 0).
  *   G < 0: automatic grid (about 8 cells per face, at most 2^23 cells: C3 G = 200, 544 MB) — the default;
  *   G = 0: no cut (frees one already built); queries start at the root;
  *   G > 0: G^3 cells.
@@ -277,6 +279,20 @@ int msh_host_alloc(size_t bytes, void** out);
 void msh_host_free(void* p);
 int msh_host_pool_trim(void);
 size_t msh_host_pool_bytes(void);
+
+/* ---- device memory kept between handles (no reference counterpart) ----
+ * Two process-wide caches keep device memory after the handles that used it are freed, so a caller that builds
+ * a tree per call (Mesh.closest_faces_and_points, mesh.py:454-455) does not reallocate it every call:
+ *  - the query workspace of a freed triangle tree (sort keys, permutations, spill stacks, deferred lists:
+ *    ~80 B per query of its largest call, ~8 GB at 100M queries), one idle workspace per device, handed to the
+ *    next triangle tree built on that device;
+ *  - up to two idle sets of host-call staging slabs per device (three device slabs of chunk x row bytes each,
+ *    plus two page-locked host slabs).
+ * msh_device_pool_trim frees both (idle entries only: memory held by live handles stays with them);
+ * msh_device_pool_bytes reports the device bytes they hold (either pointer may be NULL).  A process that
+ * shares the GPU with other allocators (torch) calls the trim after freeing its handles. */
+int msh_device_pool_trim(void);
+int msh_device_pool_bytes(uint64_t* workspace, uint64_t* staging);
 
 #ifdef __cplusplus
 }

@@ -87,6 +87,8 @@ SIGNATURES = [
     ("msh_host_free", None, [_vp]),
     ("msh_host_pool_trim", _i, []),
     ("msh_host_pool_bytes", _sz, []),
+    ("msh_device_pool_trim", _i, []),
+    ("msh_device_pool_bytes", _i, [_c_u64_p, _c_u64_p]),
 ]
 
 
@@ -329,6 +331,18 @@ def blob_unpack(d_src, nbytes, device, stream=None, kind="triangles"):
     check(lib().msh_tree_blob_unpack(_vp(d_src), nbytes, int(device), _vp(stream) if stream else None,
                                      ctypes.byref(out)))
     return Handle(out.value, kind)
+
+
+def device_pool_trim():
+    """msh_device_pool_trim: free the idle query workspace and staging slabs kept between handles."""
+    check(lib().msh_device_pool_trim())
+
+
+def device_pool_bytes():
+    """msh_device_pool_bytes -> (workspace bytes, staging bytes) kept on the devices between handles."""
+    w, s = ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(lib().msh_device_pool_bytes(ctypes.byref(w), ctypes.byref(s)))
+    return w.value, s.value
 
 
 def timing_enable(on=True):

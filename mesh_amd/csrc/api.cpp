@@ -65,6 +65,14 @@ void Workspace::release() {
     for (DevBuf* b : all) b->release();
 }
 
+size_t Workspace::bytes() const {
+    const DevBuf* all[] = {&keys, &vals, &keys_alt, &vals_alt, &hist, &scan, &q, &n, &out_a, &out_b, &out_c, &out_d,
+                           &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w};
+    size_t t = 0;
+    for (const DevBuf* b : all) t += b->bytes;
+    return t;
+}
+
 // Query workspaces handed from a freed triangle tree to the next one built on the device.  A caller that builds a
 // tree per query batch — the reference's Mesh.closest_faces_and_points (mesh.py:454-455) — otherwise allocated and
 // freed the whole query workspace per call (~8 GB of device buffers at 100M queries).  free_tree gives the
@@ -73,18 +81,35 @@ class WsPool {
   public:
     void give(int dev, Workspace& ws) {
         std::lock_guard<std::mutex> g(mu_);
-        auto it = idle_.find(dev);
-        if (it != idle_.end()) it->second.release();  // keep the newest
-        idle_[dev] = ws;
-        ws = Workspace{};
+        idle_[dev] = std::move(ws);  // keep the newest (move-assignment frees the one it replaces)
     }
     void take(int dev, Workspace& ws) {
         std::lock_guard<std::mutex> g(mu_);
         auto it = idle_.find(dev);
         if (it == idle_.end()) return;
-        ws.release();
-        ws = it->second;
+        ws = std::move(it->second);
         idle_.erase(it);
+    }
+    // frees every idle workspace; returns the bytes released
+    size_t trim() {
+        std::lock_guard<std::mutex> g(mu_);
+        size_t n = 0;
+        int cur = 0;
+        const bool have = hipGetDevice(&cur) == hipSuccess;
+        for (auto& kv : idle_) {
+            n += kv.second.bytes();
+            (void)hipSetDevice(kv.first);
+            kv.second.release();
+        }
+        if (have) (void)hipSetDevice(cur);
+        idle_.clear();
+        return n;
+    }
+    size_t bytes() {
+        std::lock_guard<std::mutex> g(mu_);
+        size_t n = 0;
+        for (auto& kv : idle_) n += kv.second.bytes();
+        return n;
     }
 
   private:
@@ -349,7 +374,7 @@ static int build_entry_cut(msh_tree* t) {
                 st = MSH_EDEVICE;
             }
         } while (0);
-        (void)hipStreamSynchronize(s);  // the temporaries die with this scope
+        (void)hipStreamSynchronize(s);  // the temporaries are freed (DevBuf destructors) as this scope ends
     }
     if (st == MSH_OK) {
         float ms = 0.f;
@@ -435,7 +460,8 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
     (void)hipStreamSynchronize(s);
     dF.release(); dLo.release(); dHi.release(); dOrder.release();
     t->ws.release();  // build scratch (sort buffers, parents, ranges) is not needed by queries
-    if (st == MSH_OK) ws_pool().take(t->device, t->ws);  // a freed tree's query workspace, if one is idle
+    // a freed tree's query workspace, if one is idle; only kinds that give it back at free_tree take it
+    if (st == MSH_OK && t->kind == kTriangles && t->B == 1) ws_pool().take(t->device, t->ws);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return st;
@@ -457,19 +483,10 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
     *ord = QueryOrder{d_q, d_n, nullptr, nullptr};
     if (S < kSortMin) return MSH_OK;
     Workspace& ws = t->ws;
-    MSH_TRY(ws.keys.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.vals.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.keys_alt.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.vals_alt.reserve(S * sizeof(uint32_t)));
     MSH_TRY(ws.inv.reserve(S * sizeof(uint32_t)));
-    bool in_alt = false;
-    MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
-    MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
-                             ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
-    if (in_alt) {  // odd pass count: the sorted pairs are in the alt buffers; swap roles instead of copying
-        std::swap(ws.keys, ws.keys_alt);
-        std::swap(ws.vals, ws.vals_alt);
-    }
+    float lo[3], hi[3];
+    query_box(t, lo, hi);
+    MSH_TRY(query_sort(lo, hi, d_q, S, kQuerySortLo, ws, s));
     if (allow_lazy && !d_n) {
         *ord = QueryOrder{d_q, nullptr, ws.vals.as<uint32_t>(), ws.inv.as<uint32_t>(), false};
         return MSH_OK;
@@ -484,7 +501,8 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
 }
 
 // Batched trees: Morton order inside each mesh, meshes in order (two stable passes), then the gather.
-static int sort_batch_queries(msh_tree* t, const double* d_q, size_t n, size_t S, hipStream_t s, QueryOrder* ord) {
+static int sort_batch_queries(msh_tree* t, const double* d_q, size_t n, size_t S, hipStream_t s, QueryOrder* ord,
+                              size_t mesh0 = 0) {
     *ord = QueryOrder{d_q, nullptr, nullptr, nullptr};
     if (n < kSortMin) return MSH_OK;
     Workspace& ws = t->ws;
@@ -496,12 +514,13 @@ static int sort_batch_queries(msh_tree* t, const double* d_q, size_t n, size_t S
     MSH_TRY(ws.inv.reserve(n * sizeof(uint32_t)));
     uint32_t* keys = ws.keys.as<uint32_t>();
     uint32_t* vals = ws.vals.as<uint32_t>();
-    MSH_TRY(query_morton_batch(t, d_q, n, S, keys, vals, s));
+    MSH_TRY(query_morton_batch(t, d_q, n, S, keys, vals, s, mesh0));
     MSH_TRY(radix_sort_pairs(keys, vals, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n, 30, ws, s));
-    if (t->B > 1) {
+    const size_t meshes = n / S;  // of this launch
+    if (meshes > 1) {
         MSH_TRY(mesh_keys(vals, n, S, keys, s));
         int bits = 0;
-        while (bits < 32 && ((size_t)1 << bits) < t->B) ++bits;
+        while (bits < 32 && ((size_t)1 << bits) < meshes) ++bits;
         MSH_TRY(radix_sort_pairs(keys, vals, ws.keys_alt.as<uint32_t>(), ws.vals_alt.as<uint32_t>(), n, bits, ws, s));
     }
     MSH_TRY(gather_rows(d_q, nullptr, vals, n, ws.qs.as<double>(), nullptr, ws.inv.as<uint32_t>(), s));
@@ -691,6 +710,13 @@ class StagePool {
         }
     }
 
+    size_t device_bytes() {
+        std::lock_guard<std::mutex> g(mu_);
+        size_t n = 0;
+        for (auto& kv : idle_)
+            for (const StageSet& s : kv.second) n += 3 * s.dbytes;
+        return n;
+    }
     void trim() {
         std::lock_guard<std::mutex> g(mu_);
         for (auto& kv : idle_) {
@@ -776,28 +802,17 @@ static bool host_register_enabled() {
 // Measured on C3 (100M queries, results in pinned pool arrays, three device slabs; profiles/r04_c3np_plan_ab.json):
 // 32M chunks 98 ms, 24M 94-96, 16M 120, 6M + 30M 96, 4M + 12M + 28M 94-96, 8M + 16M + 32M 92-94, 12M + 28M 91,
 // 8M + 24M 89-91, 8M + 20M 86-89.  Staged outputs (caller arrays outside the pool): 16M chunks (4M 155 ms, 8M 137,
-// 16M 134, 32M 150).  Overrides: MESH_AMD_HOST_CHUNK = rows (uniform chunks), MESH_AMD_HOST_PLAN = "a,b,..." in
-// units of 2^20 rows.
+// 16M 134, 32M 150).  Test hook: MESH_AMD_HOST_CHUNK = rows (uniform chunks, so small calls run several chunks; it
+// also overrides the plans of callers whose rows are meshes or cameras).
+static size_t host_chunk_env() {
+    const char* e = getenv("MESH_AMD_HOST_CHUNK");
+    const long long c = e ? atoll(e) : 0;
+    return c > 0 ? (size_t)c : 0;
+}
 static std::vector<size_t> host_plan(bool direct_out) {
-    if (const char* e = getenv("MESH_AMD_HOST_CHUNK")) {
-        const long long c = atoll(e);
-        if (c > 0) return {(size_t)c};
-    }
-    std::vector<size_t> plan;
-    if (const char* e = getenv("MESH_AMD_HOST_PLAN")) {
-        for (const char* p = e; *p;) {
-            char* q = nullptr;
-            const double v = strtod(p, &q);
-            if (q == p) break;
-            if (v > 0) plan.push_back(std::max<size_t>(64, (size_t)(v * (double)(1 << 20))));
-            p = *q ? q + 1 : q;
-        }
-    }
-    if (plan.empty()) {
-        if (direct_out) plan = {(size_t)8 << 20, (size_t)20 << 20};
-        else plan = {(size_t)16 << 20};
-    }
-    return plan;
+    if (const size_t c = host_chunk_env()) return {c};
+    if (direct_out) return {(size_t)8 << 20, (size_t)20 << 20};
+    return {(size_t)16 << 20};
 }
 
 // Page-locked result pool (msh_host_alloc / msh_host_free, meshsearch.h).  Blocks are hipHostMalloc'd in 2-MB
@@ -945,8 +960,11 @@ static int pipelined_registered(msh_tree* t, size_t S, const std::vector<HostArr
     return st;
 }
 
+// plan_rows (optional): the chunk plan in rows (the last entry repeated) instead of host_plan's, for callers whose
+// rows are whole meshes (batched trees) or cameras (visibility)
 template <class Run>
-static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Run run) {
+static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Run run,
+                     const std::vector<size_t>* plan_rows = nullptr) {
     size_t row = 0, in_end = 0;  // in_end: the inputs' share of a slab row (they come first)
     for (const HostArr& a : arrs) {
         row += a.row_bytes;
@@ -990,9 +1008,10 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
     // chunks (host_plan): first rows c0s[k], rows cns[k]; slabs are sized for the largest
     std::vector<size_t> c0s, cns;
     {
-        const std::vector<size_t> plan = host_plan(direct_out);
+        const std::vector<size_t> plan =
+            plan_rows && !plan_rows->empty() && !host_chunk_env() ? *plan_rows : host_plan(direct_out);
         for (size_t r = 0, j = 0; r < S; ++j) {
-            const size_t n = std::min(plan[std::min(j, plan.size() - 1)], S - r);
+            const size_t n = std::min(std::max<size_t>(1, plan[std::min(j, plan.size() - 1)]), S - r);
             c0s.push_back(r);
             cns.push_back(n);
             r += n;
@@ -1272,15 +1291,10 @@ int msh_tree_query_order(msh_tree* t, const double* d_q, size_t S, uint32_t* d_p
     hipStream_t s = pick(t, stream);
     WsOrder order(t, s);
     Workspace& ws = t->ws;
-    MSH_TRY(ws.keys.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.vals.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.keys_alt.reserve(S * sizeof(uint32_t)));
-    MSH_TRY(ws.vals_alt.reserve(S * sizeof(uint32_t)));
-    bool in_alt = false;
-    MSH_TRY(query_morton(t, d_q, S, ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), s));
-    MSH_TRY(radix_sort_pairs(ws.keys.as<uint32_t>(), ws.vals.as<uint32_t>(), ws.keys_alt.as<uint32_t>(),
-                             ws.vals_alt.as<uint32_t>(), S, 30 - kQuerySortLo, ws, s, kQuerySortLo, &in_alt));
-    MSH_HIP(hipMemcpyAsync(d_perm, in_alt ? ws.vals_alt.ptr : ws.vals.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    float lo[3], hi[3];
+    query_box(t, lo, hi);
+    MSH_TRY(query_sort(lo, hi, d_q, S, kQuerySortLo, ws, s));
+    MSH_HIP(hipMemcpyAsync(d_perm, ws.vals.ptr, S * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     return MSH_OK;
 }
 
@@ -1333,8 +1347,9 @@ int msh_tree_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* 
                             void* stream) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_device"));
     MSH_TRY(check_count(S, "msh_tree_nearest_device"));
-    ensure_entry_cut(t);
     if (S == 0) return MSH_OK;
+    if (!d_q || !d_face || !d_pt) { set_error("msh_tree_nearest_device: null argument"); return MSH_EINVAL; }
+    ensure_entry_cut(t);
     hipStream_t s = pick(t, stream);
     WsOrder order(t, s);
     QueryOrder ord;
@@ -1346,9 +1361,9 @@ int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint3
                                  void* stream) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_bary_device"));
     MSH_TRY(check_count(S, "msh_tree_nearest_bary_device"));
-    ensure_entry_cut(t);
     if (S == 0) return MSH_OK;
     if (!d_w) { set_error("msh_tree_nearest_bary_device: null weights"); return MSH_EINVAL; }
+    ensure_entry_cut(t);
     hipStream_t s = pick(t, stream);
     WsOrder order(t, s);
     QueryOrder ord;
@@ -1359,9 +1374,9 @@ int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint3
 int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest"));
     MSH_TRY(check_count(S, "msh_tree_nearest"));
-    ensure_entry_cut(t);
     if (S == 0) return MSH_OK;
     if (!q || !face || !pt) { set_error("msh_tree_nearest: null argument"); return MSH_EINVAL; }
+    ensure_entry_cut(t);
     // rows: q (24 B in) | face (4 B out) | part (4 B out) | point (24 B out)
     const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, part, 4}, {nullptr, pt, 24}};
     return pipelined(t, S, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
@@ -1374,9 +1389,9 @@ int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uin
 int msh_tree_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face, double* pt, double* w) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_bary"));
     MSH_TRY(check_count(S, "msh_tree_nearest_bary"));
-    ensure_entry_cut(t);
     if (S == 0) return MSH_OK;
     if (!q || !face || !pt || !w) { set_error("msh_tree_nearest_bary: null argument"); return MSH_EINVAL; }
+    ensure_entry_cut(t);
     const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, pt, 24}, {nullptr, w, 24}};
     return pipelined(t, S, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
         return msh_tree_nearest_bary_device(t, reinterpret_cast<const double*>(d[0]), n, reinterpret_cast<uint32_t*>(d[1]),
@@ -1387,10 +1402,10 @@ int msh_tree_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face
 int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* nodes, uint64_t* leaves) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_stats"));
     MSH_TRY(check_count(S, "msh_tree_nearest_stats"));
-    ensure_entry_cut(t);
     *nodes = 0;
     *leaves = 0;
     if (S == 0) return MSH_OK;
+    ensure_entry_cut(t);
     hipStream_t s = t->stream;
     unsigned long long h[48] = {0};
     {
@@ -1602,34 +1617,32 @@ int msh_visibility_device(msh_tree* t, const double* d_cams, size_t C, const dou
     return launch_visibility(t, d_cams, C, d_normals, d_sensors, min_dist, v_begin, v_count, d_vis, d_ndc, s);
 }
 
+// Host arrays: the cameras, normals and sensors are uploaded once; the (C, P) outputs come back through the pinned
+// pipeline a few cameras at a time (api.cpp pipelined(): rows = cameras), so the downloads of earlier cameras (C5:
+// 30 MB per camera, 1.92 GB in all) overlap the rays of later ones, and land straight in page-locked pool arrays
+// when the caller's arrays are carved from it.
 int msh_visibility(msh_tree* t, const double* cams, size_t C, const double* normals, const double* sensors,
                    double min_dist, uint32_t* vis, double* ndc) {
     MSH_TRY(check_tree(t, kTriangles, "msh_visibility"));
-    const size_t n = C * t->P;
-    if (n == 0) return MSH_OK;
+    const size_t P = t->P;
+    if (C * P == 0) return MSH_OK;
+    if (!cams || !vis || !ndc) { set_error("msh_visibility: null argument"); return MSH_EINVAL; }
     hipStream_t s = t->stream;
-    DevBuf dc, dn, ds, dv, dd;
+    DevBuf dc, dn, ds;
     int st = MSH_OK;
     do {
         if ((st = upload(dc, cams, 3 * C, s)) != MSH_OK) break;
-        if (normals && (st = upload(dn, normals, 3 * t->P, s)) != MSH_OK) break;
+        if (normals && (st = upload(dn, normals, 3 * P, s)) != MSH_OK) break;
         if (sensors && (st = upload(ds, sensors, 9 * C, s)) != MSH_OK) break;
-        if ((st = dv.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
-        if ((st = dd.reserve(n * sizeof(double))) != MSH_OK) break;
-        if ((st = msh_visibility_device(t, dc.as<double>(), C, normals ? dn.as<double>() : nullptr,
-                                        sensors ? ds.as<double>() : nullptr, min_dist, 0, t->P, dv.as<uint32_t>(),
-                                        dd.as<double>(), s)) != MSH_OK)
-            break;
-        hipError_t e;
-        if ((e = hipMemcpyAsync(vis, dv.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipMemcpyAsync(ndc, dd.ptr, n * sizeof(double), hipMemcpyDeviceToHost, s)) != hipSuccess ||
-            (e = hipStreamSynchronize(s)) != hipSuccess) {
-            set_error("visibility: %s", hipGetErrorString(e));
-            st = MSH_EDEVICE;
-        }
+        const std::vector<HostArr> arrs = {{nullptr, vis, P * sizeof(uint32_t)}, {nullptr, ndc, P * sizeof(double)}};
+        const std::vector<size_t> plan = {std::max<size_t>(1, ((size_t)16 << 20) / P)};  // ~16M rays a chunk
+        st = pipelined(t, C, arrs, [&](size_t c0, size_t nc, const std::vector<char*>& d) {
+            return msh_visibility_device(t, dc.as<double>() + 3 * c0, nc, normals ? dn.as<double>() : nullptr,
+                                         sensors ? ds.as<double>() + 9 * c0 : nullptr, min_dist, 0, P,
+                                         reinterpret_cast<uint32_t*>(d[0]), reinterpret_cast<double*>(d[1]), s);
+        }, &plan);
     } while (0);
     (void)hipStreamSynchronize(s);
-    dc.release(); dn.release(); ds.release(); dv.release(); dd.release();
     return st;
 }
 
@@ -1939,6 +1952,18 @@ int msh_host_pool_trim(void) {
 
 size_t msh_host_pool_bytes(void) { return pinned_pool().bytes(); }
 
+int msh_device_pool_trim(void) {
+    ws_pool().trim();
+    stage_pool().trim();
+    return MSH_OK;
+}
+
+int msh_device_pool_bytes(uint64_t* workspace, uint64_t* staging) {
+    if (workspace) *workspace = ws_pool().bytes();
+    if (staging) *staging = stage_pool().device_bytes();
+    return MSH_OK;
+}
+
 int msh_timing_reset(void) {
     resolve_pending();
     std::lock_guard<std::mutex> g(g_tmu);
@@ -1977,8 +2002,14 @@ int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size
         if (e == hipSuccess) e = hipMalloc(&t->d_nodes, B * (T - 1) * sizeof(BNode));
         if (e == hipSuccess) e = hipMalloc(&t->d_leaves, B * T * sizeof(TriRec));
         if (e != hipSuccess) { set_error("msh_batch_build: %s", hipGetErrorString(e)); st = MSH_ENOMEM; break; }
-        e = hipMemcpyAsync(t->d_v, v, B * P * 3 * sizeof(double), hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) { set_error("msh_batch_build: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
+        // the vertices (C4: 496 MB) through the pinned staging pipeline, a chunk of meshes at a time (one pageable
+        // hipMemcpy of them ran well below the host link's rate)
+        const std::vector<HostArr> va = {{v, nullptr, P * 3 * sizeof(double)}};
+        st = pipelined(t, B, va, [&](size_t m0, size_t nm, const std::vector<char*>& d) {
+            MSH_HIP(hipMemcpyAsync(t->d_v + m0 * P * 3, d[0], nm * P * 3 * sizeof(double), hipMemcpyDeviceToDevice, s));
+            return MSH_OK;
+        });
+        if (st != MSH_OK) break;
         if ((st = upload(dF, f, 3 * T, s)) != MSH_OK) break;
         if ((st = dLo.reserve(3 * B * T * sizeof(double))) != MSH_OK) break;
         if ((st = dHi.reserve(3 * B * T * sizeof(double))) != MSH_OK) break;
@@ -2013,16 +2044,23 @@ int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size
     return MSH_OK;
 }
 
+// meshes [mesh0, mesh0 + nmesh) of a batched tree; d_q and the outputs hold those meshes' rows only
+static int batch_query_range(msh_tree* t, const double* d_q, size_t S, size_t mesh0, size_t nmesh, const SlotOut& o,
+                             hipStream_t s) {
+    const size_t n = nmesh * S;
+    if (n == 0) return MSH_OK;
+    WsOrder order(t, s);
+    QueryOrder ord;
+    MSH_TRY(sort_batch_queries(t, d_q, n, S, s, &ord, mesh0));
+    return launch_nearest_batch(t, ord, n, S, o, s, mesh0);
+}
+
 static int batch_query(msh_tree* t, const double* d_q, size_t S, const SlotOut& o, void* stream, const char* fn) {
     MSH_TRY(check_batch(t, fn));
     const size_t n = t->B * S;
     if (n == 0) return MSH_OK;
     MSH_TRY(check_count(n, fn));
-    hipStream_t s = pick(t, stream);
-    WsOrder order(t, s);
-    QueryOrder ord;
-    MSH_TRY(sort_batch_queries(t, d_q, n, S, s, &ord));
-    return launch_nearest_batch(t, ord, n, S, o, s);
+    return batch_query_range(t, d_q, S, 0, t->B, o, pick(t, stream));
 }
 
 int msh_batch_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part, double* d_pt,
@@ -2036,6 +2074,11 @@ int msh_batch_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint
     return batch_query(t, d_q, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_w}, stream, "msh_batch_nearest_bary_device");
 }
 
+// Host arrays of a batched tree, pipelined over meshes (api.cpp pipelined(): a chunk is a range of whole meshes, so
+// its queries sort and run as the meshes' own launch): uploads, kernels and downloads of consecutive chunks overlap,
+// and results go straight into page-locked pool arrays (msh_host_alloc) when the caller's arrays are carved from it.
+// C4 (4096 meshes x 10k queries): one pageable upload of 983 MB and downloads of 1.3 GB had made the call 4x slower
+// than its host-link bound.
 static int batch_host(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt, double* w,
                       const char* fn) {
     MSH_TRY(check_batch(t, fn));
@@ -2043,37 +2086,22 @@ static int batch_host(msh_tree* t, const double* q, size_t S, uint32_t* face, ui
     if (n == 0) return MSH_OK;
     MSH_TRY(check_count(n, fn));
     if (!q || !face || !pt) { set_error("%s: null argument", fn); return MSH_EINVAL; }
-    hipStream_t s = t->stream;
-    Workspace& ws = t->ws;
-    int st = MSH_OK;
-    {
-        WsOrder order(t, s);
-        do {
-            if ((st = upload(ws.q, q, 3 * n, s)) != MSH_OK) break;
-            if ((st = ws.out_a.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
-            if ((st = ws.out_b.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
-            if ((st = ws.out_c.reserve(3 * n * sizeof(double))) != MSH_OK) break;
-            if (w && (st = ws.out_d.reserve(3 * n * sizeof(double))) != MSH_OK) break;
-            const SlotOut o{ws.out_a.as<uint32_t>(), part && !w ? ws.out_b.as<uint32_t>() : nullptr, ws.out_c.as<double>(),
-                            nullptr, w ? ws.out_d.as<double>() : nullptr};
-            QueryOrder ord;
-            if ((st = sort_batch_queries(t, ws.q.as<double>(), n, S, s, &ord)) != MSH_OK) break;
-            if ((st = launch_nearest_batch(t, ord, n, S, o, s)) != MSH_OK) break;
-            hipError_t e = hipMemcpyAsync(face, ws.out_a.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess && o.part) e = hipMemcpyAsync(part, ws.out_b.ptr, n * sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(pt, ws.out_c.ptr, 3 * n * sizeof(double), hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess && w) e = hipMemcpyAsync(w, ws.out_d.ptr, 3 * n * sizeof(double), hipMemcpyDeviceToHost, s);
-            if (e != hipSuccess) {
-                set_error("%s: %s", fn, hipGetErrorString(e));
-                st = MSH_EDEVICE;
-            }
-        } while (0);
-    }
-    if (hipStreamSynchronize(s) != hipSuccess && st == MSH_OK) {
-        set_error("%s: kernel failure", fn);
-        st = MSH_EDEVICE;
-    }
-    return st;
+    if (w) part = nullptr;
+    // rows = meshes: q (24 S B in) | face (4 S out) | [part (4 S out)] | point (24 S out) | [weights (24 S out)]
+    std::vector<HostArr> arrs = {{q, nullptr, 24 * S}, {nullptr, face, 4 * S}};
+    const int ipart = part ? (int)arrs.size() : -1;
+    if (part) arrs.push_back({nullptr, part, 4 * S});
+    const int ipt = (int)arrs.size();
+    arrs.push_back({nullptr, pt, 24 * S});
+    const int iw = w ? (int)arrs.size() : -1;
+    if (w) arrs.push_back({nullptr, w, 24 * S});
+    // chunks of ~2M then ~6M queries (whole meshes)
+    const std::vector<size_t> plan = {std::max<size_t>(1, ((size_t)2 << 20) / S), std::max<size_t>(1, ((size_t)6 << 20) / S)};
+    return pipelined(t, t->B, arrs, [&](size_t m0, size_t nm, const std::vector<char*>& d) {
+        const SlotOut o{reinterpret_cast<uint32_t*>(d[1]), ipart >= 0 ? reinterpret_cast<uint32_t*>(d[ipart]) : nullptr,
+                        reinterpret_cast<double*>(d[ipt]), nullptr, iw >= 0 ? reinterpret_cast<double*>(d[iw]) : nullptr};
+        return batch_query_range(t, reinterpret_cast<const double*>(d[0]), S, m0, nm, o, t->stream);
+    }, &plan);
 }
 
 int msh_batch_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {

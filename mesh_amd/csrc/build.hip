@@ -974,8 +974,8 @@ int mesh_keys(const uint32_t* vals, size_t n, size_t per, uint32_t* keys, hipStr
 }
 
 int query_morton_batch(const msh_tree* tree, const double* d_q, size_t n, size_t S, uint32_t* keys, uint32_t* vals,
-                       hipStream_t s) {
-    k_query_morton_batch<<<nblocks(n), kBlock, 0, s>>>(d_q, n, S, tree->d_boxes, keys, vals);
+                       hipStream_t s, size_t mesh0) {
+    k_query_morton_batch<<<nblocks(n), kBlock, 0, s>>>(d_q, n, S, tree->d_boxes + 6 * mesh0, keys, vals);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }

@@ -29,10 +29,26 @@ void set_error(const char* fmt, ...);
         if (_s != MSH_OK) return _s; \
     } while (0)
 
-// Grow-only device scratch buffer.
+// Grow-only device scratch buffer.  Owning and move-only: a scope's buffers are freed when it ends (hipFree
+// waits for the device, so a buffer still read by queued launches is not released under them).
 struct DevBuf {
     void* ptr = nullptr;
     size_t bytes = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    DevBuf(DevBuf&& o) noexcept : ptr(o.ptr), bytes(o.bytes) { o.ptr = nullptr; o.bytes = 0; }
+    DevBuf& operator=(DevBuf&& o) noexcept {
+        if (this != &o) {
+            release();
+            ptr = o.ptr;
+            bytes = o.bytes;
+            o.ptr = nullptr;
+            o.bytes = 0;
+        }
+        return *this;
+    }
+    ~DevBuf() { release(); }
     int reserve(size_t need);
     void release();
     template <class T>
@@ -45,6 +61,7 @@ struct Workspace {
     DevBuf keys, vals, keys_alt, vals_alt, hist, scan, q, n, out_a, out_b, out_c, out_d, flags, counters, spill, stats,
         ranges, qs, ns, inv, res, res_w;
     void release();
+    size_t bytes() const;
 };
 
 enum Kind { kTriangles = 0, kNormals = 1, kPoints = 2 };
@@ -155,9 +172,9 @@ int tri_bounds_batch(const double* d_v, size_t P, const uint32_t* d_f, size_t B,
                      hipStream_t s);
 int pack_tri_leaves_batch(const double* d_v, size_t P, const uint32_t* d_f, const uint32_t* d_order, size_t B, size_t T,
                           TriRec* d_out, hipStream_t s);
-// Morton codes of (B*S,3) queries in their mesh's box (query i belongs to mesh i / S) + iota values.
+// Morton codes of (B*S,3) queries in their mesh's box (query i belongs to mesh mesh0 + i / S) + iota values.
 int query_morton_batch(const msh_tree* tree, const double* d_q, size_t n, size_t S, uint32_t* keys, uint32_t* vals,
-                       hipStream_t s);
+                       hipStream_t s, size_t mesh0 = 0);
 // keys[j] = vals[j] / per (the mesh of element vals[j]), for the second, per-mesh sort phase
 int mesh_keys(const uint32_t* vals, size_t n, size_t per, uint32_t* keys, hipStream_t s);
 // largest distance from origin to a corner of box (lo xyz, hi xyz): msh_tree::half_diag
@@ -178,6 +195,11 @@ int point_bounds(const double* d_v, size_t P, double* d_lo, double* d_hi, hipStr
 // ---- queries (nearest.hip) ----
 // 30-bit Morton codes of query points in the tree's scene box + iota values.
 int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* keys, uint32_t* vals, hipStream_t s);
+// the box query Morton codes are taken in: the scene box widened by 10 % of its extent per side
+void query_box(const msh_tree* tree, float* lo, float* hi);
+// Query order (sort.hip): the S rows stably sorted by the top 30 - lo_bit bits (<= 24) of their Morton codes in the
+// box lo..hi; the permutation (slot -> row) ends in ws.vals.  Uses ws.keys, ws.keys_alt, ws.vals_alt, ws.hist.
+int query_sort(const float* lo, const float* hi, const double* d_q, size_t S, int lo_bit, Workspace& ws, hipStream_t s);
 // slot i <- rows perm[i] of a (and b when non-null); inv[perm[i]] = i
 int gather_rows(const double* d_a, const double* d_b, const uint32_t* d_perm, size_t S, double* d_as, double* d_bs,
                 uint32_t* d_inv, hipStream_t s);
@@ -193,9 +215,9 @@ int cut_build(msh_tree* tree, int G, const double* lo, const double* w, const do
 int cut_hints(const msh_tree* tree, const uint32_t* d_face, size_t n, uint32_t* d_inv, int* d_hint, hipStream_t s);
 // closest point: o.face, o.part (nullable), o.pt; with o.w (3 per row) the barycentric variant (part unused)
 int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s);
-// batched trees: n = B*S queries, slot i answered on mesh i / S (the batched sort is mesh-major)
+// batched trees: n = (meshes) * S queries, slot i answered on mesh mesh0 + i / S (the batched sort is mesh-major)
 int launch_nearest_batch(const msh_tree* tree, const QueryOrder& ord, size_t n, size_t S, const SlotOut& o,
-                         hipStream_t s);
+                         hipStream_t s, size_t mesh0 = 0);
 int launch_nearest_stats(const msh_tree* tree, const QueryOrder& ord, size_t S, unsigned long long* d_counts,
                          hipStream_t s);
 // normals metric: o.face, o.pt; ord.n = query normals in slot order

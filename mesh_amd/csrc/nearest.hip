@@ -82,6 +82,7 @@ struct KnnArgs {
     const double* orgs;
     size_t qper;
     size_t npm;
+    size_t root0;  // batched trees: root of the launch's first mesh (a launch over meshes [mesh0, ...): mesh0 * npm)
     unsigned* counters;
     unsigned ntiles;
     uint2* spill;
@@ -117,7 +118,7 @@ __device__ inline int query_root(const KnnArgs& a, size_t i, const D3& q, QF& qf
         const size_t mb = i / a.qper;
         const double o[3] = {a.orgs[3 * mb], a.orgs[3 * mb + 1], a.orgs[3 * mb + 2]};
         qf = make_qf(q, o, a.tm);
-        return (int)(mb * a.npm);
+        return (int)(a.root0 + mb * a.npm);
     }
     const double o[3] = {a.org[0], a.org[1], a.org[2]};
     qf = make_qf(q, o, a.tm);
@@ -525,6 +526,9 @@ __device__ inline D3 load_q(const KnnArgs& a, size_t i) {
 #ifndef MSH_KFWIN
 #define MSH_KFWIN 64
 #endif
+#ifndef MSH_FOLLOW_CELL
+#define MSH_FOLLOW_CELL 0
+#endif
 constexpr unsigned kLead = MSH_KLEAD;
 constexpr unsigned kLead2 = 256;
 constexpr size_t kFWin = MSH_KFWIN;
@@ -713,6 +717,19 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             } else if (fin && (a.phase == 2 || a.phase == 1)) {
                 const int lf = a.phase == 2 ? leader_leaf(a, i, q, kFWin, kLead) : leader_leaf(a, i, q, kLWin * kLead2, kLead2);
                 if (STATS) hint_leaf = lf;
+#if MSH_FOLLOW_CELL
+                // followers inside the grid also test their cell's hint leaf (one call site: a loop of two)
+                const int lc = (kList && a.cut_hint && cell != kNoCell) ? a.cut_hint[cell] : -1;
+#pragma nounroll
+                for (int j = 0; j < 2; ++j) {
+                    const int h = j == 0 ? lf : (lc != lf ? lc : -1);
+                    if (h >= 0) {
+                        pol.test(h);
+                        if (STATS) ++n_leaves;
+                    }
+                }
+                if (STATS && lf >= 0) ++n_hinted;
+#else
                 if (lf >= 0) {
                     pol.test(lf);
                     if (STATS) {
@@ -720,6 +737,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                         ++n_hinted;
                     }
                 }
+#endif
             }
         }
         if (a.T == 1) {
@@ -1235,6 +1253,14 @@ __global__ __launch_bounds__(kBlock) void k_query_morton(const double* __restric
 }
 
 constexpr float kQueryBoxMargin = 0.1f;
+void query_box(const msh_tree* tree, float* lo, float* hi) {
+    for (int k = 0; k < 3; ++k) {
+        const float e = tree->scene_hi[k] - tree->scene_lo[k];
+        lo[k] = tree->scene_lo[k] - kQueryBoxMargin * e;
+        hi[k] = tree->scene_hi[k] + kQueryBoxMargin * e;
+    }
+}
+
 int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* keys, uint32_t* vals, hipStream_t s) {
     if (S == 0) return MSH_OK;
     TimedLaunch tl("morton", s);
@@ -1244,11 +1270,7 @@ int query_morton(const msh_tree* tree, const double* d_q, size_t S, uint32_t* ke
     // the unit sphere's box; 1143 -> 1154-1158 M q/s for 5-20 % margins; a reduction over the queries to
     // fit the box exactly cost 0.9 ms and gained nothing net)
     float lo[3], hi[3];
-    for (int k = 0; k < 3; ++k) {
-        const float e = tree->scene_hi[k] - tree->scene_lo[k];
-        lo[k] = tree->scene_lo[k] - kQueryBoxMargin * e;
-        hi[k] = tree->scene_hi[k] + kQueryBoxMargin * e;
-    }
+    query_box(tree, lo, hi);
     k_query_morton<<<(unsigned)((S + kBlock - 1) / kBlock), kBlock, 0, s>>>(d_q, S, lo[0], lo[1], lo[2], hi[0], hi[1],
                                                                            hi[2], keys, vals);
     MSH_HIP(hipGetLastError());
@@ -1513,11 +1535,12 @@ int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const 
 }
 
 int launch_nearest_batch(const msh_tree* tree, const QueryOrder& ord, size_t n, size_t S, const SlotOut& o,
-                         hipStream_t s) {
+                         hipStream_t s, size_t mesh0) {
     KnnArgs a = tree_args(tree, n);
-    a.orgs = tree->d_orgs;
+    a.orgs = tree->d_orgs + 3 * mesh0;
     a.qper = S;
     a.npm = tree->T - 1;
+    a.root0 = mesh0 * a.npm;
     SlotOut oo = o;
     oo.dist = nullptr;
     if (o.w) {

@@ -223,4 +223,203 @@ int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_
     return MSH_OK;
 }
 
+
+// ---- query order: stable sort of query rows by the top 24 bits of their 30-bit Morton codes ----
+// Specialised for the query path (3 passes of 8 bits, values = row indices), so the passes move fewer bytes than
+// radix_sort_pairs does with the same ballot ranking:
+//   k_qkeys      Morton key of every row + the first pass's per-tile digit counts (no separate histogram read);
+//   pass 1       u32 keys in, rows implied by the index (no value array is written or read), packed u64 out
+//                (key << 32 | row: one 8-B store per element, so a digit run of a tile is twice as long in
+//                bytes as two 4-B arrays);
+//   pass 2       packed in, packed out;   pass 3  packed in, rows only out (the keys are not needed after it).
+// Tiles of kQsNT x 16 elements: with 1024-thread blocks a tile's 256 digit runs average 64 elements (512 B
+// packed), so the scattered stores are mostly whole lines.  HBM bytes per element: 24 (rows) + 4 (keys) in
+// k_qkeys; 4 + 8 in pass 1; 8 (histogram) + 8 + 8 in pass 2; 8 + 8 + 4 in pass 3.
+#ifndef MSH_QSORT_NT
+#define MSH_QSORT_NT 1024
+#endif
+constexpr int kQsNT = MSH_QSORT_NT;
+constexpr int kQsItems = 16;
+constexpr int kQsTile = kQsNT * kQsItems;
+
+template <int NT, int ITEMS>
+__global__ __launch_bounds__(NT) void k_qkeys(const double* __restrict__ q, size_t n, int lo_bit, float lx, float ly,
+                                              float lz, float hx, float hy, float hz, uint32_t* __restrict__ keys,
+                                              uint32_t* __restrict__ hist, unsigned nb) {
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t h[NW][256];
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int i = tid; i < NW * 256; i += NT) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * (NT * ITEMS);
+#pragma unroll 4
+    for (int k = 0; k < ITEMS; ++k) {
+        const size_t i = base + (size_t)k * NT + tid;
+        if (i < n) {
+            const uint32_t key = query_morton30(q[3 * i], q[3 * i + 1], q[3 * i + 2], lx, ly, lz, hx, hy, hz) >> lo_bit;
+            keys[i] = key;
+            atomicAdd(&h[w][key & 255u], 1u);
+        }
+    }
+    __syncthreads();
+    for (int d = tid; d < 256; d += NT) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int x = 0; x < NW; ++x) c += h[x][d];
+        hist[(size_t)d * nb + blockIdx.x] = c;
+    }
+}
+
+template <int NT, int ITEMS>
+__global__ __launch_bounds__(NT) void k_qhist64(const unsigned long long* __restrict__ in, size_t n, int shift,
+                                                uint32_t* __restrict__ hist, unsigned nb) {
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t h[NW][256];
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int i = tid; i < NW * 256; i += NT) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * (NT * ITEMS);
+    unsigned long long e[ITEMS];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const size_t i = base + (size_t)k * NT + tid;
+        e[k] = i < n ? in[i] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k)
+        if (e[k] != ~0ull) atomicAdd(&h[w][(uint32_t)(e[k] >> (32 + shift)) & 255u], 1u);
+    __syncthreads();
+    for (int d = tid; d < 256; d += NT) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int x = 0; x < NW; ++x) c += h[x][d];
+        hist[(size_t)d * nb + blockIdx.x] = c;
+    }
+}
+
+// One stable pass on digit (key >> shift) & 255.  IN64: packed input, else u32 keys whose row is the index.
+// OUT64: packed output, else the rows only.  Ranking as k_scatter: eight ballots per element give its rank among
+// the wave's equal digits; per-wave digit counts are scanned over the block, the tile is staged in LDS in its
+// sorted order and written out linearly (each digit run of the tile contiguous).
+template <int NT, int ITEMS, bool IN64, bool OUT64>
+__global__ __launch_bounds__(NT) void k_qscatter(const void* __restrict__ in, void* __restrict__ out, size_t n, int shift,
+                                                 const uint32_t* __restrict__ offs, unsigned nb) {
+    constexpr int NW = NT / 64, TILE = NT * ITEMS, WI = 64 * ITEMS;
+    static_assert(NT >= 256, "one thread per digit");
+    __shared__ uint32_t wcnt[NW][256];
+    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t ssum[4];
+    __shared__ unsigned long long stage[TILE];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    for (int i = tid; i < NW * 256; i += NT) (&wcnt[0][0])[i] = 0;
+    const uint32_t g_off = tid < 256 ? offs[(size_t)tid * nb + blockIdx.x] : 0u;
+    __syncthreads();
+    const size_t tile0 = (size_t)blockIdx.x * TILE;
+    const size_t base = tile0 + (size_t)w * WI;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const unsigned long long* in64 = static_cast<const unsigned long long*>(in);
+    const uint32_t* in32 = static_cast<const uint32_t*>(in);
+    unsigned long long ee[ITEMS];
+    uint32_t rr[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const size_t i = base + (size_t)it * 64 + lane;
+        ee[it] = i < n ? (IN64 ? in64[i] : (((unsigned long long)in32[i] << 32) | (uint32_t)i)) : 0ull;
+    }
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const size_t i = base + (size_t)it * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = (uint32_t)(ee[it] >> (32 + shift)) & 255u;
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const unsigned long long m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t prev = valid ? wcnt[w][d] : 0u;
+        if (valid && (peers & lt) == 0ull) wcnt[w][d] = prev + (uint32_t)__popcll(peers);
+        rr[it] = prev + (uint32_t)__popcll(peers & lt);
+    }
+    __syncthreads();
+    // digit tid (< 256): the tile's count, its exclusive scan over the digits, then each wave's start inside the run
+    uint32_t tot = 0;
+    if (tid < 256) {
+#pragma unroll
+        for (int x = 0; x < NW; ++x) tot += wcnt[x][tid];
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (w < 4 && lane == 63) ssum[w] = incl;
+    __syncthreads();
+    if (tid < 256) {
+        uint32_t run = incl - tot;
+        for (int k = 0; k < w; ++k) run += ssum[k];
+        gbase[tid] = g_off - run;
+#pragma unroll
+        for (int x = 0; x < NW; ++x) {
+            const uint32_t c = wcnt[x][tid];
+            wcnt[x][tid] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const size_t i = base + (size_t)it * 64 + lane;
+        if (i < n) stage[wcnt[w][(uint32_t)(ee[it] >> (32 + shift)) & 255u] + rr[it]] = ee[it];
+    }
+    __syncthreads();
+    const uint32_t tn = (uint32_t)(n - tile0 < (size_t)TILE ? n - tile0 : (size_t)TILE);
+    for (uint32_t p = tid; p < tn; p += NT) {
+        const unsigned long long e = stage[p];
+        const uint32_t dst = gbase[(uint32_t)(e >> (32 + shift)) & 255u] + p;
+        if (OUT64) static_cast<unsigned long long*>(out)[dst] = e;
+        else static_cast<uint32_t*>(out)[dst] = (uint32_t)e;
+    }
+}
+
+int query_sort(const float* lo, const float* hi, const double* d_q, size_t S, int lo_bit, Workspace& ws, hipStream_t s) {
+    if (S == 0) return MSH_OK;
+    if (S > 0xFFFFFFFFull || lo_bit < 6) {
+        set_error("query sort: %zu rows (at most 2^32 - 1) on Morton bits from %d (keys of at most 24 bits)", S, lo_bit);
+        return MSH_EINVAL;
+    }
+    const unsigned nb = (unsigned)((S + kQsTile - 1) / kQsTile);
+    MSH_TRY(ws.keys.reserve(S * sizeof(uint32_t)));
+    MSH_TRY(ws.vals.reserve(S * sizeof(uint32_t)));
+    MSH_TRY(ws.keys_alt.reserve(S * sizeof(unsigned long long)));
+    MSH_TRY(ws.vals_alt.reserve(S * sizeof(unsigned long long)));
+    MSH_TRY(ws.hist.reserve((size_t)nb * 256 * sizeof(uint32_t)));
+    uint32_t* hist = ws.hist.as<uint32_t>();
+    unsigned long long* A = ws.keys_alt.as<unsigned long long>();
+    unsigned long long* B = ws.vals_alt.as<unsigned long long>();
+    {
+        TimedLaunch tl("morton", s);
+        k_qkeys<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(d_q, S, lo_bit, lo[0], lo[1], lo[2], hi[0], hi[1], hi[2],
+                                                     ws.keys.as<uint32_t>(), hist, nb);
+        MSH_HIP(hipGetLastError());
+    }
+    TimedLaunch tl("sort", s);
+    MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
+    k_qscatter<kQsNT, kQsItems, false, true><<<nb, kQsNT, 0, s>>>(ws.keys.ptr, A, S, 0, hist, nb);
+    MSH_HIP(hipGetLastError());
+    k_qhist64<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(A, S, 8, hist, nb);
+    MSH_HIP(hipGetLastError());
+    MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
+    k_qscatter<kQsNT, kQsItems, true, true><<<nb, kQsNT, 0, s>>>(A, B, S, 8, hist, nb);
+    MSH_HIP(hipGetLastError());
+    k_qhist64<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(B, S, 16, hist, nb);
+    MSH_HIP(hipGetLastError());
+    MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
+    k_qscatter<kQsNT, kQsItems, true, false><<<nb, kQsNT, 0, s>>>(B, ws.vals.ptr, S, 16, hist, nb);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
 }  // namespace msh

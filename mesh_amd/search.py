@@ -172,9 +172,7 @@ class AabbTreeBatch(object):
     def nearest(self, v_samples, nearest_part=False):
         q = self._q(v_samples)
         B, S = q.shape[0], q.shape[1]
-        face = np.empty((B, S), dtype=np.uint32)
-        part = np.empty((B, S), dtype=np.uint32)
-        pt = np.empty((B, S, 3), dtype=np.float64)
+        face, part, pt = N.empty_results(((B, S), np.uint32), ((B, S), np.uint32), ((B, S, 3), np.float64))
         N.check(N.lib().msh_batch_nearest(self.cpp_handle.ptr, N.dptr(q), S, N.uptr(face), N.uptr(part),
                                           N.dptr(pt)))
         return (face, part, pt) if nearest_part else (face, pt)
@@ -183,9 +181,7 @@ class AabbTreeBatch(object):
         """(face (B,S) u32, point (B,S,3) f64, barycentric weights (B,S,3) f64) per mesh."""
         q = self._q(v_samples)
         B, S = q.shape[0], q.shape[1]
-        face = np.empty((B, S), dtype=np.uint32)
-        pt = np.empty((B, S, 3), dtype=np.float64)
-        bary = np.empty((B, S, 3), dtype=np.float64)
+        face, pt, bary = N.empty_results(((B, S), np.uint32), ((B, S, 3), np.float64), ((B, S, 3), np.float64))
         N.check(N.lib().msh_batch_nearest_bary(self.cpp_handle.ptr, N.dptr(q), S, N.uptr(face), N.dptr(pt),
                                                N.dptr(bary)))
         return face, pt, bary

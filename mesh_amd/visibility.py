@@ -64,8 +64,8 @@ def visibility_compute(cams=None, v=None, f=None, tree=None, n=None, sensors=Non
         if sensors.ndim != 2 or sensors.shape[1] != 9 or sensors.shape[0] != C:
             raise ValueError("Sensors should have same number of rows as cameras, 3x3 columns")
         ss = np.ascontiguousarray(sensors, dtype=np.float64)
-    vis = np.empty((C, P), dtype=np.uint32)
-    ndc = np.empty((C, P), dtype=np.float64)
+    # large results come from the library's page-locked pool (downloaded straight into place, no page faults)
+    vis, ndc = N.empty_results(((C, P), np.uint32), ((C, P), np.float64))
     N.check(N.lib().msh_visibility(handle.ptr, N.dptr(cams), C, N.dptr(nn), N.dptr(ss), float(min_dist), N.uptr(vis),
                                    N.dptr(ndc)), VisibilityError)
     return vis, ndc

@@ -4,7 +4,7 @@
 #   VARIANTS="name:FLAGS;name2:FLAGS2" bash scripts/build_variants.sh
 set -eu
 R=$(cd "$(dirname "$0")/.." && pwd)
-rm -rf "$R/build/variants"
+[ -n "${KEEP:-}" ] || rm -rf "$R/build/variants"
 mkdir -p "$R/build/variants"
 IFS=';' read -ra VS <<< "${VARIANTS:?set VARIANTS}"
 for v in "${VS[@]}"; do

@@ -42,8 +42,6 @@ for s in $STAGES; do
     pmc)    PASSES="${PMC_PASSES:-stats fetch write tcc sq valu valu2 sq2}" TARGET=${PMC_TARGET:-c3} bash scripts/profile_pmc.sh > gpurun_out/pmc_${PMC_TARGET:-c3}.log 2>&1; ok pmc_${PMC_TARGET:-c3} $? ;;
     pmc_cfg) for t in ${PMC_CFGS:-c5 c2}; do PASSES="stats fetch write tcc" TARGET=$t bash scripts/profile_pmc.sh > gpurun_out/pmc_$t.log 2>&1; ok pmc_$t $?; done ;;
     nptl)   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OLDPWD/gpurun_out/nptl" -o run -- python3 "$OLDPWD/scripts/numpy_timeline.py" --calls 3 > "$OLDPWD/gpurun_out/nptl.log" 2>&1); ok nptl $? ;;
-    npplan_check) MESH_AMD_HOST_PLAN=0.1,0.3 timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread -k "host_api" > gpurun_out/npplan_check.log 2>&1; ok npplan_check $? ;;
-    npplan) for p in ${NPPLAN:-32 8,24 4,12,28 6,30 8,16,32 16 24}; do MESH_AMD_HOST_PLAN=$p timeout -k 10 300 python scripts/numpy_timeline.py --calls 6 > gpurun_out/npplan_${p//,/_}.log 2>&1; ok npplan_$p $?; done ;;
     facade) timeout -k 10 900 python scripts/bench_configs.py --configs facade --reps 2 > gpurun_out/facade.log 2>&1; ok facade $? ;;
     repl)   timeout -k 10 300 python scripts/replication_timing.py > gpurun_out/repl.log 2>&1; ok repl $? ;;
     bench_stats) MESH_AMD_STATS_DUMP=1 timeout -k 10 600 python bench.py --steps 2 --warmup 1 --no-cpu > gpurun_out/bench_stats.log 2>&1; ok bench_stats $? ;;

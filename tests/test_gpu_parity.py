@@ -270,6 +270,36 @@ def test_entry_cut_lazy_and_failure_fallback(oracle):
         t.set_entry_cut(5000)
 
 
+def test_entry_cut_rebuild_memory_flat():
+    # Rebuilding the entry cut (set_entry_cut(-1) then a query) frees its build temporaries (~420 MB of cell-centre
+    # queries and answers on C3): device memory is flat across cycles.  msh_device_pool_trim then frees the idle
+    # query workspace a freed tree leaves to the next one (api.cpp WsPool).
+    import gc
+    import torch
+    from mesh_amd import _native as N, spatialsearch
+    v, f = W.c3_mesh()
+    q = W.uniform_in_box(v.min(0), v.max(0), 50_000, seed=61)
+    t = spatialsearch.aabbtree_compute(v, f)
+    ref = _nearest_tree(t, q)
+    free = []
+    for _ in range(4):
+        t.set_entry_cut(-1)
+        got = _nearest_tree(t, q)
+        assert t.entry_cut_info()["state"] == "built"
+        for a, b in zip(ref, got):
+            assert np.array_equal(a, b)
+        free.append(torch.cuda.mem_get_info(0)[0])
+    assert max(free) - min(free) < (64 << 20), free
+    del t
+    gc.collect()
+    ws, _ = N.device_pool_bytes()
+    assert ws > 0  # the freed tree's workspace waits for the next tree
+    before = torch.cuda.mem_get_info(0)[0]
+    N.device_pool_trim()
+    assert N.device_pool_bytes() == (0, 0)
+    assert torch.cuda.mem_get_info(0)[0] >= before + ws - (16 << 20)
+
+
 def test_c3_replication_roundtrip():
     # north_star's replication path on one GPU: the C3 tree packed into one device blob (what rank 0
     # broadcasts), unpacked on the same device (what every other rank does), answers the C3 stream bit for
@@ -861,3 +891,68 @@ def test_c4_full_size(oracle):
     n = np.cross(tri[..., 1, :] - tri[..., 0, :], tri[..., 2, :] - tri[..., 0, :])
     off = np.abs(np.einsum("bsk,bsk->bs", pt - tri[..., 0, :], n)) / np.linalg.norm(n, axis=-1)
     assert off.max() < 1e-9
+
+
+@pytest.mark.parametrize("chunk", [None, "7"])
+def test_batch_host_pipelined_equals_device(monkeypatch, chunk):
+    # AabbTreeBatch.nearest (numpy) runs pipelined over chunks of whole meshes (api.cpp batch_host): the answers equal
+    # the device entry point's over the same rows, bit for bit, with the library's plan and with 7-mesh chunks (a
+    # chunk that starts mid-batch: per-chunk sort, roots and origins of meshes mesh0...)
+    import torch
+    from mesh_amd import _native as N
+    from mesh_amd.search import AabbTreeBatch
+    if chunk:
+        monkeypatch.setenv("MESH_AMD_HOST_CHUNK", chunk)
+    B, S = 64, 10_000
+    f = W.c4_mesh(0)[1]
+    v = np.stack([W.c4_mesh(i)[0] + 0.1 * i for i in range(B)])
+    rng = np.random.default_rng(71)
+    q = np.stack([W.uniform_in_box(v[b].min(0), v[b].max(0), S, seed=int(rng.integers(1 << 30))) for b in range(B)])
+    bt = AabbTreeBatch(v, f)
+    face, part, pt = bt.nearest(q, nearest_part=True)
+    bface, bpt, bw = bt.nearest_barycentric(q)
+    dq = torch.from_numpy(q).cuda()
+    df = torch.empty((B, S), dtype=torch.int32, device="cuda")
+    dp = torch.empty((B, S), dtype=torch.int32, device="cuda")
+    dpt = torch.empty((B, S, 3), dtype=torch.float64, device="cuda")
+    dw = torch.empty((B, S, 3), dtype=torch.float64, device="cuda")
+    N.check(N.lib().msh_batch_nearest_device(bt.cpp_handle.ptr, dq.data_ptr(), S, df.data_ptr(), dp.data_ptr(),
+                                             dpt.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(face, df.cpu().numpy().view(np.uint32)) and np.array_equal(part, dp.cpu().numpy().view(np.uint32))
+    assert np.array_equal(pt, dpt.cpu().numpy())
+    N.check(N.lib().msh_batch_nearest_bary_device(bt.cpp_handle.ptr, dq.data_ptr(), S, df.data_ptr(), dpt.data_ptr(),
+                                                  dw.data_ptr(), None))
+    torch.cuda.synchronize()
+    assert np.array_equal(bface, df.cpu().numpy().view(np.uint32)) and np.array_equal(bpt, dpt.cpu().numpy())
+    assert np.array_equal(bw, dw.cpu().numpy())
+    assert np.array_equal(bface, face)
+
+
+@pytest.mark.parametrize("chunk", [None, "3"])
+def test_visibility_host_pipelined_equals_device(monkeypatch, chunk):
+    # visibility_compute (numpy) downloads its (C, P) outputs a few cameras at a time (api.cpp msh_visibility): equal
+    # to msh_visibility_device over all vertices, with normals and sensors (offset per camera chunk), bit for bit
+    import torch
+    from mesh_amd import spatialsearch, visibility
+    from mesh_amd.distributed import visibility_device
+    from mesh_amd.mesh import Mesh
+    if chunk:
+        monkeypatch.setenv("MESH_AMD_HOST_CHUNK", chunk)
+    v, f = W.geodesic_icosphere(100)
+    v = v * (1.0 + 0.1 * np.sin(5 * v[:, :1]) * np.cos(4 * v[:, 1:2]))
+    t = spatialsearch.aabbtree_compute(v, f)
+    vn = Mesh(v=v, f=f).estimate_vertex_normals()
+    C = 16
+    cams = W.fibonacci_cameras(C, 3.0)
+    sens = np.random.default_rng(72).normal(size=(C, 9)) * 4.0
+    for kw in ({"n": vn}, {"n": vn, "sensors": sens}):
+        vis, ndc = visibility.visibility_compute(cams=cams, tree=t, **kw)
+        assert vis.shape == (C, v.shape[0]) and vis.dtype == np.uint32 and ndc.dtype == np.float64
+        dv = torch.empty((C, v.shape[0]), dtype=torch.int32, device="cuda")
+        dd = torch.empty((C, v.shape[0]), dtype=torch.float64, device="cuda")
+        visibility_device(t, torch.from_numpy(cams).cuda(), dv, dd, torch.from_numpy(vn).cuda(),
+                          torch.from_numpy(kw["sensors"]).cuda() if "sensors" in kw else None)
+        torch.cuda.synchronize()
+        assert np.array_equal(vis, dv.cpu().numpy().view(np.uint32)) and np.array_equal(ndc, dd.cpu().numpy())
+        assert 0.05 < vis.mean() < 0.95
