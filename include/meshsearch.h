@@ -83,6 +83,23 @@ const char* msh_build_id(void);
 int msh_device_count(int* n);
 /* Device used by subsequent builds on the calling thread (default: current HIP device). */
 int msh_set_device(int device);
+/* In-process multi-device handles (SURVEY §8(b) msh_set_devices; the reference's drop-in call
+ * Mesh.closest_faces_and_points -> AabbTree.nearest, mesh.py:454-455 / search.py:26-30, has no device argument).
+ * Trees built afterwards on the calling thread are built on the first device and replicated to the others
+ * (blob pack + peer copy + unpack); the host-buffer entry points (msh_tree_nearest, _nearest_bary,
+ * _nearest_alongnormal, msh_ntree_nearest, msh_points_nearest: contiguous row ranges; msh_visibility: camera
+ * ranges) then split their rows over the devices, one host thread and one chunk pipeline per device, so each
+ * device's host link carries its share.  Calls below 32 MB of rows stay on the first device.  The answers equal
+ * the one-device answers bit for bit (disjoint row ranges of the same arrays).  *_device entry points, batched
+ * trees and the intersection tests stay on the handle's own device.
+ *   msh_set_devices(G): devices d, d + 1, ..., d + G - 1 from the current device d (G = 1: one device again);
+ *   msh_set_device_list(devices, G): an explicit list (an entry may repeat: several replicas on one device);
+ *   msh_tree_devices: the devices of a handle (G = 1 + replicas; devices may be NULL);
+ *   msh_device_plan: the row split of S rows over G devices, begins[0..G] (host only, no device needed). */
+int msh_set_devices(int G);
+int msh_set_device_list(const int* devices, int G);
+int msh_tree_devices(const msh_tree* tree, int* devices, int cap, int* G);
+int msh_device_plan(uint64_t S, int G, uint64_t* begins);
 
 /* ---- spatialsearch (spatialsearchmodule.cpp) ---- */
 /* aabbtree_compute(v, f) -> capsule: spatialsearchmodule.cpp:74-127 (TreeAndTri build :108-123).

@@ -33,6 +33,10 @@ SIGNATURES = [
     ("msh_build_id", ctypes.c_char_p, []),
     ("msh_device_count", _i, [ctypes.POINTER(_i)]),
     ("msh_set_device", _i, [_i]),
+    ("msh_set_devices", _i, [_i]),
+    ("msh_set_device_list", _i, [ctypes.POINTER(_i), _i]),
+    ("msh_tree_devices", _i, [_vp, ctypes.POINTER(_i), _i, ctypes.POINTER(_i)]),
+    ("msh_device_plan", _i, [ctypes.c_uint64, _i, _c_u64_p]),
     ("msh_tree_build", _i, [_c_double_p, _sz, _c_u32_p, _sz, ctypes.POINTER(_vp)]),
     ("msh_tree_build_ex", _i, [_c_double_p, _sz, _c_u32_p, _sz, _c_double_p, _sz, _c_u32_p, _sz, ctypes.POINTER(_vp)]),
     ("msh_tree_free", None, [_vp]),
@@ -285,6 +289,33 @@ def device_count():
 
 def set_device(device):
     check(lib().msh_set_device(int(device)))
+
+
+def set_devices(devices):
+    """Devices of the trees built next on this thread: an int G (G devices from the current one,
+    msh_set_devices) or a list of device ordinals (msh_set_device_list; entries may repeat).  Host-buffer calls
+    on those trees split their rows over the devices."""
+    if isinstance(devices, int):
+        check(lib().msh_set_devices(devices))
+        return
+    arr = (ctypes.c_int * max(1, len(devices)))(*devices)
+    check(lib().msh_set_device_list(arr, len(devices)))
+
+
+def tree_devices(h):
+    """msh_tree_devices -> the device ordinals of a handle and its replicas"""
+    g = ctypes.c_int(0)
+    check(lib().msh_tree_devices(h.ptr, None, 0, ctypes.byref(g)))
+    arr = (ctypes.c_int * g.value)()
+    check(lib().msh_tree_devices(h.ptr, arr, g.value, ctypes.byref(g)))
+    return list(arr)
+
+
+def device_plan(S, G):
+    """msh_device_plan: row boundaries begins[0..G] of S rows split over G devices"""
+    out = (ctypes.c_uint64 * (G + 1))()
+    check(lib().msh_device_plan(int(S), int(G), out))
+    return list(out)
 
 
 def build_tree(v, f, extra_v=None, extra_f=None):

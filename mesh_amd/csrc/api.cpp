@@ -29,6 +29,8 @@ namespace msh {
 
 static thread_local std::string g_err;
 static thread_local int g_device = -1;
+// devices of the trees built next on this thread (msh_set_devices / msh_set_device_list); empty: one device
+static thread_local std::vector<int> g_devices;
 
 void set_error(const char* fmt, ...) {
     char buf[1024];
@@ -221,6 +223,8 @@ static int upload(DevBuf& buf, const T* host, size_t n, hipStream_t s) {
 
 static void free_tree(msh_tree* t) {
     if (!t) return;
+    for (msh_tree* r : t->replicas) free_tree(r);
+    t->replicas.clear();
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     if (t->ws_done) (void)hipEventSynchronize(t->ws_done);
@@ -1149,9 +1153,56 @@ static int pipelined(msh_tree* t, size_t S, const std::vector<HostArr>& arrs, Ru
 }
 
 
+// ---- one handle on several devices (msh_set_devices) ----
+// Contiguous shards of n rows over G parts, the first n % G one row larger (mesh_amd/distributed.py shard_range).
+static void shard_rows(size_t n, size_t G, size_t g, size_t* r0, size_t* cnt) {
+    const size_t base = n / G, rem = n % G;
+    *r0 = g * base + std::min(g, rem);
+    *cnt = base + (g < rem ? 1 : 0);
+}
+
+// Host-buffer calls below this many bytes of rows stay on the handle's own device (a fan-out costs a thread per
+// replica and a chunk pipeline per device).
+constexpr size_t kFanMinBytes = (size_t)32 << 20;
+
+// Rows [0, S) of a host-buffer call over the handle and its replicas: replica g - 1 answers shard g (shard 0 stays
+// here), each from its own host thread through the entry point's own pipelined path, so every device's host link
+// and copy engines carry their share.  The shards are disjoint row ranges of the caller's arrays, so the answer is
+// the one-device answer bit for bit.  call(h, r0, n) runs rows [r0, r0 + n) on handle h.
+template <class Call>
+static int fan_out(msh_tree* t, size_t S, size_t row_bytes, Call call) {
+    const size_t G = 1 + t->replicas.size();
+    if (G == 1 || S * row_bytes < kFanMinBytes || S < G) return call(t, (size_t)0, S);
+    std::vector<int> st(G, MSH_OK);
+    std::vector<std::string> err(G);
+    std::vector<std::thread> th;
+    th.reserve(G - 1);
+    for (size_t g = 1; g < G; ++g)
+        th.emplace_back([&, g] {
+            size_t r0, n;
+            shard_rows(S, G, g, &r0, &n);
+            if (n) st[g] = call(t->replicas[g - 1], r0, n);
+            if (st[g] != MSH_OK) err[g] = g_err;
+        });
+    size_t r0, n;
+    shard_rows(S, G, 0, &r0, &n);
+    st[0] = call(t, r0, n);
+    if (st[0] != MSH_OK) err[0] = g_err;
+    for (auto& x : th) x.join();
+    (void)use_device(t->device);  // the caller's thread stays on the handle's device
+    for (size_t g = 0; g < G; ++g)
+        if (st[g] != MSH_OK) {
+            g_err = err[g];
+            return st[g];
+        }
+    return MSH_OK;
+}
+
 }  // namespace msh
 
 using namespace msh;
+
+static int replicate_tree(msh_tree* t);
 
 extern "C" {
 
@@ -1187,6 +1238,56 @@ int msh_set_device(int device) {
     return use_device(device);
 }
 
+int msh_set_device_list(const int* devices, int G) {
+    if (G < 0 || (G > 0 && !devices) || G > 64) { set_error("msh_set_device_list: bad device list (G = %d)", G); return MSH_EINVAL; }
+    int c = 0;
+    MSH_TRY(msh_device_count(&c));
+    for (int g = 0; g < G; ++g)
+        if (devices[g] < 0 || devices[g] >= c) {
+            set_error("msh_set_device_list: device %d out of range (%d devices)", devices[g], c);
+            return MSH_EINVAL;
+        }
+    if (G <= 1) {
+        g_devices.clear();
+        return G == 1 ? msh_set_device(devices[0]) : MSH_OK;
+    }
+    g_devices.assign(devices, devices + G);
+    return msh_set_device(devices[0]);
+}
+
+int msh_set_devices(int G) {
+    int c = 0, d = 0;
+    MSH_TRY(msh_device_count(&c));
+    MSH_TRY(current_device(&d));
+    if (G < 1 || d + G > c) {
+        set_error("msh_set_devices: %d devices from device %d (%d visible)", G, d, c);
+        return MSH_EINVAL;
+    }
+    std::vector<int> list(G);
+    for (int g = 0; g < G; ++g) list[g] = d + g;
+    return msh_set_device_list(list.data(), G);
+}
+
+int msh_tree_devices(const msh_tree* t, int* devices, int cap, int* G) {
+    if (!t || !G) { set_error("msh_tree_devices: null argument"); return MSH_EINVAL; }
+    *G = 1 + (int)t->replicas.size();
+    if (devices && cap > 0) devices[0] = t->device;
+    for (int g = 1; g < *G && g < cap; ++g)
+        if (devices) devices[g] = t->replicas[g - 1]->device;
+    return MSH_OK;
+}
+
+int msh_device_plan(uint64_t S, int G, uint64_t* begins) {
+    if (G < 1 || !begins) { set_error("msh_device_plan: bad argument"); return MSH_EINVAL; }
+    for (int g = 0; g < G; ++g) {
+        size_t r0, n;
+        shard_rows((size_t)S, (size_t)G, (size_t)g, &r0, &n);
+        begins[g] = r0;
+    }
+    begins[G] = S;
+    return MSH_OK;
+}
+
 int msh_tree_build_ex(const double* v, size_t P, const uint32_t* f, size_t T, const double* ev, size_t EP,
                       const uint32_t* ef, size_t ET, msh_tree** out) {
     if (!out) { set_error("null output handle"); return MSH_EINVAL; }
@@ -1212,6 +1313,7 @@ int msh_tree_build_ex(const double* v, size_t P, const uint32_t* f, size_t T, co
         for (size_t i = 0; i < 3 * ET; ++i) fall[3 * T + i] = ef[i] + (uint32_t)P;
         st = build_triangles(t, vall.data(), P + EP, fall.data(), T + ET);
     }
+    if (st == MSH_OK) st = replicate_tree(t);
     if (st != MSH_OK) {
         std::string keep = g_err;
         free_tree(t);
@@ -1228,8 +1330,14 @@ int msh_tree_build(const double* v, size_t P, const uint32_t* f, size_t T, msh_t
 
 int msh_ntree_build(const double* v, size_t P, const uint32_t* f, size_t T, double eps, msh_tree** out) {
     MSH_TRY(msh_tree_build_ex(v, P, f, T, nullptr, 0, nullptr, 0, out));
-    (*out)->kind = kNormals;  // the normals metric starts at the root: no entry cut is ever built
-    (*out)->eps = eps;
+    for (msh_tree* h : {*out}) {
+        h->kind = kNormals;  // the normals metric starts at the root: no entry cut is ever built
+        h->eps = eps;
+        for (msh_tree* r : h->replicas) {
+            r->kind = kNormals;
+            r->eps = eps;
+        }
+    }
     return MSH_OK;
 }
 
@@ -1271,6 +1379,7 @@ int msh_points_build(const double* v, size_t P, msh_tree** out) {
     (void)hipStreamSynchronize(s);
     dLo.release(); dHi.release(); dOrder.release();
     t->ws.release();
+    if (st == MSH_OK) st = replicate_tree(t);
     if (st != MSH_OK) {
         std::string keep = g_err;
         free_tree(t);
@@ -1302,6 +1411,7 @@ int msh_tree_set_entry_cut(msh_tree* t, int G) {
     if (!t) { set_error("msh_tree_set_entry_cut: null tree handle"); return MSH_EINVAL; }
     if (G > 4096) { set_error("msh_tree_set_entry_cut: G = %d cells per axis (at most 4096)", G); return MSH_EINVAL; }
     const int want = G < 0 ? -1 : G;
+    for (msh_tree* r : t->replicas) MSH_TRY(msh_tree_set_entry_cut(r, G));
     if (want == t->cut_req && t->cut_state != kCutFailed) return MSH_OK;
     free_entry_cut(t);
     t->cut_req = want;
@@ -1371,11 +1481,8 @@ int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint3
     return launch_nearest(t, ord, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_w}, s);
 }
 
-int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
-    MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest"));
-    MSH_TRY(check_count(S, "msh_tree_nearest"));
-    if (S == 0) return MSH_OK;
-    if (!q || !face || !pt) { set_error("msh_tree_nearest: null argument"); return MSH_EINVAL; }
+static int nearest_host(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
+    MSH_TRY(use_device(t->device));
     ensure_entry_cut(t);
     // rows: q (24 B in) | face (4 B out) | part (4 B out) | point (24 B out)
     const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, part, 4}, {nullptr, pt, 24}};
@@ -1386,16 +1493,31 @@ int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uin
     });
 }
 
+int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest"));
+    MSH_TRY(check_count(S, "msh_tree_nearest"));
+    if (S == 0) return MSH_OK;
+    if (!q || !face || !pt) { set_error("msh_tree_nearest: null argument"); return MSH_EINVAL; }
+    return fan_out(t, S, 56, [&](msh_tree* h, size_t r0, size_t n) {
+        return nearest_host(h, q + 3 * r0, n, face + r0, part ? part + r0 : nullptr, pt + 3 * r0);
+    });
+}
+
 int msh_tree_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face, double* pt, double* w) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_bary"));
     MSH_TRY(check_count(S, "msh_tree_nearest_bary"));
     if (S == 0) return MSH_OK;
     if (!q || !face || !pt || !w) { set_error("msh_tree_nearest_bary: null argument"); return MSH_EINVAL; }
-    ensure_entry_cut(t);
-    const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, pt, 24}, {nullptr, w, 24}};
-    return pipelined(t, S, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
-        return msh_tree_nearest_bary_device(t, reinterpret_cast<const double*>(d[0]), n, reinterpret_cast<uint32_t*>(d[1]),
-                                            reinterpret_cast<double*>(d[2]), reinterpret_cast<double*>(d[3]), t->stream);
+    return fan_out(t, S, 76, [&](msh_tree* h, size_t r0, size_t S_h) {
+        MSH_TRY(use_device(h->device));
+        ensure_entry_cut(h);
+        const std::vector<HostArr> arrs = {{q + 3 * r0, nullptr, 24}, {nullptr, face + r0, 4}, {nullptr, pt + 3 * r0, 24},
+                                           {nullptr, w + 3 * r0, 24}};
+        return pipelined(h, S_h, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
+            return msh_tree_nearest_bary_device(h, reinterpret_cast<const double*>(d[0]), n,
+                                                reinterpret_cast<uint32_t*>(d[1]), reinterpret_cast<double*>(d[2]),
+                                                reinterpret_cast<double*>(d[3]), h->stream);
+        });
     });
 }
 
@@ -1501,13 +1623,16 @@ int msh_tree_nearest_alongnormal(msh_tree* t, const double* p, const double* n, 
     MSH_TRY(check_count(S, "msh_tree_nearest_alongnormal"));
     if (S == 0) return MSH_OK;
     if (!p || !n || !dist || !face || !pt) { set_error("msh_tree_nearest_alongnormal: null argument"); return MSH_EINVAL; }
-    const std::vector<HostArr> arrs = {{p, nullptr, 24}, {n, nullptr, 24}, {nullptr, dist, 8}, {nullptr, face, 4},
-                                       {nullptr, pt, 24}};
-    return pipelined(t, S, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
-        return msh_tree_nearest_alongnormal_device(t, reinterpret_cast<const double*>(d[0]),
-                                                   reinterpret_cast<const double*>(d[1]), c,
-                                                   reinterpret_cast<double*>(d[2]), reinterpret_cast<uint32_t*>(d[3]),
-                                                   reinterpret_cast<double*>(d[4]), t->stream);
+    return fan_out(t, S, 84, [&](msh_tree* h, size_t r0, size_t S_h) {
+        MSH_TRY(use_device(h->device));
+        const std::vector<HostArr> arrs = {{p + 3 * r0, nullptr, 24}, {n + 3 * r0, nullptr, 24}, {nullptr, dist + r0, 8},
+                                           {nullptr, face + r0, 4}, {nullptr, pt + 3 * r0, 24}};
+        return pipelined(h, S_h, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
+            return msh_tree_nearest_alongnormal_device(h, reinterpret_cast<const double*>(d[0]),
+                                                       reinterpret_cast<const double*>(d[1]), c,
+                                                       reinterpret_cast<double*>(d[2]), reinterpret_cast<uint32_t*>(d[3]),
+                                                       reinterpret_cast<double*>(d[4]), h->stream);
+        });
     });
 }
 
@@ -1562,15 +1687,19 @@ int msh_ntree_nearest(msh_tree* t, const double* q, const double* n, size_t S, u
     MSH_TRY(check_count(S, "msh_ntree_nearest"));
     if (S == 0) return MSH_OK;
     if (!q || !n || !face || !pt) { set_error("msh_ntree_nearest: null argument"); return MSH_EINVAL; }
-    // rows: q (24 B in) | n (24 B in) | face (4 B out) | point (24 B out); chunked like msh_tree_nearest
-    const std::vector<HostArr> arrs = {{q, nullptr, 24}, {n, nullptr, 24}, {nullptr, face, 4}, {nullptr, pt, 24}};
-    return pipelined(t, S, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
-        hipStream_t s = t->stream;
-        WsOrder order(t, s);
-        QueryOrder ord;
-        MSH_TRY(sort_queries(t, reinterpret_cast<const double*>(d[0]), reinterpret_cast<const double*>(d[1]), c, s, &ord));
-        return launch_nnearest(t, ord, c, SlotOut{reinterpret_cast<uint32_t*>(d[2]), nullptr, reinterpret_cast<double*>(d[3]),
-                                                  nullptr, nullptr}, s);
+    return fan_out(t, S, 76, [&](msh_tree* h, size_t r0, size_t S_h) {
+        MSH_TRY(use_device(h->device));
+        // rows: q (24 B in) | n (24 B in) | face (4 B out) | point (24 B out); chunked like msh_tree_nearest
+        const std::vector<HostArr> arrs = {{q + 3 * r0, nullptr, 24}, {n + 3 * r0, nullptr, 24}, {nullptr, face + r0, 4},
+                                           {nullptr, pt + 3 * r0, 24}};
+        return pipelined(h, S_h, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
+            hipStream_t s = h->stream;
+            WsOrder order(h, s);
+            QueryOrder ord;
+            MSH_TRY(sort_queries(h, reinterpret_cast<const double*>(d[0]), reinterpret_cast<const double*>(d[1]), c, s, &ord));
+            return launch_nnearest(h, ord, c, SlotOut{reinterpret_cast<uint32_t*>(d[2]), nullptr,
+                                                      reinterpret_cast<double*>(d[3]), nullptr, nullptr}, s);
+        });
     });
 }
 
@@ -1621,12 +1750,10 @@ int msh_visibility_device(msh_tree* t, const double* d_cams, size_t C, const dou
 // pipeline a few cameras at a time (api.cpp pipelined(): rows = cameras), so the downloads of earlier cameras (C5:
 // 30 MB per camera, 1.92 GB in all) overlap the rays of later ones, and land straight in page-locked pool arrays
 // when the caller's arrays are carved from it.
-int msh_visibility(msh_tree* t, const double* cams, size_t C, const double* normals, const double* sensors,
-                   double min_dist, uint32_t* vis, double* ndc) {
-    MSH_TRY(check_tree(t, kTriangles, "msh_visibility"));
+static int visibility_host(msh_tree* t, const double* cams, size_t C, const double* normals, const double* sensors,
+                           double min_dist, uint32_t* vis, double* ndc) {
+    MSH_TRY(use_device(t->device));
     const size_t P = t->P;
-    if (C * P == 0) return MSH_OK;
-    if (!cams || !vis || !ndc) { set_error("msh_visibility: null argument"); return MSH_EINVAL; }
     hipStream_t s = t->stream;
     DevBuf dc, dn, ds;
     int st = MSH_OK;
@@ -1646,20 +1773,39 @@ int msh_visibility(msh_tree* t, const double* cams, size_t C, const double* norm
     return st;
 }
 
+// Host arrays: the cameras, normals and sensors are uploaded once; the (C, P) outputs come back through the pinned
+// pipeline a few cameras at a time (api.cpp pipelined(): rows = cameras), so the downloads of earlier cameras (C5:
+// 30 MB per camera, 1.92 GB in all) overlap the rays of later ones, and land straight in page-locked pool arrays
+// when the caller's arrays are carved from it.  With replicas (msh_set_devices) each device casts a camera range.
+int msh_visibility(msh_tree* t, const double* cams, size_t C, const double* normals, const double* sensors,
+                   double min_dist, uint32_t* vis, double* ndc) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_visibility"));
+    const size_t P = t->P;
+    if (C * P == 0) return MSH_OK;
+    if (!cams || !vis || !ndc) { set_error("msh_visibility: null argument"); return MSH_EINVAL; }
+    return fan_out(t, C, 12 * P, [&](msh_tree* h, size_t c0, size_t nc) {
+        return visibility_host(h, cams + 3 * c0, nc, normals, sensors ? sensors + 9 * c0 : nullptr, min_dist,
+                               vis + c0 * P, ndc + c0 * P);
+    });
+}
+
 int msh_points_nearest(msh_tree* t, const double* q, size_t S, uint32_t* idx, double* dist) {
     MSH_TRY(check_tree(t, kPoints, "msh_points_nearest"));
     MSH_TRY(check_count(S, "msh_points_nearest"));
     if (S == 0) return MSH_OK;
     if (!q || !idx || !dist) { set_error("msh_points_nearest: null argument"); return MSH_EINVAL; }
-    // rows: q (24 B in) | index (4 B out) | distance (8 B out); chunked like msh_tree_nearest
-    const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, idx, 4}, {nullptr, dist, 8}};
-    return pipelined(t, S, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
-        hipStream_t s = t->stream;
-        WsOrder order(t, s);
-        QueryOrder ord;
-        MSH_TRY(sort_queries(t, reinterpret_cast<const double*>(d[0]), nullptr, c, s, &ord));
-        return launch_points_nearest(t, ord, c, SlotOut{reinterpret_cast<uint32_t*>(d[1]), nullptr, nullptr,
-                                                        reinterpret_cast<double*>(d[2]), nullptr}, s);
+    return fan_out(t, S, 36, [&](msh_tree* h, size_t r0, size_t S_h) {
+        MSH_TRY(use_device(h->device));
+        // rows: q (24 B in) | index (4 B out) | distance (8 B out); chunked like msh_tree_nearest
+        const std::vector<HostArr> arrs = {{q + 3 * r0, nullptr, 24}, {nullptr, idx + r0, 4}, {nullptr, dist + r0, 8}};
+        return pipelined(h, S_h, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
+            hipStream_t s = h->stream;
+            WsOrder order(h, s);
+            QueryOrder ord;
+            MSH_TRY(sort_queries(h, reinterpret_cast<const double*>(d[0]), nullptr, c, s, &ord));
+            return launch_points_nearest(h, ord, c, SlotOut{reinterpret_cast<uint32_t*>(d[1]), nullptr, nullptr,
+                                                            reinterpret_cast<double*>(d[2]), nullptr}, s);
+        });
     });
 }
 
@@ -2114,3 +2260,49 @@ int msh_batch_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* fac
 }
 
 }  // extern "C"
+
+// Copies of a freshly built tree on the other devices of the calling thread's device list (msh_set_devices): the
+// tree is packed into one device blob (msh_tree_blob_pack), copied peer to peer to each device and unpacked there
+// (msh_tree_blob_unpack) — the in-process form of bench.py's RCCL broadcast.  A replica on the handle's own device
+// (a repeated entry of the list) unpacks from the blob in place.
+static int replicate_tree(msh_tree* t) {
+    if (g_devices.size() <= 1) return MSH_OK;
+    size_t bytes = 0;
+    MSH_TRY(msh_tree_blob_size(t, &bytes));
+    MSH_TRY(use_device(t->device));
+    void* blob = nullptr;
+    MSH_HIP(hipMalloc(&blob, bytes));
+    int st = msh_tree_blob_pack(t, blob, nullptr);
+    const std::vector<int> devs = g_devices;
+    for (size_t g = 1; g < devs.size() && st == MSH_OK; ++g) {
+        const int d = devs[g];
+        void* src = blob;
+        void* copy = nullptr;
+        if (d != t->device) {
+            (void)hipSetDevice(d);
+            hipError_t e = hipMalloc(&copy, bytes);
+            if (e == hipSuccess) e = hipMemcpyPeer(copy, d, blob, t->device, bytes);
+            if (e != hipSuccess) {
+                set_error("replicating the tree to device %d: %s", d, hipGetErrorString(e));
+                st = e == hipErrorOutOfMemory ? MSH_ENOMEM : MSH_EDEVICE;
+                if (copy) (void)hipFree(copy);
+                break;
+            }
+            src = copy;
+        }
+        msh_tree* r = nullptr;
+        st = msh_tree_blob_unpack(src, bytes, d, nullptr, &r);
+        if (copy) {
+            (void)hipSetDevice(d);
+            (void)hipFree(copy);
+        }
+        if (st == MSH_OK) {
+            r->cut_req = t->cut_req;
+            r->build_ms = t->build_ms;
+            t->replicas.push_back(r);
+        }
+    }
+    (void)use_device(t->device);
+    (void)hipFree(blob);
+    return st;
+}

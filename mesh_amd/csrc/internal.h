@@ -6,6 +6,7 @@
 #include <stdint.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/meshsearch.h"
 #include "common.h"
@@ -148,6 +149,9 @@ struct msh_tree {
     double cut_ms = 0.0;
     double cut_lo[3] = {0, 0, 0}, cut_iw[3] = {0, 0, 0};
     msh::Workspace ws;
+    // copies of this tree on the other devices of msh_set_devices / msh_set_device_list (owned; freed with it):
+    // host-buffer calls split their rows over this handle and its replicas
+    std::vector<msh_tree*> replicas;
 };
 
 namespace msh {

@@ -168,3 +168,25 @@ def test_build_id_matches_sources():
     from mesh_amd import _native
     bid = _native.build_id()
     assert len(bid) == 16 and bid == _native.source_build_id()
+
+
+@pytest.mark.parametrize("S,G", [(0, 1), (1, 3), (7, 3), (100, 8), (10**8, 8), (2**32 - 1, 7), (5, 8)])
+def test_device_plan_matches_shard_range(S, G):
+    # the row split of a host-buffer call over a handle's devices (msh_set_devices): contiguous, covering, balanced
+    # and identical to the multi-process split (mesh_amd/distributed.py shard_range) — host only, no device
+    from mesh_amd import _native
+    from mesh_amd.distributed import shard_range
+    b = _native.device_plan(S, G)
+    assert len(b) == G + 1 and b[0] == 0 and b[-1] == S
+    for g in range(G):
+        assert (b[g], b[g + 1]) == shard_range(S, g, G)
+    sizes = [b[g + 1] - b[g] for g in range(G)]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_device_list_validation():
+    from mesh_amd import _native
+    with pytest.raises((ValueError, RuntimeError)):
+        _native.set_devices([0, -1])
+    with pytest.raises((ValueError, RuntimeError)):
+        _native.device_plan(10, 0)

@@ -956,3 +956,41 @@ def test_visibility_host_pipelined_equals_device(monkeypatch, chunk):
         torch.cuda.synchronize()
         assert np.array_equal(vis, dv.cpu().numpy().view(np.uint32)) and np.array_equal(ndc, dd.cpu().numpy())
         assert 0.05 < vis.mean() < 0.95
+
+
+def test_multi_device_replicas_equal_one_device():
+    # msh_set_device_list([0, 0, 0]): trees built next get two replicas (blob pack + copy + unpack, here on the one
+    # GPU of the box), and host-buffer calls split their rows over the three handles from three host threads.  Every
+    # entry point that fans out gives the one-device arrays bit for bit; G = 1 again afterwards.
+    from mesh_amd import _native as N, aabb_normals, spatialsearch, visibility
+    from mesh_amd.mesh import Mesh
+    from mesh_amd.search import ClosestPointTree
+    v, f = W.c2_mesh()
+    q, _ = W.surface_samples(v, f, 1_500_000, seed=81, sigma=0.02)  # 84 MB of rows: above the fan-out floor
+    nrm = np.random.default_rng(82).normal(size=q.shape)
+    cams = W.fibonacci_cameras(16, 3.0)
+    vb, fb = W.geodesic_icosphere(160)  # 256k vertices: 16 cameras x 256k x 12 B = 49 MB of outputs
+    vn = Mesh(v=vb, f=fb).estimate_vertex_normals()
+
+    def run():
+        t = spatialsearch.aabbtree_compute(v, f)
+        tb = spatialsearch.aabbtree_compute(vb, fb)
+        h = aabb_normals.aabbtree_n_compute(v, f, 0.1)
+        out = [spatialsearch.aabbtree_nearest(t, q), spatialsearch.aabbtree_nearest_barycentric(t, q),
+               spatialsearch.aabbtree_nearest_alongnormal(t, q, nrm), aabb_normals.aabbtree_n_nearest(h, q, nrm),
+               ClosestPointTree(Mesh(v=v, f=f))._query(q), visibility.visibility_compute(cams=cams, tree=tb, n=vn)]
+        return out, N.tree_devices(t), N.tree_devices(h)
+
+    one, d1, _ = run()
+    assert d1 == [0]
+    try:
+        N.set_devices([0, 0, 0])
+        many, d3, dh = run()
+        assert d3 == [0, 0, 0] and dh == [0, 0, 0]
+    finally:
+        N.set_devices([0])
+    for a, b in zip(one, many):
+        for x, y in zip(a, b):
+            assert np.array_equal(np.asarray(x), np.asarray(y), equal_nan=np.asarray(x).dtype.kind == "f")
+    t = spatialsearch.aabbtree_compute(v, f)
+    assert N.tree_devices(t) == [0]
