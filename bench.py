@@ -70,13 +70,14 @@ def host_threads():
         return os.cpu_count() or 1
 
 
-def cpu_baseline(v, f, per_thread):
-    """Oracle CGAL-tree restatement on the C3 query stream (seed 3, rank 0), in two modes:
+def cpu_baseline(v, f, per_thread, stream_rows):
+    """Oracle CGAL-tree restatement on the bench's own C3 query stream (rank 0), in two modes:
       * 1 thread (the reference's aabbtree_nearest loop is serial: its omp pragma is compiled out,
         spatialsearchmodule.cpp:212-214) -> the reported `cpu_baseline`;
       * all host threads this process may use (OpenMP over queries) -> `cpu_baseline_allcores`.
-    Each mode answers a FIXED sample — the same rows of the stream in every session (per_thread x threads
-    queries after 2,000 x threads warm-up rows) — and reports its total queries / total time, so the sample's
+    Each mode answers a FIXED sample — the first rows of the stream the GPU answers (stream_rows(k): its first k
+    rows copied to the host; per_thread x threads queries after 2,000 x threads warm-up rows) — and reports its
+    total queries / total time, so the sample's
     content (its few costly queries near the sphere's centre, equidistant from much of the mesh) is identical
     from run to run and only the host's speed varies; 4 sub-chunks give the spread."""
     from oracle import oracle as O
@@ -87,7 +88,7 @@ def cpu_baseline(v, f, per_thread):
     for mode, threads in (("1", 1), ("all", host_threads())):
         n = per_thread * threads
         warm = 2000 * threads
-        pool = np.random.default_rng(3).uniform(-1.1, 1.1, (warm + n, 3))
+        pool = stream_rows(warm + n)
         tree.nearest(pool[:warm], threads=threads)
         chunk = n // 4
         times = []
@@ -102,8 +103,9 @@ def cpu_baseline(v, f, per_thread):
     def obj(mode, label):
         rate, n, threads, lo, hi = out[mode]
         return {"value": rate, "unit": "queries/s", "cores": threads, "kind": "port",
-                "sample": "%d uniform C3 queries (the stream's rows after %d warm-up rows, seed 3; the same rows "
-                          "every session), total queries / total time (4 sub-chunks: %.0f-%.0f q/s) on the "
+                "sample": "%d uniform C3 queries (rows %d.. of the bench's own stream, the rows the GPU answers, "
+                          "copied to the host; the same rows every session), total queries / total time (4 "
+                          "sub-chunks: %.0f-%.0f q/s) on the "
                           "1,003,520-face icosphere; CGAL-faithful restatement (median-split AABB tree + KD hint, "
                           "fp64, g++ -O3 -ffp-contract=off), %s; tree build %.2f s excluded"
                           % (n, 2000 * threads, lo, hi, label, build_s)}
@@ -409,7 +411,8 @@ def main():
     if sec:
         out.update(sec)
     if world == 1 and not args.no_cpu:
-        out["cpu_baseline"], out["cpu_baseline_allcores"] = cpu_baseline(v, f, args.cpu_queries)
+        out["cpu_baseline"], out["cpu_baseline_allcores"] = cpu_baseline(
+            v, f, args.cpu_queries, lambda k: np.ascontiguousarray(q_all[:k].cpu().numpy()))
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

@@ -63,13 +63,13 @@ void DevBuf::release() {
 
 void Workspace::release() {
     DevBuf* all[] = {&keys, &vals, &keys_alt, &vals_alt, &hist, &scan, &q, &n, &out_a, &out_b, &out_c, &out_d,
-                     &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w};
+                     &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w, &resume};
     for (DevBuf* b : all) b->release();
 }
 
 size_t Workspace::bytes() const {
     const DevBuf* all[] = {&keys, &vals, &keys_alt, &vals_alt, &hist, &scan, &q, &n, &out_a, &out_b, &out_c, &out_d,
-                           &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w};
+                           &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w, &resume};
     size_t t = 0;
     for (const DevBuf* b : all) t += b->bytes;
     return t;

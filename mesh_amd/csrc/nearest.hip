@@ -49,9 +49,9 @@ struct DeferRec {
     uint32_t slot;
     uint32_t face;
     int32_t leaf;
-    uint32_t pad;
+    uint32_t roff;   // first of the query's resume entries (KnnArgs::resume)
     double best;
-    double pad2;
+    uint64_t rcnt;   // resume entries: pass 1's unexplored work (0: pass 2 starts at the root)
 };
 static_assert(sizeof(DeferRec) == 32, "DeferRec must be 32 B");
 
@@ -110,6 +110,12 @@ struct KnnArgs {
     DeferRec* deferred;
     unsigned* n_deferred;
     unsigned max_deferred;
+    // pass-1 work a deferred query leaves (list path): its pending node and its stack as (ref, fp32 bound bits),
+    // appended to one arena, from which pass 2 resumes instead of walking again from the root; a query that does
+    // not fit keeps rcnt = 0
+    uint2* resume;
+    unsigned* n_resume;
+    unsigned resume_cap;
 };
 
 // root node and fp32 query of slot i (batched trees: its mesh's root and origin)
@@ -529,6 +535,9 @@ __device__ inline D3 load_q(const KnnArgs& a, size_t i) {
 #ifndef MSH_FOLLOW_CELL
 #define MSH_FOLLOW_CELL 0
 #endif
+#ifndef MSH_RESUME
+#define MSH_RESUME 1
+#endif
 constexpr unsigned kLead = MSH_KLEAD;
 constexpr unsigned kLead2 = 256;
 constexpr size_t kFWin = MSH_KFWIN;
@@ -881,9 +890,24 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 r.slot = (uint32_t)i;
                 r.face = pol.best_face;
                 r.leaf = pol.best_leaf;
-                r.pad = 0;
+                r.roff = 0;
                 r.best = pol.best;
-                r.pad2 = 0;
+                r.rcnt = 0;
+                if (a.resume) {
+                    // what is left of this walk: the pending entry (w.node, not yet visited: bound 0) above the stack
+                    const unsigned cnt = (unsigned)w.sp + 1;
+                    const unsigned off = atomicAdd(a.n_resume, cnt);
+                    if (off + cnt <= a.resume_cap) {
+                        uint2* dst = a.resume + off;
+                        for (int j = 0; j < w.sp; ++j) {
+                            const typename E::T e = stack_get(lds, spill, j);
+                            dst[j] = make_uint2((uint32_t)E::ref(e), __float_as_uint(E::bound(e)));
+                        }
+                        dst[w.sp] = make_uint2((uint32_t)w.node, 0u);
+                        r.roff = off;
+                        r.rcnt = cnt;
+                    }
+                }
                 a.deferred[dslot] = r;
             }
             if (STATS) {  // per-tile step profile of this phase (stats[8 + 9 * phase slot ...])
@@ -1053,9 +1077,9 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                             r.slot = (uint32_t)i;
                             r.face = pol.best_face;
                             r.leaf = pol.best_leaf;
-                            r.pad = 0;
+                            r.roff = 0;
                             r.best = pol.best;
-                            r.pad2 = 0;
+                            r.rcnt = 0;
                             a.deferred[slot] = r;
                             active = false;
                             deferred = true;  // pass 2 owns this query
@@ -1167,30 +1191,50 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         // to the lanes' own stacks for depth-first walks.
         uint2* W = &front[wv][0][0];  // kWork contiguous entries
         constexpr int kWork = 2 * kFront;
+        // pass 1's unexplored entries (oldest first, its pending node on top), or the root
+        const int rc = (int)r.rcnt;
         int top = 1;
-        if (lane == 0) W[0] = make_uint2((unsigned)root, 0u);
+        if (rc > 0 && rc <= kWork - 128) {
+            for (int j = lane; j < rc; j += 64) W[j] = a.resume[r.roff + j];
+            top = rc;
+        } else if (lane == 0) {
+            W[0] = make_uint2((unsigned)root, 0u);
+        }
         __builtin_amdgcn_wave_barrier();
         while (top > 0 && top <= kWork - 128) {
             const int nt = min(64, top);
             const int base = top - nt;
             bool k0 = false, k1 = false;
             uint2 e0, e1;
+            int lf0 = -1, lf1 = -1;  // leaves to test: a resumed leaf entry, or leaf children within the bound
             if (lane < nt) {
                 const uint2 e = W[base + lane];
                 if (__uint_as_float(e.y) <= pol.limf) {
-                    const NodeV nd = load_node(a.nodes, (int)e.x);
-                    ++n_nodes;
-                    float d0, d1;
-                    node_child_bounds(nd, qf, d0, d1);
-                    const int c0 = nd.child(0), c1 = nd.child(1);
-                    if (d0 <= pol.limf) {
-                        if (c0 < 0) { pol.test(~c0); ++n_leaves; }
-                        else { k0 = true; e0 = make_uint2((unsigned)c0, __float_as_uint(d0)); }
+                    if ((int)e.x < 0) {
+                        lf0 = ~(int)e.x;
+                    } else {
+                        const NodeV nd = load_node(a.nodes, (int)e.x);
+                        ++n_nodes;
+                        float d0, d1;
+                        node_child_bounds(nd, qf, d0, d1);
+                        const int c0 = nd.child(0), c1 = nd.child(1);
+                        if (d0 <= pol.limf) {
+                            if (c0 < 0) lf0 = ~c0;
+                            else { k0 = true; e0 = make_uint2((unsigned)c0, __float_as_uint(d0)); }
+                        }
+                        if (d1 <= pol.limf) {
+                            if (c1 < 0) lf1 = ~c1;
+                            else { k1 = true; e1 = make_uint2((unsigned)c1, __float_as_uint(d1)); }
+                        }
                     }
-                    if (d1 <= pol.limf) {
-                        if (c1 < 0) { pol.test(~c1); ++n_leaves; }
-                        else { k1 = true; e1 = make_uint2((unsigned)c1, __float_as_uint(d1)); }
-                    }
+                }
+            }
+#pragma nounroll
+            for (int j = 0; j < 2; ++j) {  // one call site of the construction
+                const int lf = j == 0 ? lf0 : lf1;
+                if (lf >= 0) {
+                    pol.test(lf);
+                    ++n_leaves;
                 }
             }
             __builtin_amdgcn_wave_barrier();
@@ -1349,12 +1393,15 @@ static int device_cus(int dev) {
     return cache[dev];
 }
 
-constexpr unsigned kBudget = 512;  // pass-1 node steps per lane before a query is deferred
+#ifndef MSH_BUDGET
+#define MSH_BUDGET 512
+#endif
+constexpr unsigned kBudget = MSH_BUDGET;  // pass-1 node steps per lane before a query is deferred
 // super-leaders: their launch has few tiles (C3: 6104 for 8192 wave slots), so its slowest tile sets its
 // length; with 256 steps the launch takes 1.4 instead of 2.9 ms and pass 2 gets ~18k more (cheap) items
 // (+0.4 ms).  A deferred super-leader publishes its best point so far as its leaders' hint.
 constexpr unsigned kBudget3 = 256;
-constexpr unsigned kBudget1 = 512;  // leaders (C3: 13.8 -> 12.6 ms, pass 2 +0.5 ms)
+constexpr unsigned kBudget1 = MSH_BUDGET;  // leaders (C3: 13.8 -> 12.6 ms, pass 2 +0.5 ms)
 constexpr unsigned kKnnBlocksPerCU = 4;  // resident pass-1 blocks per CU (persistent grid)
 
 // Common launch: grid, counters, spill area, deferred list; pass 1 then pass 2 (both also in STATS
@@ -1365,11 +1412,12 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     for (int k = 0; k < 3; ++k) a.org[k] = tree->origin[k];
     const unsigned ncu = (unsigned)device_cus(tree->device);
     Workspace& ws = tree->ws;
-    // counters: 8 group counters (one 128-B line each) + the deferred count + pass 2's item counter
-    MSH_TRY(ws.counters.reserve(10 * 32 * sizeof(unsigned)));
+    // counters: 8 group counters (one 128-B line each) + the deferred count + pass 2's item counter + the resume arena's
+    MSH_TRY(ws.counters.reserve(11 * 32 * sizeof(unsigned)));
     a.counters = ws.counters.as<unsigned>();
     a.n_deferred = a.counters + 8 * 32;
-    MSH_HIP(hipMemsetAsync(a.counters, 0, 10 * 32 * sizeof(unsigned), s));  // + the pass-2 item counter
+    a.n_resume = a.counters + 10 * 32;
+    MSH_HIP(hipMemsetAsync(a.counters, 0, 11 * 32 * sizeof(unsigned), s));  // + the pass-2 item counter
     // leader ordering: closest-point launches over a Morton-sorted slot order (records in a.res)
 // leader phases only for trees of >= kLeadMinLeaves leaves: on a small tree the hint saves little and the
 // three dependent launches serialise their slowest tiles (C1: 0.56 -> 0.29 ms)
@@ -1402,6 +1450,16 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     DevBuf& dbuf = ws.flags;
     MSH_TRY(dbuf.reserve((size_t)a.max_deferred * sizeof(DeferRec)));
     a.deferred = dbuf.as<DeferRec>();
+    a.resume = nullptr;
+    a.resume_cap = 0;
+#if MSH_RESUME
+    if (a.list) {  // resume arena: ~48 entries per expected deferral (C3: 75k deferred of 100M queries), >= 1M entries
+        const size_t cap = std::min<size_t>((size_t)1 << 26, std::max<size_t>((size_t)1 << 20, 48 * (a.S / 1024 + 1024)));
+        MSH_TRY(ws.resume.reserve(cap * sizeof(uint2)));
+        a.resume = ws.resume.as<uint2>();
+        a.resume_cap = (unsigned)cap;
+    }
+#endif
     auto pass1 = [&](int phase, size_t nunits, const char* name) -> int {
         a.phase = phase;
         a.budget = phase == 3 ? kBudget3 : ((phase == 1 || phase == 4) ? kBudget1 : kBudget);

@@ -238,7 +238,48 @@ int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_
 #ifndef MSH_QSORT_NT
 #define MSH_QSORT_NT 1024
 #endif
+#ifndef MSH_QORDER_HILBERT
+#define MSH_QORDER_HILBERT 0
+#endif
 constexpr int kQsNT = MSH_QSORT_NT;
+
+// 24-bit Hilbert index of a cell of the 256^3 grid (Skilling, "Programming the Hilbert curve", 2004: the axes to
+// the transposed form, then the transposed bits interleaved, axis 0 first at each level).  Consecutive indices are
+// face-adjacent cells, so a tile of consecutive queries never jumps across the box the way a Morton tile does at
+// the octree's block boundaries.
+__device__ inline uint32_t hilbert24(uint32_t x, uint32_t y, uint32_t z) {
+    uint32_t X[3] = {x, y, z};
+#pragma unroll
+    for (uint32_t Q = 128; Q > 1; Q >>= 1) {
+        const uint32_t P = Q - 1;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            if (X[i] & Q) {
+                X[0] ^= P;
+            } else {
+                const uint32_t t = (X[0] ^ X[i]) & P;
+                X[0] ^= t;
+                X[i] ^= t;
+            }
+        }
+    }
+    X[1] ^= X[0];
+    X[2] ^= X[1];
+    uint32_t t = 0;
+#pragma unroll
+    for (uint32_t Q = 128; Q > 1; Q >>= 1)
+        if (X[2] & Q) t ^= Q - 1;
+    X[0] ^= t;
+    X[1] ^= t;
+    X[2] ^= t;
+    auto spread = [](uint32_t v) {  // bit k -> bit 3k (8 bits)
+        v = (v | (v << 8)) & 0x0000F00Fu;
+        v = (v | (v << 4)) & 0x000C30C3u;
+        v = (v | (v << 2)) & 0x00249249u;
+        return v;
+    };
+    return (spread(X[0]) << 2) | (spread(X[1]) << 1) | spread(X[2]);
+}
 constexpr int kQsItems = 16;
 constexpr int kQsTile = kQsNT * kQsItems;
 
@@ -256,7 +297,17 @@ __global__ __launch_bounds__(NT) void k_qkeys(const double* __restrict__ q, size
     for (int k = 0; k < ITEMS; ++k) {
         const size_t i = base + (size_t)k * NT + tid;
         if (i < n) {
-            const uint32_t key = query_morton30(q[3 * i], q[3 * i + 1], q[3 * i + 2], lx, ly, lz, hx, hy, hz) >> lo_bit;
+            uint32_t key = query_morton30(q[3 * i], q[3 * i + 1], q[3 * i + 2], lx, ly, lz, hx, hy, hz) >> lo_bit;
+            if (MSH_QORDER_HILBERT) {  // the same 256^3 cells (lo_bit == 6) in Hilbert order
+                auto axis = [](uint32_t m, int k) {  // every third bit of the 24-bit code, from bit k
+                    uint32_t v = (m >> k) & 0x00249249u;
+                    v = (v | (v >> 2)) & 0x000C30C3u;
+                    v = (v | (v >> 4)) & 0x0000F00Fu;
+                    v = (v | (v >> 8)) & 0x000000FFu;
+                    return v;
+                };
+                key = hilbert24(axis(key, 2), axis(key, 1), axis(key, 0));
+            }
             keys[i] = key;
             atomicAdd(&h[w][key & 255u], 1u);
         }

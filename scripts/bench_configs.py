@@ -324,6 +324,11 @@ def c5(reps):
     ndc = torch.empty((C, P), dtype=torch.float64, device="cuda")
     wall_v = _device_timed(lambda: visibility_device(tree, dc, vis, ndc, dvn), reps)
     k_v = kernel_ms("visibility")
+    # the same call through the numpy entry point (visibility_compute: the (C, P) outputs downloaded camera chunk by
+    # camera chunk into pinned pool arrays); its bound is the kernel plus 12 B per ray over the host link
+    from mesh_amd import visibility as VIS
+    _, wall_vnp = timed(lambda: VIS.visibility_compute(cams=cams, tree=tree, n=vn), reps)
+    link_gbs = 57.0  # pinned device-to-host rate of the box (profiles/r04_pcie_probe.json)
     _native.check(_native.lib().msh_visibility_stats(tree.ptr, dc.data_ptr(), C, 1e-3, _native.ctypes.byref(nodes),
                                                       _native.ctypes.byref(leaves)))
     R = C * P
@@ -340,6 +345,10 @@ def c5(reps):
                                          "cache-served re-reads included",
                             "measured": pmc_of("c5", "msh::k_rays<0, false>", S)},
             "visibility": {"rays_per_s_device": R / wall_v, "kernel_ms": k_v, "wall_ms_device": wall_v * 1e3,
+                           "rays_per_s_numpy_api": R / wall_vnp, "ms_numpy_api": wall_vnp * 1e3,
+                           "numpy_bound_ms": k_v + 12.0 * R / link_gbs / 1e6,
+                           "numpy_over_bound": wall_vnp * 1e3 / (k_v + 12.0 * R / link_gbs / 1e6),
+                           "numpy_bound_note": "kernel + 12 B per ray of outputs at %.0f GB/s (no overlap)" % link_gbs,
                            "nodes_per_ray": nn_v, "leaves_per_ray": nl_v, "bytes_per_ray": b_v,
                            "achieved_GBps": R * b_v / (k_v / 1e3) / 1e9,
                            "frac_of_8TBps": R * b_v / (k_v / 1e3) / 8e12,

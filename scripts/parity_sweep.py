@@ -3,7 +3,10 @@ brute force), one JSON line per config:
   c3  bench.py's exact query stream (100M uniform queries generated in HBM, seed 3) through the device entry
       point; K random rows plus the rows nearest the sphere's centre (the deferred pass-2 queries);
   c2  the 10M C2 queries through the numpy entry point (aabbtree_nearest); K random rows;
-  c5  the 10M C5 nearest_alongnormal rays through the numpy entry point; K random rays.
+  c5  the 10M C5 nearest_alongnormal rays through the numpy entry point; --rays random rays;
+  c5v visibility_compute (numpy) on the C5 mesh from the 64 Fibonacci cameras with vertex normals: --pairs
+      (camera, vertex) pairs (8 cameras x pairs/8 vertices), and --sensor-pairs more with random sensors
+      (2 cameras), against oracle.brute_visibility (every one of the 5M triangles).
 Every checked row must equal the oracle's exhaustive brute force bit for bit (same tie rule).
 
     python scripts/parity_sweep.py [--configs c3,c2,c5] [--rows 20000] [--centre 2000]
@@ -86,9 +89,13 @@ def sweep_c5(args):
     v, f = W.c5_mesh()
     p, n, _, _ = W.c5_rays(v, f)
     d, face, pt = spatialsearch.aabbtree_nearest_alongnormal(spatialsearch.aabbtree_compute(v, f), p, n)
-    idx = np.random.default_rng(13).choice(p.shape[0], args.rows // 5, replace=False)
+    idx = np.random.default_rng(13).choice(p.shape[0], args.rays, replace=False)
     t0 = time.perf_counter()
-    bd, bf, bpt = O.brute_alongnormal(v, f, p[idx], n[idx])
+    parts = []
+    for c0 in range(0, idx.size, 2000):  # progress lines
+        parts.append(O.brute_alongnormal(v, f, p[idx[c0:c0 + 2000]], n[idx[c0:c0 + 2000]]))
+        print("c5 brute force: %d / %d rays" % (min(c0 + 2000, idx.size), idx.size), file=sys.stderr, flush=True)
+    bd, bf, bpt = (np.concatenate([c[k] for c in parts]) for k in range(3))
     hit = bd < 1e100
     same_pt = np.all((pt[idx] == bpt) | ~hit[:, None], axis=1)
     bad = np.nonzero((d[idx] != bd) | (face[idx] != bf) | ~same_pt)[0]
@@ -98,17 +105,58 @@ def sweep_c5(args):
                 check="dist, face and (for hits) point bit-exact vs oracle.brute_alongnormal")
 
 
+def sweep_c5v(args):
+    from mesh_amd import spatialsearch, visibility
+    from mesh_amd.mesh import Mesh
+    from oracle import oracle as O
+    import workloads as W
+    v, f = W.c5_mesh()
+    t = spatialsearch.aabbtree_compute(v, f)
+    vn = Mesh(v=v, f=f).estimate_vertex_normals()
+    cams = W.fibonacci_cameras(64, 3.0)
+    P = v.shape[0]
+    rng = np.random.default_rng(14)
+    vis, ndc = visibility.visibility_compute(cams=cams, tree=t, n=vn)
+    ci = np.sort(rng.choice(64, 8, replace=False))
+    vi = np.sort(rng.choice(P, args.pairs // 8, replace=False))
+    t0 = time.perf_counter()
+    bv, bn = [], []
+    for c in ci:  # progress lines
+        a, b = O.brute_visibility(v, f, cams[c:c + 1], n=vn, src_idx=vi)
+        bv.append(a)
+        bn.append(b)
+        print("c5v brute force: camera %d (%d vertices)" % (c, vi.size), file=sys.stderr, flush=True)
+    bv, bn = np.concatenate(bv), np.concatenate(bn)
+    bad = int(np.count_nonzero((vis[ci][:, vi] != bv) | (ndc[ci][:, vi] != bn)))
+    # sensors (visibility.cpp:79-85,96-111): 2 cameras with random sensor frames
+    sc = np.sort(rng.choice(64, 2, replace=False))
+    sens = rng.normal(size=(2, 9))
+    svis, sndc = visibility.visibility_compute(cams=cams[sc], tree=t, n=vn, sensors=sens)
+    si = np.sort(rng.choice(P, args.sensor_pairs // 2, replace=False))
+    sv, sn = O.brute_visibility(v, f, cams[sc], n=vn, sensors=sens, src_idx=si)
+    sbad = int(np.count_nonzero((svis[:, si] != sv) | (sndc[:, si] != sn)))
+    return dict(workload="C5 visibility_compute (numpy entry point) on the 5M-face bumped icosphere, 64 Fibonacci cameras, "
+                         "vertex normals; sensor frames on 2 cameras",
+                pairs_checked=int(bv.size), sensor_pairs_checked=int(sv.size), rows_checked=int(bv.size + sv.size),
+                visible_frac=float(bv.mean()), sensor_visible_frac=float(sv.mean()), mismatches=bad + sbad,
+                brute_force_s=time.perf_counter() - t0,
+                check="vis and n.dir bit-exact vs oracle.brute_visibility (any hit over all 5M triangles)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="c3")
     ap.add_argument("--rows", type=int, default=20000)
     ap.add_argument("--centre", type=int, default=2000)
+    ap.add_argument("--rays", type=int, default=20000, help="c5: alongnormal rays checked")
+    ap.add_argument("--pairs", type=int, default=18000, help="c5v: (camera, vertex) pairs without sensors")
+    ap.add_argument("--sensor-pairs", type=int, default=2000, help="c5v: pairs with sensors")
     args = ap.parse_args()
     from mesh_amd import _native
     _native.set_device(0)
     fails = 0
     for c in args.configs.split(","):
-        r = {"c3": sweep_c3, "c2": sweep_c2, "c5": sweep_c5}[c](args)
+        r = {"c3": sweep_c3, "c2": sweep_c2, "c5": sweep_c5, "c5v": sweep_c5v}[c](args)
         r["config"] = c
         r["build_id"] = _native.build_id()
         fails += r["mismatches"]
