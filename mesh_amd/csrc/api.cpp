@@ -317,8 +317,14 @@ static void free_entry_cut(msh_tree* t) {
     t->cut_ms = 0.0;
 }
 
+#ifndef MSH_CUT_PER_LEAF
+#define MSH_CUT_PER_LEAF 8
+#endif
+#ifndef MSH_CUT_MAX_LOG2
+#define MSH_CUT_MAX_LOG2 23
+#endif
 static int build_entry_cut(msh_tree* t) {
-    const size_t cells = std::min<size_t>(8 * t->T, (size_t)1 << 23);
+    const size_t cells = std::min<size_t>((size_t)MSH_CUT_PER_LEAF * t->T, (size_t)1 << MSH_CUT_MAX_LOG2);
     const int G = t->cut_req > 0 ? t->cut_req : std::max(16, (int)std::lround(std::cbrt((double)cells)));
     double half[3], H = 0.0, lo[3], w[3];
     for (int k = 0; k < 3; ++k) {

@@ -1418,11 +1418,6 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     a.n_deferred = a.counters + 8 * 32;
     a.n_resume = a.counters + 10 * 32;
     MSH_HIP(hipMemsetAsync(a.counters, 0, 11 * 32 * sizeof(unsigned), s));  // + the pass-2 item counter
-    // leader ordering: closest-point launches over a Morton-sorted slot order (records in a.res)
-// leader phases only for trees of >= kLeadMinLeaves leaves: on a small tree the hint saves little and the
-// three dependent launches serialise their slowest tiles (C1: 0.56 -> 0.29 ms)
-    const bool lead = kLead > 1 && (MODE == 0 || MODE == 3) && a.res != nullptr && a.S >= 64 * (size_t)kLead &&
-                      a.T >= kLeadMinLeaves;
     const size_t n_lead = (a.S + kLead - 1) / kLead;
     const unsigned max_tiles = (unsigned)((a.S + 63) / 64);
     const unsigned nblk_max = std::min<unsigned>((max_tiles + 3) / 4, ncu * kKnnBlocksPerCU);
@@ -1446,6 +1441,14 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         a.list = (MODE == 0 || MODE == 3) && hook != 0 && tree->B * tree->T < kListMaxLeaves;
         list_pf = a.list && hook != 2 && tree->B * tree->T <= kEnt4MaxLeaves;
     }
+    // leader ordering: closest-point launches over a sorted slot order (records in a.res); leader phases only for
+    // trees of >= kLeadMinLeaves leaves (on a small tree the hint saves little and the three dependent launches
+    // serialise their slowest tiles: C1 0.56 -> 0.29 ms), and only without the entry cut's cell hints: every query inside the cut's grid starts from its cell's entries
+    // with the hint leaf of the cell centre, and the leader launch's hints for the followers no longer pay for the
+    // launch (C3 100M: 1985-1990 -> 2150-2179 M q/s without leader phases; one N = 8 shard of 12.5M rows 9.0 ->
+    // 7.55 ms, profiles/r05_ab_leaders_sort_resume.jsonl); batched trees and trees without a cut keep them
+    const bool lead = kLead > 1 && (MODE == 0 || MODE == 3) && a.res != nullptr && a.S >= 64 * (size_t)kLead &&
+                      a.T >= kLeadMinLeaves && !(a.list && a.cut_hint);
     a.max_deferred = (unsigned)std::min<size_t>(a.S, (a.S / 16) + 65536);
     DevBuf& dbuf = ws.flags;
     MSH_TRY(dbuf.reserve((size_t)a.max_deferred * sizeof(DeferRec)));

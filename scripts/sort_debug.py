@@ -29,6 +29,55 @@ def keys24(q, lo, hi):
     return (out >> np.uint32(6)) & np.uint32(0xFFFFFF)
 
 
+def hilbert24(keys):
+    """24-bit Hilbert indices of the 256^3 cells whose 24-bit Morton codes are `keys` (sort.hip hilbert24: Skilling's
+    axes-to-transpose, then the transposed bits interleaved, axis 0 first)"""
+    keys = np.asarray(keys, dtype=np.uint32)
+
+    def axis(m, k):
+        v = (m >> np.uint32(k)) & np.uint32(0x00249249)
+        v = (v | (v >> np.uint32(2))) & np.uint32(0x000C30C3)
+        v = (v | (v >> np.uint32(4))) & np.uint32(0x0000F00F)
+        v = (v | (v >> np.uint32(8))) & np.uint32(0x000000FF)
+        return v
+
+    X = [axis(keys, 2), axis(keys, 1), axis(keys, 0)]
+    Q = 128
+    while Q > 1:
+        P = np.uint32(Q - 1)
+        for i in range(3):
+            m = (X[i] & np.uint32(Q)) != 0
+            x0 = np.where(m, X[0] ^ P, X[0])
+            t = np.where(m, np.uint32(0), (X[0] ^ X[i]) & P)
+            if i == 0:
+                X[0] = x0
+            else:
+                X[0] = x0 ^ t
+                X[i] = X[i] ^ t
+        Q >>= 1
+    X[1] = X[1] ^ X[0]
+    X[2] = X[2] ^ X[1]
+    t = np.zeros_like(X[2])
+    Q = 128
+    while Q > 1:
+        t = np.where((X[2] & np.uint32(Q)) != 0, t ^ np.uint32(Q - 1), t)
+        Q >>= 1
+    X = [x ^ t for x in X]
+
+    def spread(v):
+        v = (v | (v << np.uint32(8))) & np.uint32(0x0000F00F)
+        v = (v | (v << np.uint32(4))) & np.uint32(0x000C30C3)
+        v = (v | (v << np.uint32(2))) & np.uint32(0x00249249)
+        return v
+
+    return (spread(X[0]) << np.uint32(2)) | (spread(X[1]) << np.uint32(1)) | spread(X[2])
+
+
+def order_keys(q, lo, hi):
+    """the keys the query order sorts by (sort.hip k_qkeys): Hilbert indices of the 24-bit Morton cells"""
+    return hilbert24(keys24(q, lo, hi))
+
+
 def sort_box(info):
     """The cells of query_morton: the tree's scene box widened by 10 % of its extent per side, in fp32."""
     lo, hi = [], []
@@ -56,7 +105,7 @@ def main():
                                                          torch.cuda.current_stream().cuda_stream))
         torch.cuda.synchronize()
         p = p.cpu().numpy().astype(np.int64)
-        ref = np.argsort(keys24(x.cpu().numpy(), lo, hi), kind="stable")
+        ref = np.argsort(order_keys(x.cpu().numpy(), lo, hi), kind="stable")
         print(n, "equal to the stable argsort:", bool(np.array_equal(p, ref)), flush=True)
 
 

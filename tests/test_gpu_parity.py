@@ -334,12 +334,12 @@ def test_c3_replication_roundtrip():
 
 
 def test_query_order_equals_stable_argsort():
-    # the closest-point path's query order (msh_tree_query_order: Morton codes + the 3-pass LDS radix sort) equals
-    # numpy's stable argsort of the same 24-bit Morton keys (scripts/sort_debug.keys24, the kernel's fp32
-    # arithmetic): on the C3 stream (100M rows), a ragged size, a size below one tile and rows with NaN / inf
+    # the closest-point path's query order (msh_tree_query_order: Hilbert indices of the 24-bit Morton cells + the
+    # 3-pass LDS radix sort) equals numpy's stable argsort of the same keys (scripts/sort_debug.order_keys, the kernel's
+    # fp32 arithmetic): on the C3 stream (100M rows), a ragged size, a size below one tile and rows with NaN / inf
     import torch
     from mesh_amd import _native, spatialsearch
-    from scripts.sort_debug import keys24, sort_box
+    from scripts.sort_debug import order_keys, sort_box
     v, f = W.c3_mesh()
     t = spatialsearch.aabbtree_compute(v, f)
     lo, hi = sort_box(t.info())
@@ -354,7 +354,7 @@ def test_query_order_equals_stable_argsort():
         _native.check(_native.lib().msh_tree_query_order(t.ptr, x.data_ptr(), x.shape[0], p.data_ptr(),
                                                          torch.cuda.current_stream().cuda_stream))
         torch.cuda.synchronize()
-        ref = np.argsort(keys24(x.cpu().numpy(), lo, hi), kind="stable")
+        ref = np.argsort(order_keys(x.cpu().numpy(), lo, hi), kind="stable")
         assert np.array_equal(p.cpu().numpy().astype(np.int64), ref), "rows %d" % x.shape[0]
 
 
