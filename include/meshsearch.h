@@ -145,7 +145,7 @@ int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* 
  * metric never hold it.  Trees of < 4096 faces never get one.  That first call is synchronous, also for the
  * *_device entry points (the cut's build waits for its own cell-centre queries): a caller that captures
  * *_device calls in a graph or needs them asynchronous makes one small query first (or sets G = 0).
- *   G < 0: automatic grid (about 8 cells per face, at most 2^23 cells: C3 G = 200, 544 MB) — the default;
+ *   G < 0: automatic grid (about 64 cells per face, at most 2^26 cells: C3 G = 400, 4.4 GB) — the default;
  *   G = 0: no cut (frees one already built); queries start at the root;
  *   G > 0: G^3 cells.
  * Changing G frees the current cut; the next closest-point query builds the new one.  A cut that cannot be

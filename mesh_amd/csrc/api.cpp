@@ -291,8 +291,8 @@ struct WsOrder {
 
 // Entry cut of a single triangle tree (nearest.hip cut_start / k_cut_build): a G^3 grid over the scene box
 // widened by 1/4 on every side (each axis at least 1/20 of the largest, so flat meshes get cells of a sane
-// shape), ~8 cells per leaf up to 2^23 cells (C3: G = 200, 8M cells, 544 MB; G = 64 / 126 / 160: 1718 /
-// 1742-1765 / 1782 M q/s against 1789-1800); the cell centres are answered
+// shape), MSH_CUT_PER_LEAF cells per leaf up to 2^MSH_CUT_MAX_LOG2 cells (below; round 3 with leader phases:
+// G = 64 / 126 / 160: 1718 / 1742-1765 / 1782 M q/s against 1789-1800 at G = 200); the cell centres are answered
 // by the tree itself, then every cell's start entries are cut from the root.  Trees under kCutMinLeaves
 // leaves start at the root (their top levels are few).  Built lazily by the first closest-point query
 // (ensure_entry_cut), so ray-only, visibility and normals-metric trees never pay its memory or build time;
@@ -317,11 +317,16 @@ static void free_entry_cut(msh_tree* t) {
     t->cut_ms = 0.0;
 }
 
+// cells per leaf and the cap of the automatic grid, C3 (1,003,520 faces) in M q/s: 8 per leaf, 2^23 cells: G = 200,
+// 46.9 node visits per query, 2156-2213; 16, 2^25: G = 252, 45.2 visits, 2238; 32, 2^25: G = 318 (2.2 GB, built in
+// 35 ms), 43.6 visits, 2247-2290 (profiles/r05_ab_noleaders_cut.jsonl); in another session 32: 2261-2286, 64, 2^26:
+// G = 400 (4.4 GB, 65 ms), 42.2 visits, 2293-2321, 128, 2^27: G = 505 (8.8 GB, 165 ms), 41.0 visits, 2297-2333
+// (profiles/r05_ab_cut_size.jsonl).  The grid is derived data of a kept tree: 64 per leaf.
 #ifndef MSH_CUT_PER_LEAF
-#define MSH_CUT_PER_LEAF 8
+#define MSH_CUT_PER_LEAF 64
 #endif
 #ifndef MSH_CUT_MAX_LOG2
-#define MSH_CUT_MAX_LOG2 23
+#define MSH_CUT_MAX_LOG2 26
 #endif
 static int build_entry_cut(msh_tree* t) {
     const size_t cells = std::min<size_t>((size_t)MSH_CUT_PER_LEAF * t->T, (size_t)1 << MSH_CUT_MAX_LOG2);
@@ -407,7 +412,7 @@ static int build_entry_cut(msh_tree* t) {
 }
 
 // First closest-point query of a handle: build its entry cut.  The cut is an optimisation, so a failure (device
-// memory, most likely: 544 MB plus ~420 MB of temporaries on C3) is not the query's: the partial buffers are
+// memory, most likely: 4.4 GB plus ~3.4 GB of temporaries on C3) is not the query's: the partial buffers are
 // freed, the error is cleared, the handle remembers the failure and its queries start at the root.
 static void ensure_entry_cut(msh_tree* t) {
     if (t->cut_state != kCutPending) return;

@@ -156,12 +156,13 @@ class Mesh(object):
         return self.closest_faces_and_points(vertices)[1]
 
     def closest_faces_and_points(self, vertices):
-        # a tree built for one query batch, as the reference does (mesh.py:454-455).  Its entry cut (about 8 grid
-        # cells per face, at most 2^23, each answered at build time) pays off only when the batch is large against
-        # it: C2's 10M queries on 13,776 faces run 25 -> 21 ms with it, C3's 100M on 1M faces 149 -> 198 ms
-        # (profiles/r04_facade_cut_policy.json), so the one-shot tree builds it only for >= 32 queries per cell
+        # a tree built for one query batch, as the reference does (mesh.py:454-455).  Its entry cut (each cell
+        # answered at build time) pays off only when the batch is large against it: with about 8 grid cells per face
+        # (at most 2^23) C2's 10M queries on 13,776 faces run 25 -> 21 ms with it, C3's 100M on 1M faces 149 -> 198 ms
+        # (profiles/r04_facade_cut_policy.json), so the one-shot tree takes that coarser grid (a kept tree's default
+        # is finer) and builds it only for >= 32 queries per cell
         tree = self.compute_aabb_tree()
         n_q = int(np.prod(np.shape(vertices)[:-1])) if np.ndim(vertices) > 1 else 0
-        if n_q < 32 * min(8 * len(self.f), 1 << 23):
-            tree.cpp_handle.set_entry_cut(0)
+        cells = min(8 * len(self.f), 1 << 23)
+        tree.cpp_handle.set_entry_cut(max(16, int(round(cells ** (1.0 / 3.0)))) if n_q >= 32 * cells else 0)
         return tree.nearest(vertices)

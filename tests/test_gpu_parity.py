@@ -210,7 +210,7 @@ def test_entry_cut_bit_exact(oracle):
     from mesh_amd import spatialsearch
     v, f = W.c3_mesh()
     rng = np.random.default_rng(41)
-    G = int(round(np.cbrt(8 * f.shape[0])))
+    G = int(round(np.cbrt(min(64 * f.shape[0], 1 << 26))))  # api.cpp build_entry_cut's automatic grid
     lo, w = -1.25, 2.5 / G  # scene box +-1 (icosphere vertices on the unit sphere), widened by 1/4
     on_faces = rng.uniform(-1.2, 1.2, (20_000, 3))
     on_faces[np.arange(20_000), rng.integers(0, 3, 20_000)] = lo + rng.integers(0, G + 1, 20_000) * w
