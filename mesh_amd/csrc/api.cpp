@@ -228,7 +228,8 @@ static void free_tree(msh_tree* t) {
     (void)hipSetDevice(t->device);
     if (t->stream) (void)hipStreamSynchronize(t->stream);
     if (t->ws_done) (void)hipEventSynchronize(t->ws_done);
-    if (t->kind == kTriangles && t->B == 1) ws_pool().give(t->device, t->ws);
+    // triangle trees (single, batched, normals metric) took one when they were built, if one was idle
+    if (t->kind != kPoints) ws_pool().give(t->device, t->ws);
     t->ws.release();
     if (t->d_v) (void)hipFree(t->d_v);
     if (t->d_nodes) (void)hipFree(t->d_nodes);
@@ -475,8 +476,8 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
     (void)hipStreamSynchronize(s);
     dF.release(); dLo.release(); dHi.release(); dOrder.release();
     t->ws.release();  // build scratch (sort buffers, parents, ranges) is not needed by queries
-    // a freed tree's query workspace, if one is idle; only kinds that give it back at free_tree take it
-    if (st == MSH_OK && t->kind == kTriangles && t->B == 1) ws_pool().take(t->device, t->ws);
+    // a freed tree's query workspace, if one is idle (free_tree gives it back)
+    if (st == MSH_OK) ws_pool().take(t->device, t->ws);
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return st;
@@ -2161,11 +2162,13 @@ int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size
         if (e != hipSuccess) { set_error("msh_batch_build: %s", hipGetErrorString(e)); st = MSH_ENOMEM; break; }
         // the vertices (C4: 496 MB) through the pinned staging pipeline, a chunk of meshes at a time (one pageable
         // hipMemcpy of them ran well below the host link's rate)
+        // chunks of ~32 MB, so the host's copies into the pinned slabs overlap the uploads
         const std::vector<HostArr> va = {{v, nullptr, P * 3 * sizeof(double)}};
+        const std::vector<size_t> vplan = {std::max<size_t>(1, ((size_t)32 << 20) / (P * 3 * sizeof(double)))};
         st = pipelined(t, B, va, [&](size_t m0, size_t nm, const std::vector<char*>& d) {
             MSH_HIP(hipMemcpyAsync(t->d_v + m0 * P * 3, d[0], nm * P * 3 * sizeof(double), hipMemcpyDeviceToDevice, s));
             return MSH_OK;
-        });
+        }, &vplan);
         if (st != MSH_OK) break;
         if ((st = upload(dF, f, 3 * T, s)) != MSH_OK) break;
         if ((st = dLo.reserve(3 * B * T * sizeof(double))) != MSH_OK) break;
@@ -2189,6 +2192,7 @@ int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size
     (void)hipStreamSynchronize(s);
     dF.release(); dLo.release(); dHi.release(); dOrder.release();
     t->ws.release();
+    if (st == MSH_OK) ws_pool().take(t->device, t->ws);  // a freed tree's query workspace, if one is idle
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (st != MSH_OK) {

@@ -437,6 +437,122 @@ __global__ __launch_bounds__(NT) void k_qscatter(const void* __restrict__ in, vo
     }
 }
 
+// Split-array form of the middle passes (MSH_QSORT_SPLIT): keys and rows in two u32 arrays, so a histogram pass
+// reads 4 B per element instead of the packed 8 B (16384-key tiles keep a digit run at 256 B per array).
+template <int NT, int ITEMS>
+__global__ __launch_bounds__(NT) void k_qhist32(const uint32_t* __restrict__ keys, size_t n, int shift,
+                                                uint32_t* __restrict__ hist, unsigned nb) {
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t h[NW][256];
+    const int tid = threadIdx.x, w = tid >> 6;
+    for (int i = tid; i < NW * 256; i += NT) (&h[0][0])[i] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * (NT * ITEMS);
+    uint32_t e[ITEMS];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const size_t i = base + (size_t)k * NT + tid;
+        e[k] = i < n ? keys[i] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k)
+        if (e[k] != 0xFFFFFFFFu) atomicAdd(&h[w][(e[k] >> shift) & 255u], 1u);
+    __syncthreads();
+    for (int d = tid; d < 256; d += NT) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int x = 0; x < NW; ++x) c += h[x][d];
+        hist[(size_t)d * nb + blockIdx.x] = c;
+    }
+}
+
+// ROWS_IN: rows from rin (else the index); KEYS_OUT: keys written to kout (else the rows only).  Staged and ranked as
+// k_qscatter.
+template <int NT, int ITEMS, bool ROWS_IN, bool KEYS_OUT>
+__global__ __launch_bounds__(NT) void k_qscatter2(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin,
+                                                  uint32_t* __restrict__ kout, uint32_t* __restrict__ rout, size_t n,
+                                                  int shift, const uint32_t* __restrict__ offs, unsigned nb) {
+    constexpr int NW = NT / 64, TILE = NT * ITEMS, WI = 64 * ITEMS;
+    static_assert(NT >= 256, "one thread per digit");
+    __shared__ uint32_t wcnt[NW][256];
+    __shared__ uint32_t gbase[256];
+    __shared__ uint32_t ssum[4];
+    __shared__ unsigned long long stage[TILE];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    for (int i = tid; i < NW * 256; i += NT) (&wcnt[0][0])[i] = 0;
+    const uint32_t g_off = tid < 256 ? offs[(size_t)tid * nb + blockIdx.x] : 0u;
+    __syncthreads();
+    const size_t tile0 = (size_t)blockIdx.x * TILE;
+    const size_t base = tile0 + (size_t)w * WI;
+    const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    unsigned long long ee[ITEMS];
+    uint32_t rr[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const size_t i = base + (size_t)it * 64 + lane;
+        ee[it] = i < n ? (((unsigned long long)kin[i] << 32) | (ROWS_IN ? rin[i] : (uint32_t)i)) : 0ull;
+    }
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const size_t i = base + (size_t)it * 64 + lane;
+        const bool valid = i < n;
+        const uint32_t d = (uint32_t)(ee[it] >> (32 + shift)) & 255u;
+        unsigned long long peers = __ballot(valid);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const unsigned long long m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t prev = valid ? wcnt[w][d] : 0u;
+        if (valid && (peers & lt) == 0ull) wcnt[w][d] = prev + (uint32_t)__popcll(peers);
+        rr[it] = prev + (uint32_t)__popcll(peers & lt);
+    }
+    __syncthreads();
+    uint32_t tot = 0;
+    if (tid < 256) {
+#pragma unroll
+        for (int x = 0; x < NW; ++x) tot += wcnt[x][tid];
+    }
+    uint32_t incl = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (w < 4 && lane == 63) ssum[w] = incl;
+    __syncthreads();
+    if (tid < 256) {
+        uint32_t run = incl - tot;
+        for (int k = 0; k < w; ++k) run += ssum[k];
+        gbase[tid] = g_off - run;
+#pragma unroll
+        for (int x = 0; x < NW; ++x) {
+            const uint32_t c = wcnt[x][tid];
+            wcnt[x][tid] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITEMS; ++it) {
+        const size_t i = base + (size_t)it * 64 + lane;
+        if (i < n) stage[wcnt[w][(uint32_t)(ee[it] >> (32 + shift)) & 255u] + rr[it]] = ee[it];
+    }
+    __syncthreads();
+    const uint32_t tn = (uint32_t)(n - tile0 < (size_t)TILE ? n - tile0 : (size_t)TILE);
+    for (uint32_t p = tid; p < tn; p += NT) {
+        const unsigned long long e = stage[p];
+        const uint32_t dst = gbase[(uint32_t)(e >> (32 + shift)) & 255u] + p;
+        if (KEYS_OUT) kout[dst] = (uint32_t)(e >> 32);
+        rout[dst] = (uint32_t)e;
+    }
+}
+
+#ifndef MSH_QSORT_SPLIT
+#define MSH_QSORT_SPLIT 1
+#endif
+
 int query_sort(const float* lo, const float* hi, const double* d_q, size_t S, int lo_bit, Workspace& ws, hipStream_t s) {
     if (S == 0) return MSH_OK;
     if (S > 0xFFFFFFFFull || lo_bit < 6) {
@@ -460,6 +576,27 @@ int query_sort(const float* lo, const float* hi, const double* d_q, size_t S, in
     }
     TimedLaunch tl("sort", s);
     MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
+    if (MSH_QSORT_SPLIT) {
+        uint32_t* k0 = ws.keys.as<uint32_t>();
+        uint32_t* k1 = ws.keys_alt.as<uint32_t>();
+        uint32_t* r1 = k1 + S;
+        uint32_t* k2 = ws.vals_alt.as<uint32_t>();
+        uint32_t* r2 = k2 + S;
+        k_qscatter2<kQsNT, kQsItems, false, true><<<nb, kQsNT, 0, s>>>(k0, nullptr, k1, r1, S, 0, hist, nb);
+        MSH_HIP(hipGetLastError());
+        k_qhist32<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(k1, S, 8, hist, nb);
+        MSH_HIP(hipGetLastError());
+        MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
+        k_qscatter2<kQsNT, kQsItems, true, true><<<nb, kQsNT, 0, s>>>(k1, r1, k2, r2, S, 8, hist, nb);
+        MSH_HIP(hipGetLastError());
+        k_qhist32<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(k2, S, 16, hist, nb);
+        MSH_HIP(hipGetLastError());
+        MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
+        k_qscatter2<kQsNT, kQsItems, true, false><<<nb, kQsNT, 0, s>>>(k2, r2, nullptr, ws.vals.as<uint32_t>(), S, 16,
+                                                                        hist, nb);
+        MSH_HIP(hipGetLastError());
+        return MSH_OK;
+    }
     k_qscatter<kQsNT, kQsItems, false, true><<<nb, kQsNT, 0, s>>>(ws.keys.ptr, A, S, 0, hist, nb);
     MSH_HIP(hipGetLastError());
     k_qhist64<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(A, S, 8, hist, nb);
