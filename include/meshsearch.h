@@ -298,18 +298,20 @@ int msh_host_pool_trim(void);
 size_t msh_host_pool_bytes(void);
 
 /* ---- device memory kept between handles (no reference counterpart) ----
- * Two process-wide caches keep device memory after the handles that used it are freed, so a caller that builds
+ * Three process-wide caches keep device memory after the handles that used it are freed, so a caller that builds
  * a tree per call (Mesh.closest_faces_and_points, mesh.py:454-455) does not reallocate it every call:
+ *  - every device block the library frees (tree buffers, build temporaries, scratch) is cached for the next
+ *    request of a similar size on its device, up to MESH_AMD_DEVICE_CACHE_MB (default 16384; 0 turns it off);
  *  - the query workspace of a freed triangle tree (sort keys, permutations, spill stacks, deferred lists:
  *    ~80 B per query of its largest call, ~8 GB at 100M queries), one idle workspace per device, handed to the
  *    next triangle tree built on that device;
  *  - up to two idle sets of host-call staging slabs per device (three device slabs of chunk x row bytes each,
  *    plus two page-locked host slabs).
- * msh_device_pool_trim frees both (idle entries only: memory held by live handles stays with them);
- * msh_device_pool_bytes reports the device bytes they hold (either pointer may be NULL).  A process that
+ * msh_device_pool_trim frees all three (idle entries only: memory held by live handles stays with them);
+ * msh_device_pool_bytes reports the device bytes they hold (any pointer may be NULL).  A process that
  * shares the GPU with other allocators (torch) calls the trim after freeing its handles. */
 int msh_device_pool_trim(void);
-int msh_device_pool_bytes(uint64_t* workspace, uint64_t* staging);
+int msh_device_pool_bytes(uint64_t* workspace, uint64_t* staging, uint64_t* cached);
 
 #ifdef __cplusplus
 }

@@ -92,7 +92,7 @@ SIGNATURES = [
     ("msh_host_pool_trim", _i, []),
     ("msh_host_pool_bytes", _sz, []),
     ("msh_device_pool_trim", _i, []),
-    ("msh_device_pool_bytes", _i, [_c_u64_p, _c_u64_p]),
+    ("msh_device_pool_bytes", _i, [_c_u64_p, _c_u64_p, _c_u64_p]),
 ]
 
 
@@ -374,10 +374,10 @@ def device_pool_trim():
 
 
 def device_pool_bytes():
-    """msh_device_pool_bytes -> (workspace bytes, staging bytes) kept on the devices between handles."""
-    w, s = ctypes.c_uint64(0), ctypes.c_uint64(0)
-    check(lib().msh_device_pool_bytes(ctypes.byref(w), ctypes.byref(s)))
-    return w.value, s.value
+    """msh_device_pool_bytes -> (workspace, staging, cached block) bytes kept on the devices between handles."""
+    w, s, c = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+    check(lib().msh_device_pool_bytes(ctypes.byref(w), ctypes.byref(s), ctypes.byref(c)))
+    return w.value, s.value, c.value
 
 
 def timing_enable(on=True):

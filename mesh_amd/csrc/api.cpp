@@ -41,22 +41,174 @@ void set_error(const char* fmt, ...) {
     g_err = buf;
 }
 
+// Device allocations of the library (tree buffers, build temporaries, scratch) go through one process-wide cache: a
+// freed block is kept for the next request of a similar size on its device instead of being unmapped, so a caller
+// that builds a tree per call (Mesh.closest_faces_and_points; C4's batched build + query: ~11 GB of buffers per
+// call) does not pay hipMalloc / hipFree of gigabytes every time.  A free waits for the device as hipFree does (a
+// block still read by queued launches is never handed out again), the cache holds at most MESH_AMD_DEVICE_CACHE_MB
+// (default 16384; 0 turns it off) and msh_device_pool_trim empties it.
+class DevCache {
+  public:
+    hipError_t alloc(void** p, size_t bytes) {
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        const size_t want = grain(bytes);
+        if (cap() > 0) {
+            std::lock_guard<std::mutex> g(mu_);
+            auto& fl = free_[dev];
+            auto it = fl.lower_bound(want);
+            if (it != fl.end() && it->first <= want + want / 4) {
+                *p = it->second;
+                cached_ -= it->first;
+                fl.erase(it);
+                return hipSuccess;
+            }
+        }
+        e = hipMalloc(p, want);
+        if (e == hipErrorOutOfMemory) {  // the cached blocks of this device go first
+            (void)hipGetLastError();
+            trim_device(dev);
+            e = hipMalloc(p, want);
+        }
+        if (e != hipSuccess) return e;
+        std::lock_guard<std::mutex> g(mu_);
+        blocks_[*p] = Blk{want, dev};
+        return hipSuccess;
+    }
+    hipError_t free(void* p) {
+        if (!p) return hipSuccess;
+        Blk b;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            auto it = blocks_.find(p);
+            if (it == blocks_.end()) return hipFree(p);  // not ours
+            b = it->second;
+            if (cap() == 0) {
+                blocks_.erase(it);
+                return hipFree(p);
+            }
+        }
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != b.dev) (void)hipSetDevice(b.dev);
+        const hipError_t e = hipDeviceSynchronize();  // the wait hipFree would make
+        if (cur != b.dev && cur >= 0) (void)hipSetDevice(cur);
+        std::vector<std::pair<void*, int>> drop;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            free_[b.dev].emplace(b.bytes, p);
+            cached_ += b.bytes;
+            while (cached_ > cap()) {  // over the cap: unmap the largest cached blocks
+                std::multimap<size_t, void*>* big = nullptr;
+                int bd = 0;
+                for (auto& kv : free_)
+                    if (!kv.second.empty() && (!big || std::prev(kv.second.end())->first > std::prev(big->end())->first)) {
+                        big = &kv.second;
+                        bd = kv.first;
+                    }
+                if (!big) break;
+                auto last = std::prev(big->end());
+                cached_ -= last->first;
+                blocks_.erase(last->second);
+                drop.emplace_back(last->second, bd);
+                big->erase(last);
+            }
+        }
+        for (auto& d : drop) unmap(d.first, d.second);
+        return e;
+    }
+    size_t trim() {
+        std::vector<std::pair<void*, int>> drop;
+        size_t n = 0;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (auto& kv : free_) {
+                for (auto& x : kv.second) {
+                    n += x.first;
+                    blocks_.erase(x.second);
+                    drop.emplace_back(x.second, kv.first);
+                }
+                kv.second.clear();
+            }
+            cached_ = 0;
+        }
+        for (auto& d : drop) unmap(d.first, d.second);
+        return n;
+    }
+    size_t cached() {
+        std::lock_guard<std::mutex> g(mu_);
+        return cached_;
+    }
+
+  private:
+    struct Blk {
+        size_t bytes = 0;
+        int dev = 0;
+    };
+    static size_t grain(size_t n) {
+        if (n == 0) n = 16;
+        const size_t g = n >= ((size_t)1 << 20) ? ((size_t)2 << 20) : 4096;
+        return (n + g - 1) / g * g;
+    }
+    static size_t cap() {
+        static const size_t c = [] {
+            const char* e = getenv("MESH_AMD_DEVICE_CACHE_MB");
+            const long long mb = e ? atoll(e) : 16384;
+            return mb > 0 ? (size_t)mb << 20 : (size_t)0;
+        }();
+        return c;
+    }
+    static void unmap(void* p, int dev) {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (cur != dev) (void)hipSetDevice(dev);
+        (void)hipFree(p);
+        if (cur != dev && cur >= 0) (void)hipSetDevice(cur);
+    }
+    void trim_device(int dev) {
+        std::vector<std::pair<void*, int>> drop;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (auto& x : free_[dev]) {
+                cached_ -= x.first;
+                blocks_.erase(x.second);
+                drop.emplace_back(x.second, dev);
+            }
+            free_[dev].clear();
+        }
+        for (auto& d : drop) unmap(d.first, d.second);
+    }
+    std::mutex mu_;
+    std::map<void*, Blk> blocks_;                     // every block this cache allocated (handed out or cached)
+    std::map<int, std::multimap<size_t, void*>> free_;  // cached blocks per device, by size
+    size_t cached_ = 0;
+};
+static DevCache& dev_cache() {
+    static DevCache* c = new DevCache;  // never destroyed: the runtime may be gone at static destruction
+    return *c;
+}
+hipError_t dmalloc_raw(void** p, size_t bytes) { return dev_cache().alloc(p, bytes); }
+hipError_t dfree(void* p) { return dev_cache().free(p); }
+size_t dcache_trim() { return dev_cache().trim(); }
+size_t dcache_bytes() { return dev_cache().cached(); }
+
 int DevBuf::reserve(size_t need) {
     if (need <= bytes && ptr) return MSH_OK;
     if (ptr) {
-        hipError_t e = hipFree(ptr);
+        hipError_t e = dfree(ptr);
         ptr = nullptr;
         bytes = 0;
         MSH_HIP(e);
     }
     if (need == 0) need = 16;
-    MSH_HIP(hipMalloc(&ptr, need));
+    MSH_HIP(dmalloc(&ptr, need));
     bytes = need;
     return MSH_OK;
 }
 
 void DevBuf::release() {
-    if (ptr) (void)hipFree(ptr);
+    if (ptr) (void)dfree(ptr);
     ptr = nullptr;
     bytes = 0;
 }
@@ -221,8 +373,36 @@ static int upload(DevBuf& buf, const T* host, size_t n, hipStream_t s) {
     return MSH_OK;
 }
 
+// End of an asynchronous batched build: wait for its last kernel, free its temporaries, read its GPU time.  A kernel
+// failure of the build surfaces here (MSH_EDEVICE), at the first call that needs the tree.
+static int finish_pending(msh_tree* t) {
+    if (!t->pending) return MSH_OK;
+    (void)hipSetDevice(t->device);
+    const hipError_t e = hipEventSynchronize(t->pend_done);
+    float ms = 0.f;
+    if (e == hipSuccess && hipEventElapsedTime(&ms, t->pend_e0, t->pend_done) == hipSuccess) t->build_ms += ms;
+    for (void* p : t->pend_free)
+        if (p) (void)dfree(p);
+    t->pend_free.clear();
+    t->pend_ws.release();
+    (void)hipEventDestroy(t->pend_e0);
+    (void)hipEventDestroy(t->pend_done);
+    t->pend_e0 = t->pend_done = nullptr;
+    t->pending = false;
+    if (e != hipSuccess) {
+        set_error("batched LBVH build failed: %s", hipGetErrorString(e));
+        return MSH_EDEVICE;
+    }
+    return MSH_OK;
+}
+
 static void free_tree(msh_tree* t) {
     if (!t) return;
+    if (t->pending) {
+        const std::string keep = g_err;
+        (void)finish_pending(t);
+        g_err = keep;
+    }
     for (msh_tree* r : t->replicas) free_tree(r);
     t->replicas.clear();
     (void)hipSetDevice(t->device);
@@ -231,18 +411,18 @@ static void free_tree(msh_tree* t) {
     // triangle trees (single, batched, normals metric) took one when they were built, if one was idle
     if (t->kind != kPoints) ws_pool().give(t->device, t->ws);
     t->ws.release();
-    if (t->d_v) (void)hipFree(t->d_v);
-    if (t->d_nodes) (void)hipFree(t->d_nodes);
-    if (t->d_orgs) (void)hipFree(t->d_orgs);
-    if (t->d_boxes) (void)hipFree(t->d_boxes);
-    if (t->d_leaves) (void)hipFree(t->d_leaves);
-    if (t->d_vorder) (void)hipFree(t->d_vorder);
-    if (t->d_vorder_shard) (void)hipFree(t->d_vorder_shard);
-    if (t->d_cut) (void)hipFree(t->d_cut);
-    if (t->d_cut_hint) (void)hipFree(t->d_cut_hint);
+    if (t->d_v) (void)dfree(t->d_v);
+    if (t->d_nodes) (void)dfree(t->d_nodes);
+    if (t->d_orgs) (void)dfree(t->d_orgs);
+    if (t->d_boxes) (void)dfree(t->d_boxes);
+    if (t->d_leaves) (void)dfree(t->d_leaves);
+    if (t->d_vorder) (void)dfree(t->d_vorder);
+    if (t->d_vorder_shard) (void)dfree(t->d_vorder_shard);
+    if (t->d_cut) (void)dfree(t->d_cut);
+    if (t->d_cut_hint) (void)dfree(t->d_cut_hint);
     for (int b = 0; b < 3; ++b) {
         if (b < 2 && t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
-        if (t->d_stage[b]) (void)hipFree(t->d_stage[b]);
+        if (t->d_stage[b]) (void)dfree(t->d_stage[b]);
         if (t->e_up[b]) (void)hipEventDestroy(t->e_up[b]);
         if (t->e_run[b]) (void)hipEventDestroy(t->e_run[b]);
         if (t->e_down[b]) (void)hipEventDestroy(t->e_down[b]);
@@ -309,8 +489,8 @@ static void free_entry_cut(msh_tree* t) {
     if (t->d_cut || t->d_cut_hint) {
         (void)hipSetDevice(t->device);
         if (t->ws_done) (void)hipEventSynchronize(t->ws_done);  // no launch may still read the cut
-        if (t->d_cut) (void)hipFree(t->d_cut);
-        if (t->d_cut_hint) (void)hipFree(t->d_cut_hint);
+        if (t->d_cut) (void)dfree(t->d_cut);
+        if (t->d_cut_hint) (void)dfree(t->d_cut_hint);
     }
     t->d_cut = nullptr;
     t->d_cut_hint = nullptr;
@@ -374,8 +554,8 @@ static int build_entry_cut(msh_tree* t) {
             // the centres' own walks start at the root (no cut is installed while it is built)
             if ((st = msh_tree_nearest_device(t, dq.as<double>(), n, df.as<uint32_t>(), nullptr, dp.as<double>(), s)) != MSH_OK)
                 break;
-            e = hipMalloc(&cut, n * kCutK * sizeof(uint2));
-            if (e == hipSuccess) e = hipMalloc(&hint, n * sizeof(int));
+            e = dmalloc(&cut, n * kCutK * sizeof(uint2));
+            if (e == hipSuccess) e = dmalloc(&hint, n * sizeof(int));
             if (e != hipSuccess) {
                 set_error("hipMalloc entry cut (%zu cells): %s", n, hipGetErrorString(e));
                 st = MSH_ENOMEM;
@@ -404,8 +584,8 @@ static int build_entry_cut(msh_tree* t) {
             t->cut_iw[k] = 1.0 / w[k];
         }
     } else {
-        if (cut) (void)hipFree(cut);
-        if (hint) (void)hipFree(hint);
+        if (cut) (void)dfree(cut);
+        if (hint) (void)dfree(hint);
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
@@ -443,7 +623,7 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
     hipEvent_t e0, e1;
     MSH_HIP(hipEventCreate(&e0));
     MSH_HIP(hipEventCreate(&e1));
-    MSH_HIP(hipMalloc(&t->d_v, std::max<size_t>(Pall, 1) * 3 * sizeof(double)));
+    MSH_HIP(dmalloc(&t->d_v, std::max<size_t>(Pall, 1) * 3 * sizeof(double)));
     MSH_HIP(hipMemcpyAsync(t->d_v, v, Pall * 3 * sizeof(double), hipMemcpyHostToDevice, s));
     DevBuf dF, dLo, dHi, dOrder;
     int st = MSH_OK;
@@ -453,10 +633,10 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
         if ((st = dHi.reserve(3 * T * sizeof(double))) != MSH_OK) break;
         if ((st = dOrder.reserve(T * sizeof(uint32_t))) != MSH_OK) break;
         if (T > 1) {
-            hipError_t e = hipMalloc(&t->d_nodes, (T - 1) * sizeof(BNode));
+            hipError_t e = dmalloc(&t->d_nodes, (T - 1) * sizeof(BNode));
             if (e != hipSuccess) { set_error("hipMalloc nodes: %s", hipGetErrorString(e)); st = MSH_ENOMEM; break; }
         }
-        hipError_t e = hipMalloc(&t->d_leaves, T * sizeof(TriRec));
+        hipError_t e = dmalloc(&t->d_leaves, T * sizeof(TriRec));
         if (e != hipSuccess) { set_error("hipMalloc leaves: %s", hipGetErrorString(e)); st = MSH_ENOMEM; break; }
         (void)hipEventRecord(e0, s);
         if ((st = tri_bounds(t->d_v, dF.as<uint32_t>(), T, dLo.as<double>(), dHi.as<double>(), s)) != MSH_OK) break;
@@ -684,7 +864,7 @@ struct HostArr {
 static void release_stage(msh_tree* t, bool host, bool dev) {
     for (int b = 0; b < 3; ++b) {
         if (host && b < 2 && t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
-        if (dev && t->d_stage[b]) (void)hipFree(t->d_stage[b]);
+        if (dev && t->d_stage[b]) (void)dfree(t->d_stage[b]);
         if (host && b < 2) t->h_stage[b] = nullptr;
         if (dev) t->d_stage[b] = nullptr;
     }
@@ -722,7 +902,7 @@ class StagePool {
         }
         for (int b = 0; b < 3; ++b) {  // an extra set (concurrent calls): freed
             if (b < 2 && s.h[b]) (void)hipHostFree(s.h[b]);
-            if (s.d[b]) (void)hipFree(s.d[b]);
+            if (s.d[b]) (void)dfree(s.d[b]);
         }
     }
 
@@ -739,7 +919,7 @@ class StagePool {
             for (const StageSet& s : kv.second)
                 for (int b = 0; b < 3; ++b) {
                     if (b < 2 && s.h[b]) (void)hipHostFree(s.h[b]);
-                    if (s.d[b]) (void)hipFree(s.d[b]);
+                    if (s.d[b]) (void)dfree(s.d[b]);
                 }
             kv.second.clear();
         }
@@ -798,7 +978,7 @@ static int stage_setup(msh_tree* t, size_t host_bytes, size_t dev_bytes) {
     }
     if (t->stage_bytes < dev_bytes) {
         release_stage(t, false, true);
-        for (int b = 0; b < 3; ++b) MSH_HIP(hipMalloc(&t->d_stage[b], dev_bytes));
+        for (int b = 0; b < 3; ++b) MSH_HIP(dmalloc(&t->d_stage[b], dev_bytes));
         t->stage_bytes = dev_bytes;
     }
     return MSH_OK;
@@ -1367,7 +1547,7 @@ int msh_points_build(const double* v, size_t P, msh_tree** out) {
     int st = MSH_OK;
     DevBuf dLo, dHi, dOrder;
     do {
-        hipError_t e = hipMalloc(&t->d_v, P * 3 * sizeof(double));
+        hipError_t e = dmalloc(&t->d_v, P * 3 * sizeof(double));
         if (e != hipSuccess) { set_error("hipMalloc: %s", hipGetErrorString(e)); st = MSH_ENOMEM; break; }
         e = hipMemcpyAsync(t->d_v, v, P * 3 * sizeof(double), hipMemcpyHostToDevice, s);
         if (e != hipSuccess) { set_error("H2D: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
@@ -1375,10 +1555,10 @@ int msh_points_build(const double* v, size_t P, msh_tree** out) {
         if ((st = dHi.reserve(3 * P * sizeof(double))) != MSH_OK) break;
         if ((st = dOrder.reserve(P * sizeof(uint32_t))) != MSH_OK) break;
         if (P > 1) {
-            e = hipMalloc(&t->d_nodes, (P - 1) * sizeof(BNode));
+            e = dmalloc(&t->d_nodes, (P - 1) * sizeof(BNode));
             if (e != hipSuccess) { set_error("hipMalloc nodes: %s", hipGetErrorString(e)); st = MSH_ENOMEM; break; }
         }
-        e = hipMalloc(&t->d_leaves, P * sizeof(PtRec));
+        e = dmalloc(&t->d_leaves, P * sizeof(PtRec));
         if (e != hipSuccess) { set_error("hipMalloc leaves: %s", hipGetErrorString(e)); st = MSH_ENOMEM; break; }
         if ((st = point_bounds(t->d_v, P, dLo.as<double>(), dHi.as<double>(), s)) != MSH_OK) break;
         if ((st = build_lbvh(t, dLo.as<double>(), dHi.as<double>(), P, dOrder.as<uint32_t>())) != MSH_OK) break;
@@ -1443,6 +1623,7 @@ int msh_tree_entry_cut_info(const msh_tree* t, int* state, int* G, uint64_t* byt
 
 int msh_tree_get_info(const msh_tree* t, msh_tree_info* info) {
     if (!t || !info) { set_error("null argument"); return MSH_EINVAL; }
+    MSH_TRY(finish_pending(const_cast<msh_tree*>(t)));  // an asynchronous batched build: its GPU time
     info->device = t->device;
     info->kind = t->kind;
     info->n_points = t->P;
@@ -2044,13 +2225,13 @@ int msh_tree_blob_unpack(const void* d_src, size_t bytes, int device, void* stre
     const size_t leaf = h.leaf_bytes;
     hipStream_t s = us ? us : t->stream;
     do {
-        hipError_t e = hipMalloc(&t->d_v, std::max<uint64_t>(h.v_rows, 1) * 3 * sizeof(double));
+        hipError_t e = dmalloc(&t->d_v, std::max<uint64_t>(h.v_rows, 1) * 3 * sizeof(double));
         if (e == hipSuccess && h.v_rows)
             e = hipMemcpyAsync(t->d_v, src + h.off_v, h.v_rows * 3 * sizeof(double), hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess && h.T > 1) e = hipMalloc(&t->d_nodes, (h.T - 1) * sizeof(BNode));
+        if (e == hipSuccess && h.T > 1) e = dmalloc(&t->d_nodes, (h.T - 1) * sizeof(BNode));
         if (e == hipSuccess && h.T > 1)
             e = hipMemcpyAsync(t->d_nodes, src + h.off_nodes, (h.T - 1) * sizeof(BNode), hipMemcpyDeviceToDevice, s);
-        if (e == hipSuccess) e = hipMalloc(&t->d_leaves, h.T * leaf);
+        if (e == hipSuccess) e = dmalloc(&t->d_leaves, h.T * leaf);
         if (e == hipSuccess) e = hipMemcpyAsync(t->d_leaves, src + h.off_leaves, h.T * leaf, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) {
@@ -2113,12 +2294,14 @@ size_t msh_host_pool_bytes(void) { return pinned_pool().bytes(); }
 int msh_device_pool_trim(void) {
     ws_pool().trim();
     stage_pool().trim();
+    dcache_trim();  // last: the workspaces and slabs above were returned to it
     return MSH_OK;
 }
 
-int msh_device_pool_bytes(uint64_t* workspace, uint64_t* staging) {
+int msh_device_pool_bytes(uint64_t* workspace, uint64_t* staging, uint64_t* cached) {
     if (workspace) *workspace = ws_pool().bytes();
     if (staging) *staging = stage_pool().device_bytes();
+    if (cached) *cached = dcache_bytes();
     return MSH_OK;
 }
 
@@ -2156,9 +2339,9 @@ int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size
     do {
         hipError_t e = hipEventCreate(&e0);
         if (e == hipSuccess) e = hipEventCreate(&e1);
-        if (e == hipSuccess) e = hipMalloc(&t->d_v, B * P * 3 * sizeof(double));
-        if (e == hipSuccess) e = hipMalloc(&t->d_nodes, B * (T - 1) * sizeof(BNode));
-        if (e == hipSuccess) e = hipMalloc(&t->d_leaves, B * T * sizeof(TriRec));
+        if (e == hipSuccess) e = dmalloc(&t->d_v, B * P * 3 * sizeof(double));
+        if (e == hipSuccess) e = dmalloc(&t->d_nodes, B * (T - 1) * sizeof(BNode));
+        if (e == hipSuccess) e = dmalloc(&t->d_leaves, B * T * sizeof(TriRec));
         if (e != hipSuccess) { set_error("msh_batch_build: %s", hipGetErrorString(e)); st = MSH_ENOMEM; break; }
         // the vertices (C4: 496 MB) through the pinned staging pipeline, a chunk of meshes at a time (one pageable
         // hipMemcpy of them ran well below the host link's rate)
@@ -2181,18 +2364,31 @@ int msh_batch_build(const double* v, size_t B, size_t P, const uint32_t* f, size
         if ((st = pack_tri_leaves_batch(t->d_v, P, dF.as<uint32_t>(), dOrder.as<uint32_t>(), B, T,
                                         static_cast<TriRec*>(t->d_leaves), s)) != MSH_OK)
             break;
-        if ((st = build_obb(t, true)) != MSH_OK) break;
+        if ((st = build_obb(t, true, true)) != MSH_OK) break;
         (void)hipEventRecord(e1, s);
-        e = hipStreamSynchronize(s);
-        if (e != hipSuccess) { set_error("batched LBVH build failed: %s", hipGetErrorString(e)); st = MSH_EDEVICE; break; }
-        float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, e0, e1);
-        t->build_ms = ms;
+        if (t->ws_done) (void)hipEventRecord(t->ws_done, s);  // *_device calls on other streams wait for the build
     } while (0);
-    (void)hipStreamSynchronize(s);
-    dF.release(); dLo.release(); dHi.release(); dOrder.release();
-    t->ws.release();
-    if (st == MSH_OK) ws_pool().take(t->device, t->ws);  // a freed tree's query workspace, if one is idle
+    if (st == MSH_OK) {
+        // The tail of the build (leaf packing, oriented boxes) is still running on the handle's stream: return now, so
+        // the caller's next call overlaps it (C4 through numpy: the queries' uploads run on the copy stream while the
+        // boxes are built; the query kernels follow the build on the handle's stream).  Its temporaries and workspace
+        // are freed by finish_pending once it has passed.
+        t->pending = true;
+        t->pend_e0 = e0;
+        t->pend_done = e1;
+        e0 = e1 = nullptr;
+        for (DevBuf* b : {&dF, &dLo, &dHi, &dOrder}) {
+            t->pend_free.push_back(b->ptr);
+            b->ptr = nullptr;
+            b->bytes = 0;
+        }
+        t->pend_ws = std::move(t->ws);
+        ws_pool().take(t->device, t->ws);  // a freed tree's query workspace, if one is idle
+    } else {
+        (void)hipStreamSynchronize(s);
+        dF.release(); dLo.release(); dHi.release(); dOrder.release();
+        t->ws.release();
+    }
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
     if (st != MSH_OK) {
@@ -2221,6 +2417,8 @@ static int batch_query(msh_tree* t, const double* d_q, size_t S, const SlotOut& 
     const size_t n = t->B * S;
     if (n == 0) return MSH_OK;
     MSH_TRY(check_count(n, fn));
+    // a build still running is waited for on the device (ws_done); its temporaries go once it has passed
+    if (t->pending && hipEventQuery(t->pend_done) == hipSuccess) MSH_TRY(finish_pending(t));
     return batch_query_range(t, d_q, S, 0, t->B, o, pick(t, stream));
 }
 
@@ -2258,11 +2456,14 @@ static int batch_host(msh_tree* t, const double* q, size_t S, uint32_t* face, ui
     if (w) arrs.push_back({nullptr, w, 24 * S});
     // chunks of ~2M then ~6M queries (whole meshes)
     const std::vector<size_t> plan = {std::max<size_t>(1, ((size_t)2 << 20) / S), std::max<size_t>(1, ((size_t)6 << 20) / S)};
-    return pipelined(t, t->B, arrs, [&](size_t m0, size_t nm, const std::vector<char*>& d) {
+    // the uploads of the first chunks overlap the tail of an asynchronous build; its kernels follow it on t->stream
+    const int st = pipelined(t, t->B, arrs, [&](size_t m0, size_t nm, const std::vector<char*>& d) {
         const SlotOut o{reinterpret_cast<uint32_t*>(d[1]), ipart >= 0 ? reinterpret_cast<uint32_t*>(d[ipart]) : nullptr,
                         reinterpret_cast<double*>(d[ipt]), nullptr, iw >= 0 ? reinterpret_cast<double*>(d[iw]) : nullptr};
         return batch_query_range(t, reinterpret_cast<const double*>(d[0]), S, m0, nm, o, t->stream);
     }, &plan);
+    const int sb = finish_pending(t);
+    return st != MSH_OK ? st : sb;
 }
 
 int msh_batch_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
@@ -2286,7 +2487,7 @@ static int replicate_tree(msh_tree* t) {
     MSH_TRY(msh_tree_blob_size(t, &bytes));
     MSH_TRY(use_device(t->device));
     void* blob = nullptr;
-    MSH_HIP(hipMalloc(&blob, bytes));
+    MSH_HIP(dmalloc(&blob, bytes));
     int st = msh_tree_blob_pack(t, blob, nullptr);
     const std::vector<int> devs = g_devices;
     for (size_t g = 1; g < devs.size() && st == MSH_OK; ++g) {
@@ -2295,12 +2496,12 @@ static int replicate_tree(msh_tree* t) {
         void* copy = nullptr;
         if (d != t->device) {
             (void)hipSetDevice(d);
-            hipError_t e = hipMalloc(&copy, bytes);
+            hipError_t e = dmalloc(&copy, bytes);
             if (e == hipSuccess) e = hipMemcpyPeer(copy, d, blob, t->device, bytes);
             if (e != hipSuccess) {
                 set_error("replicating the tree to device %d: %s", d, hipGetErrorString(e));
                 st = e == hipErrorOutOfMemory ? MSH_ENOMEM : MSH_EDEVICE;
-                if (copy) (void)hipFree(copy);
+                if (copy) (void)dfree(copy);
                 break;
             }
             src = copy;
@@ -2309,7 +2510,7 @@ static int replicate_tree(msh_tree* t) {
         st = msh_tree_blob_unpack(src, bytes, d, nullptr, &r);
         if (copy) {
             (void)hipSetDevice(d);
-            (void)hipFree(copy);
+            (void)dfree(copy);
         }
         if (st == MSH_OK) {
             r->cut_req = t->cut_req;
@@ -2318,6 +2519,6 @@ static int replicate_tree(msh_tree* t) {
         }
     }
     (void)use_device(t->device);
-    (void)hipFree(blob);
+    (void)dfree(blob);
     return st;
 }

@@ -683,10 +683,10 @@ static int build_obb_big(msh_tree* tree, bool triangles, const int4* ranges, int
     if (tree->T <= 4 * (size_t)kObbBig) return MSH_OK;
     struct Tmp {
         void* p = nullptr;
-        ~Tmp() { if (p) (void)hipFree(p); }
+        ~Tmp() { if (p) (void)dfree(p); }
     } t_list, t_lr, t_cnt, t_items, t_off, t_frames, t_ext;
     const unsigned nblk = (unsigned)(((size_t)nn + kBlock - 1) / kBlock);
-    MSH_HIP(hipMalloc(&t_cnt.p, sizeof(unsigned)));
+    MSH_HIP(dmalloc(&t_cnt.p, sizeof(unsigned)));
     MSH_HIP(hipMemsetAsync(t_cnt.p, 0, sizeof(unsigned), s));
     k_big_count<<<nblk, kBlock, 0, s>>>(ranges, nn, static_cast<unsigned*>(t_cnt.p));
     MSH_HIP(hipGetLastError());
@@ -694,8 +694,8 @@ static int build_obb_big(msh_tree* tree, bool triangles, const int4* ranges, int
     MSH_HIP(hipMemcpyAsync(&nbig, t_cnt.p, sizeof(unsigned), hipMemcpyDeviceToHost, s));
     MSH_HIP(hipStreamSynchronize(s));
     if (nbig == 0) return MSH_OK;
-    MSH_HIP(hipMalloc(&t_list.p, (size_t)nbig * sizeof(int)));
-    MSH_HIP(hipMalloc(&t_lr.p, (size_t)nbig * sizeof(int4)));
+    MSH_HIP(dmalloc(&t_list.p, (size_t)nbig * sizeof(int)));
+    MSH_HIP(dmalloc(&t_lr.p, (size_t)nbig * sizeof(int4)));
     MSH_HIP(hipMemsetAsync(t_cnt.p, 0, sizeof(unsigned), s));
     k_big_nodes<<<nblk, kBlock, 0, s>>>(ranges, nn, static_cast<int*>(t_list.p), static_cast<int4*>(t_lr.p),
                                         static_cast<unsigned*>(t_cnt.p));
@@ -723,10 +723,10 @@ static int build_obb_big(msh_tree* tree, bool triangles, const int4* ranges, int
     const size_t ni = items.size();
     // a degenerate (caterpillar-like) tree has O(T^2 / kObbChunk) items: leave its big nodes to k_obb_wave
     if (ni > ((size_t)1 << 22)) return MSH_OK;
-    MSH_HIP(hipMalloc(&t_items.p, ni * sizeof(int2)));
-    MSH_HIP(hipMalloc(&t_off.p, (nbig + 1) * sizeof(int)));
-    MSH_HIP(hipMalloc(&t_frames.p, nbig * sizeof(ObbFrame)));
-    MSH_HIP(hipMalloc(&t_ext.p, ni * 12 * sizeof(double)));
+    MSH_HIP(dmalloc(&t_items.p, ni * sizeof(int2)));
+    MSH_HIP(dmalloc(&t_off.p, (nbig + 1) * sizeof(int)));
+    MSH_HIP(dmalloc(&t_frames.p, nbig * sizeof(ObbFrame)));
+    MSH_HIP(dmalloc(&t_ext.p, ni * 12 * sizeof(double)));
     MSH_HIP(hipMemcpyAsync(t_list.p, slist.data(), nbig * sizeof(int), hipMemcpyHostToDevice, s));
     MSH_HIP(hipMemcpyAsync(t_lr.p, slr.data(), nbig * sizeof(int4), hipMemcpyHostToDevice, s));
     MSH_HIP(hipMemcpyAsync(t_items.p, items.data(), ni * sizeof(int2), hipMemcpyHostToDevice, s));
@@ -753,7 +753,7 @@ static int build_obb_big(msh_tree* tree, bool triangles, const int4* ranges, int
     return MSH_OK;
 }
 
-int build_obb(msh_tree* tree, bool triangles) {
+int build_obb(msh_tree* tree, bool triangles, bool defer) {
     if (tree->T < 2) return MSH_OK;
     const int nn = (int)(tree->B * (tree->T - 1));
     const int nl = (int)(tree->B * tree->T);
@@ -765,11 +765,11 @@ int build_obb(msh_tree* tree, bool triangles) {
     // area prefix sums over all leaves (batched trees: the meshes' leaf ranges are disjoint)
     struct Tmp {
         void* p = nullptr;
-        ~Tmp() { if (p) (void)hipFree(p); }
+        ~Tmp() { if (p) (void)dfree(p); }
     } t_P, t_tot;
     const int nsb = (nl + kScanBlock - 1) / kScanBlock;
-    MSH_HIP(hipMalloc(&t_P.p, ((size_t)nl + 1) * sizeof(double4)));
-    MSH_HIP(hipMalloc(&t_tot.p, (size_t)nsb * sizeof(double4)));
+    MSH_HIP(dmalloc(&t_P.p, ((size_t)nl + 1) * sizeof(double4)));
+    MSH_HIP(dmalloc(&t_tot.p, (size_t)nsb * sizeof(double4)));
     double4* P = static_cast<double4*>(t_P.p);
     double4* tot = static_cast<double4*>(t_tot.p);
     if (triangles) k_area_scan<true><<<(unsigned)nsb, kBlock, 0, s>>>(tree->d_leaves, nl, P, tot);
@@ -791,13 +791,19 @@ int build_obb(msh_tree* tree, bool triangles) {
         k_obb_wave<false><<<blocks, kBlock, 0, s>>>(tree->d_leaves, ranges, nn, npm, tree->d_nodes, tree->d_orgs, maxr, P);
     }
     MSH_HIP(hipGetLastError());
+    if (defer) {  // freed by finish_pending once the build's last kernel has passed
+        tree->pend_free.push_back(t_P.p);
+        tree->pend_free.push_back(t_tot.p);
+        t_P.p = t_tot.p = nullptr;
+        return MSH_OK;
+    }
     MSH_HIP(hipStreamSynchronize(s));  // P is freed on return
     return MSH_OK;
 }
 
 // device copy of the single-mesh origin (kernels read per-mesh origins from tree->d_orgs)
 int upload_origin(msh_tree* tree, hipStream_t s) {
-    if (!tree->d_orgs) MSH_HIP(hipMalloc(&tree->d_orgs, 3 * sizeof(double)));
+    if (!tree->d_orgs) MSH_HIP(dmalloc(&tree->d_orgs, 3 * sizeof(double)));
     MSH_HIP(hipMemcpyAsync(tree->d_orgs, tree->origin, 3 * sizeof(double), hipMemcpyHostToDevice, s));
     return MSH_OK;
 }
@@ -902,8 +908,8 @@ int build_lbvh_batch(msh_tree* tree, const double* d_lo, const double* d_hi, siz
         set_error("batched LBVH build: %zu primitives exceed the 31-bit node index range", n);
         return MSH_EINVAL;
     }
-    MSH_HIP(hipMalloc(&tree->d_boxes, 6 * B * sizeof(double)));
-    MSH_HIP(hipMalloc(&tree->d_orgs, 3 * B * sizeof(double)));
+    MSH_HIP(dmalloc(&tree->d_boxes, 6 * B * sizeof(double)));
+    MSH_HIP(dmalloc(&tree->d_orgs, 3 * B * sizeof(double)));
     k_mesh_boxes<<<(unsigned)B, kBlock, 0, s>>>(d_lo, d_hi, T, tree->d_boxes, tree->d_orgs);
     MSH_HIP(hipGetLastError());
     // Morton codes in each mesh's own box; sort by code, then (stable) by mesh: order = (mesh, code, id)

@@ -30,6 +30,20 @@ void set_error(const char* fmt, ...);
         if (_s != MSH_OK) return _s; \
     } while (0)
 
+// Device allocations through the library's cache (api.cpp DevCache): dfree keeps the block for the next request of a
+// similar size on its device (after waiting for the device, as hipFree does).
+hipError_t dmalloc_raw(void** p, size_t bytes);
+hipError_t dfree(void* p);
+template <class T>
+inline hipError_t dmalloc(T** p, size_t bytes) {
+    void* v = nullptr;
+    const hipError_t e = dmalloc_raw(&v, bytes);
+    *p = static_cast<T*>(v);
+    return e;
+}
+size_t dcache_trim();
+size_t dcache_bytes();
+
 // Grow-only device scratch buffer.  Owning and move-only: a scope's buffers are freed when it ends (hipFree
 // waits for the device, so a buffer still read by queued launches is not released under them).
 struct DevBuf {
@@ -152,6 +166,12 @@ struct msh_tree {
     // copies of this tree on the other devices of msh_set_devices / msh_set_device_list (owned; freed with it):
     // host-buffer calls split their rows over this handle and its replicas
     std::vector<msh_tree*> replicas;
+    // batched builds return before their last kernels finish (api.cpp msh_batch_build): the build's temporaries
+    // (device pointers and its workspace) are freed, and build_ms read, once pend_done has passed (finish_pending)
+    bool pending = false;
+    std::vector<void*> pend_free;
+    msh::Workspace pend_ws;
+    hipEvent_t pend_e0 = nullptr, pend_done = nullptr;
 };
 
 namespace msh {
@@ -188,8 +208,9 @@ int upload_origin(msh_tree* tree, hipStream_t s);
 // Top-down re-split of every LBVH subtree over at most 2^log2K leaves (refine.hip): the same node ids,
 // ranges and leaf-order conventions as build_lbvh, which it must follow (triangle trees; before leaf packing).
 int resplit_tree(msh_tree* tree, const double* d_v, const uint32_t* d_f, size_t T, uint32_t* d_order, int log2K);
-// Oriented-box pass over the packed leaves (needs the node ranges recorded by build_lbvh).
-int build_obb(msh_tree* tree, bool triangles);
+// Oriented-box pass over the packed leaves (needs the node ranges recorded by build_lbvh).  defer: leave its
+// temporaries to tree->pend_free instead of synchronising and freeing them (asynchronous batched builds).
+int build_obb(msh_tree* tree, bool triangles, bool defer = false);
 int tri_bounds(const double* d_v, const uint32_t* d_f, size_t T, double* d_lo, double* d_hi, hipStream_t s);
 int pack_tri_leaves(const double* d_v, const uint32_t* d_f, const uint32_t* d_order, size_t T, uint32_t face_base,
                     TriRec* d_out, hipStream_t s);
@@ -212,7 +233,10 @@ int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32
                       hipStream_t s);
 // Entry cut of a single triangle tree: the start entries of every grid cell from the exact closest points
 // of the cell centres (d_pts, G^3 rows, answered by the tree itself), written to tree->d_cut (kCutK per cell)
-constexpr int kCutK = 8;  // 4: 1773-1800 M q/s (49.5-51.2 visits), 16: 1285 (C3, profiles/r03_c3_entry_cut_ab.jsonl)
+#ifndef MSH_CUT_K
+#define MSH_CUT_K 8
+#endif
+constexpr int kCutK = MSH_CUT_K;  // 4: 1773-1800 M q/s (49.5-51.2 visits), 16: 1285 (C3, profiles/r03_c3_entry_cut_ab.jsonl)
 int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s);
 int cut_build(msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, uint2* d_cut, hipStream_t s);
 // d_hint[cell] = the leaf holding face d_face[cell] (d_inv: T scratch words)

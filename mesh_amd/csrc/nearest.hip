@@ -607,7 +607,10 @@ __device__ inline unsigned lanes_below(unsigned long long m) {
 // owners through LDS: an atomic min of the squared distance's bits per owner, then an atomic min of
 // (face << 32 | leaf) among the entries that reached it: the lexicographic (d2, face) rule.
 // kPend (C3, M q/s): 3: 1236, 4: 1346, 8: 1593, 16: 1677, 32: 1706, unbounded: 1689; per-lane queues 1541.
-constexpr int kPend = 32;
+#ifndef MSH_KPEND
+#define MSH_KPEND 32
+#endif
+constexpr int kPend = MSH_KPEND;
 
 constexpr unsigned kRing = 256;     // ring entries per wave: < 64 left after full rounds + <= 128 per step
 constexpr size_t kListMaxLeaves = (size_t)1 << 26;  // leaf index bits of a ring entry

@@ -438,7 +438,7 @@ static int vertex_order(msh_tree* t, size_t v0, size_t nv, const uint32_t** orde
     MSH_TRY(ws.keys_alt.reserve(nv * sizeof(uint32_t)));
     MSH_TRY(ws.vals_alt.reserve(nv * sizeof(uint32_t)));
     uint32_t* buf = nullptr;
-    MSH_HIP(hipMalloc(&buf, nv * sizeof(uint32_t)));
+    MSH_HIP(dmalloc(&buf, nv * sizeof(uint32_t)));
     k_vertex_morton<<<(unsigned)((nv + kBlock - 1) / kBlock), kBlock, 0, s>>>(
         t->d_v, v0, nv, t->scene_lo[0], t->scene_lo[1], t->scene_lo[2], t->scene_hi[0], t->scene_hi[1],
         t->scene_hi[2], ws.keys.as<uint32_t>(), buf);
@@ -449,7 +449,7 @@ static int vertex_order(msh_tree* t, size_t v0, size_t nv, const uint32_t** orde
     if (st != MSH_OK) {
         if (st == MSH_EDEVICE) set_error("vertex Morton order: kernel launch failed");
         (void)hipStreamSynchronize(s);  // the buffer may still be in use by enqueued work
-        (void)hipFree(buf);
+        (void)dfree(buf);
         return st;
     }
     if (whole) {
@@ -460,7 +460,7 @@ static int vertex_order(msh_tree* t, size_t v0, size_t nv, const uint32_t** orde
             // handle's last launch sequence (ws_done, recorded on whatever stream it ran) and for this stream
             if (t->ws_done) (void)hipEventSynchronize(t->ws_done);
             (void)hipStreamSynchronize(s);
-            (void)hipFree(t->d_vorder_shard);
+            (void)dfree(t->d_vorder_shard);
         }
         t->d_vorder_shard = buf;
         t->vshard_v0 = v0;

@@ -397,23 +397,23 @@ int resplit_tree(msh_tree* tree, const double* d_v, const uint32_t* d_f, size_t 
     const uint32_t K = log2K >= 31 ? 0x7FFFFFFFu : (1u << log2K);
     struct Tmp {
         void* p = nullptr;
-        ~Tmp() { if (p) (void)hipFree(p); }
+        ~Tmp() { if (p) (void)dfree(p); }
     } t_cen, t_area, t_P, t_btot, t_idx2, t_sb, t_sb2, t_flags, t_seg, t_tab, t_cnt, t_nodes, t_ranges;
     const int nsb = (int)((T + kRbTile - 1) / kRbTile);
     const size_t nn = T - 1;
-    MSH_HIP(hipMalloc(&t_cen.p, T * sizeof(float4)));
-    MSH_HIP(hipMalloc(&t_area.p, T * sizeof(double4)));
-    MSH_HIP(hipMalloc(&t_P.p, (T + 1) * sizeof(double4)));
-    MSH_HIP(hipMalloc(&t_btot.p, (size_t)nsb * sizeof(double4)));
-    MSH_HIP(hipMalloc(&t_idx2.p, T * sizeof(uint32_t)));
-    MSH_HIP(hipMalloc(&t_sb.p, T * sizeof(uint32_t)));
-    MSH_HIP(hipMalloc(&t_sb2.p, T * sizeof(uint32_t)));
-    MSH_HIP(hipMalloc(&t_flags.p, (T + 1) * sizeof(uint32_t)));
-    MSH_HIP(hipMalloc(&t_seg.p, T * sizeof(RbSeg)));
-    MSH_HIP(hipMalloc(&t_tab.p, 4 * T * sizeof(uint32_t)));
-    MSH_HIP(hipMalloc(&t_cnt.p, 64 * sizeof(unsigned)));
-    MSH_HIP(hipMalloc(&t_nodes.p, nn * sizeof(BNode)));
-    MSH_HIP(hipMalloc(&t_ranges.p, nn * sizeof(int4)));
+    MSH_HIP(dmalloc(&t_cen.p, T * sizeof(float4)));
+    MSH_HIP(dmalloc(&t_area.p, T * sizeof(double4)));
+    MSH_HIP(dmalloc(&t_P.p, (T + 1) * sizeof(double4)));
+    MSH_HIP(dmalloc(&t_btot.p, (size_t)nsb * sizeof(double4)));
+    MSH_HIP(dmalloc(&t_idx2.p, T * sizeof(uint32_t)));
+    MSH_HIP(dmalloc(&t_sb.p, T * sizeof(uint32_t)));
+    MSH_HIP(dmalloc(&t_sb2.p, T * sizeof(uint32_t)));
+    MSH_HIP(dmalloc(&t_flags.p, (T + 1) * sizeof(uint32_t)));
+    MSH_HIP(dmalloc(&t_seg.p, T * sizeof(RbSeg)));
+    MSH_HIP(dmalloc(&t_tab.p, 4 * T * sizeof(uint32_t)));
+    MSH_HIP(dmalloc(&t_cnt.p, 64 * sizeof(unsigned)));
+    MSH_HIP(dmalloc(&t_nodes.p, nn * sizeof(BNode)));
+    MSH_HIP(dmalloc(&t_ranges.p, nn * sizeof(int4)));
     float4* cen = static_cast<float4*>(t_cen.p);
     double4* area = static_cast<double4*>(t_area.p);
     double4* P = static_cast<double4*>(t_P.p);

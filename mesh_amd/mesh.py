@@ -157,12 +157,19 @@ class Mesh(object):
 
     def closest_faces_and_points(self, vertices):
         # a tree built for one query batch, as the reference does (mesh.py:454-455).  Its entry cut (each cell
-        # answered at build time) pays off only when the batch is large against it: with about 8 grid cells per face
-        # (at most 2^23) C2's 10M queries on 13,776 faces run 25 -> 21 ms with it, C3's 100M on 1M faces 149 -> 198 ms
-        # (profiles/r04_facade_cut_policy.json), so the one-shot tree takes that coarser grid (a kept tree's default
-        # is finer) and builds it only for >= 32 queries per cell
+        # answered at build time) pays off only when the batch is large against it.  Round 4, about 8 grid cells per
+        # face (at most 2^23): C2's 10M queries on 13,776 faces 25 -> 21 ms with it, C3's 100M on 1M faces 149 -> 198 ms
+        # (profiles/r04_facade_cut_policy.json).  Round 5: the default grid (64 cells per face, at most 2^26) takes C2
+        # to 18.7 ms (22.1 with the coarse one) and C3 to 235 ms (100 ms without a cut;
+        # profiles/r05_bench_configs_c4_facade.jsonl).  So: the default grid for >= 8 queries per cell of it, else the
+        # coarse grid for >= 32 queries per cell of that, else none
         tree = self.compute_aabb_tree()
         n_q = int(np.prod(np.shape(vertices)[:-1])) if np.ndim(vertices) > 1 else 0
-        cells = min(8 * len(self.f), 1 << 23)
-        tree.cpp_handle.set_entry_cut(max(16, int(round(cells ** (1.0 / 3.0)))) if n_q >= 32 * cells else 0)
+        fine, coarse = min(64 * len(self.f), 1 << 26), min(8 * len(self.f), 1 << 23)
+        if n_q >= 8 * fine:
+            tree.cpp_handle.set_entry_cut(-1)
+        elif n_q >= 32 * coarse:
+            tree.cpp_handle.set_entry_cut(max(16, int(round(coarse ** (1.0 / 3.0)))))
+        else:
+            tree.cpp_handle.set_entry_cut(0)
         return tree.nearest(vertices)
