@@ -994,3 +994,20 @@ def test_multi_device_replicas_equal_one_device():
             assert np.array_equal(np.asarray(x), np.asarray(y), equal_nan=np.asarray(x).dtype.kind == "f")
     t = spatialsearch.aabbtree_compute(v, f)
     assert N.tree_devices(t) == [0]
+
+
+def test_facade_entry_cut_policy():
+    # Mesh.closest_faces_and_points builds a tree per call and picks its entry cut from the batch size (mesh.py): the
+    # default grid for >= 8 queries per cell (C2 mesh, 7.5M queries), the coarse one for >= 32 per coarse cell, none
+    # below; the answers equal a tree's without any cut, bit for bit
+    from mesh_amd import spatialsearch
+    from mesh_amd.mesh import Mesh
+    v, f = W.c2_mesh()
+    m = Mesh(v=v, f=f)
+    t = spatialsearch.aabbtree_compute(v, f)
+    t.set_entry_cut(0)
+    for n in (7_500_000, 4_000_000, 200_000):
+        q, _ = W.surface_samples(v, f, n, seed=90 + n % 7, sigma=0.01)
+        face, pt = m.closest_faces_and_points(q)
+        rf, _, rpt = spatialsearch.aabbtree_nearest(t, q)
+        assert np.array_equal(face, rf) and np.array_equal(pt, rpt), n
