@@ -192,6 +192,22 @@ int exclusive_scan_u32(uint32_t* data, size_t n, Workspace& ws, hipStream_t s) {
     return scan_rec(data, n, ws.scan.as<uint32_t>(), s);
 }
 
+// The first level of exclusive_scan_u32 only, when the consumer finishes it (tile_offset): *nsums chunk totals in
+// ws.scan, or *nsums = 0 with data fully scanned.
+static int scan_chunks(uint32_t* data, size_t n, Workspace& ws, hipStream_t s, const uint32_t** sums, unsigned* nsums,
+                       unsigned max_sums) {
+    const size_t nc = (n + kSortTile - 1) / kSortTile;
+    *sums = nullptr;
+    *nsums = 0;
+    if (nc <= 1 || nc > max_sums) return exclusive_scan_u32(data, n, ws, s);
+    MSH_TRY(ws.scan.reserve(nc * sizeof(uint32_t)));
+    k_scan_block<<<(unsigned)nc, kBlock, 0, s>>>(data, n, ws.scan.as<uint32_t>());
+    MSH_HIP(hipGetLastError());
+    *sums = ws.scan.as<uint32_t>();
+    *nsums = (unsigned)nc;
+    return MSH_OK;
+}
+
 int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_t* vals_alt, size_t n, int bits,
                      Workspace& ws, hipStream_t s, int lo_bit, bool* in_alt) {
     if (n <= 1) return MSH_OK;
@@ -283,6 +299,51 @@ __device__ inline uint32_t hilbert24(uint32_t x, uint32_t y, uint32_t z) {
     return (spread(X[0]) << 2) | (spread(X[1]) << 1) | spread(X[2]);
 }
 constexpr int kQsItems = 16;
+// Most chunk sums a scatter block scans itself (scan_chunks; at most 2 per thread), else the recursive scan.  Each
+// block pays for loading and scanning them, so only small sorts fold: C3 12.5M rows (48 sums) 0.278 -> 0.267 ms per
+// sort, 100M rows (382 sums) 1.95 -> 2.00 ms (profiles/r05_ab_sort_scan_fold.jsonl); 128 sums = 33.5M rows.
+#ifndef MSH_QSORT_FOLD_MAX
+#define MSH_QSORT_FOLD_MAX 128
+#endif
+constexpr unsigned kQsMaxSums = MSH_QSORT_FOLD_MAX;
+static_assert(kQsMaxSums <= 2 * MSH_QSORT_NT, "tile_offset scans 2 sums per thread");
+
+// Global start of (digit tid, this tile) for the first 256 threads.  With nsums == 0 offs holds the full exclusive
+// scan; otherwise offs holds scans local to 4096-entry chunks and sums the chunk totals, whose exclusive prefix the
+// block forms in LDS (sp, free until the tile is staged) -- the scan's recursive launches folded into the consumer.
+// Ends with a barrier (the caller's LDS zeroing is complete after it).
+template <int NT>
+__device__ inline uint32_t tile_offset(const uint32_t* __restrict__ offs, unsigned nb, const uint32_t* __restrict__ sums,
+                                       unsigned nsums, uint32_t* sp) {
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t wsum[NW];
+    const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+    const size_t idx = (size_t)tid * nb + blockIdx.x;
+    uint32_t g = tid < 256 ? offs[idx] : 0u;
+    if (nsums == 0) {
+        __syncthreads();
+        return g;
+    }
+    const unsigned j = 2u * (unsigned)tid;
+    const uint32_t a = j < nsums ? sums[j] : 0u, b = j + 1 < nsums ? sums[j + 1] : 0u;
+    const uint32_t x = a + b;
+    uint32_t incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t ex = incl - x;
+    for (int k = 0; k < w; ++k) ex += wsum[k];
+    if (j < nsums) sp[j] = ex;
+    if (j + 1 < nsums) sp[j + 1] = ex + a;
+    __syncthreads();
+    if (tid < 256) g += sp[idx / (size_t)kSortTile];
+    __syncthreads();
+    return g;
+}
 constexpr int kQsTile = kQsNT * kQsItems;
 
 template <int NT, int ITEMS>
@@ -356,7 +417,8 @@ __global__ __launch_bounds__(NT) void k_qhist64(const unsigned long long* __rest
 // sorted order and written out linearly (each digit run of the tile contiguous).
 template <int NT, int ITEMS, bool IN64, bool OUT64>
 __global__ __launch_bounds__(NT) void k_qscatter(const void* __restrict__ in, void* __restrict__ out, size_t n, int shift,
-                                                 const uint32_t* __restrict__ offs, unsigned nb) {
+                                                 const uint32_t* __restrict__ offs, unsigned nb,
+                                                 const uint32_t* __restrict__ sums, unsigned nsums) {
     constexpr int NW = NT / 64, TILE = NT * ITEMS, WI = 64 * ITEMS;
     static_assert(NT >= 256, "one thread per digit");
     __shared__ uint32_t wcnt[NW][256];
@@ -365,8 +427,6 @@ __global__ __launch_bounds__(NT) void k_qscatter(const void* __restrict__ in, vo
     __shared__ unsigned long long stage[TILE];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     for (int i = tid; i < NW * 256; i += NT) (&wcnt[0][0])[i] = 0;
-    const uint32_t g_off = tid < 256 ? offs[(size_t)tid * nb + blockIdx.x] : 0u;
-    __syncthreads();
     const size_t tile0 = (size_t)blockIdx.x * TILE;
     const size_t base = tile0 + (size_t)w * WI;
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -379,6 +439,9 @@ __global__ __launch_bounds__(NT) void k_qscatter(const void* __restrict__ in, vo
         const size_t i = base + (size_t)it * 64 + lane;
         ee[it] = i < n ? (IN64 ? in64[i] : (((unsigned long long)in32[i] << 32) | (uint32_t)i)) : 0ull;
     }
+    // after the tile's loads are issued, so the offsets' loads and scan overlap them (its barriers also order
+    // the counters' zeroing before the ranking)
+    const uint32_t g_off = tile_offset<NT>(offs, nb, sums, nsums, reinterpret_cast<uint32_t*>(stage));
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
         const size_t i = base + (size_t)it * 64 + lane;
@@ -471,7 +534,8 @@ __global__ __launch_bounds__(NT) void k_qhist32(const uint32_t* __restrict__ key
 template <int NT, int ITEMS, bool ROWS_IN, bool KEYS_OUT>
 __global__ __launch_bounds__(NT) void k_qscatter2(const uint32_t* __restrict__ kin, const uint32_t* __restrict__ rin,
                                                   uint32_t* __restrict__ kout, uint32_t* __restrict__ rout, size_t n,
-                                                  int shift, const uint32_t* __restrict__ offs, unsigned nb) {
+                                                  int shift, const uint32_t* __restrict__ offs, unsigned nb,
+                                                  const uint32_t* __restrict__ sums, unsigned nsums) {
     constexpr int NW = NT / 64, TILE = NT * ITEMS, WI = 64 * ITEMS;
     static_assert(NT >= 256, "one thread per digit");
     __shared__ uint32_t wcnt[NW][256];
@@ -480,8 +544,6 @@ __global__ __launch_bounds__(NT) void k_qscatter2(const uint32_t* __restrict__ k
     __shared__ unsigned long long stage[TILE];
     const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
     for (int i = tid; i < NW * 256; i += NT) (&wcnt[0][0])[i] = 0;
-    const uint32_t g_off = tid < 256 ? offs[(size_t)tid * nb + blockIdx.x] : 0u;
-    __syncthreads();
     const size_t tile0 = (size_t)blockIdx.x * TILE;
     const size_t base = tile0 + (size_t)w * WI;
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
@@ -492,6 +554,9 @@ __global__ __launch_bounds__(NT) void k_qscatter2(const uint32_t* __restrict__ k
         const size_t i = base + (size_t)it * 64 + lane;
         ee[it] = i < n ? (((unsigned long long)kin[i] << 32) | (ROWS_IN ? rin[i] : (uint32_t)i)) : 0ull;
     }
+    // after the tile's loads are issued, so the offsets' loads and scan overlap them (its barriers also order
+    // the counters' zeroing before the ranking)
+    const uint32_t g_off = tile_offset<NT>(offs, nb, sums, nsums, reinterpret_cast<uint32_t*>(stage));
 #pragma unroll
     for (int it = 0; it < ITEMS; ++it) {
         const size_t i = base + (size_t)it * 64 + lane;
@@ -575,39 +640,41 @@ int query_sort(const float* lo, const float* hi, const double* d_q, size_t S, in
         MSH_HIP(hipGetLastError());
     }
     TimedLaunch tl("sort", s);
-    MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
+    const uint32_t* sums;
+    unsigned nsums;
+    MSH_TRY(scan_chunks(hist, (size_t)nb * 256, ws, s, &sums, &nsums, kQsMaxSums));
     if (MSH_QSORT_SPLIT) {
         uint32_t* k0 = ws.keys.as<uint32_t>();
         uint32_t* k1 = ws.keys_alt.as<uint32_t>();
         uint32_t* r1 = k1 + S;
         uint32_t* k2 = ws.vals_alt.as<uint32_t>();
         uint32_t* r2 = k2 + S;
-        k_qscatter2<kQsNT, kQsItems, false, true><<<nb, kQsNT, 0, s>>>(k0, nullptr, k1, r1, S, 0, hist, nb);
+        k_qscatter2<kQsNT, kQsItems, false, true><<<nb, kQsNT, 0, s>>>(k0, nullptr, k1, r1, S, 0, hist, nb, sums, nsums);
         MSH_HIP(hipGetLastError());
         k_qhist32<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(k1, S, 8, hist, nb);
         MSH_HIP(hipGetLastError());
-        MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
-        k_qscatter2<kQsNT, kQsItems, true, true><<<nb, kQsNT, 0, s>>>(k1, r1, k2, r2, S, 8, hist, nb);
+        MSH_TRY(scan_chunks(hist, (size_t)nb * 256, ws, s, &sums, &nsums, kQsMaxSums));
+        k_qscatter2<kQsNT, kQsItems, true, true><<<nb, kQsNT, 0, s>>>(k1, r1, k2, r2, S, 8, hist, nb, sums, nsums);
         MSH_HIP(hipGetLastError());
         k_qhist32<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(k2, S, 16, hist, nb);
         MSH_HIP(hipGetLastError());
-        MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
+        MSH_TRY(scan_chunks(hist, (size_t)nb * 256, ws, s, &sums, &nsums, kQsMaxSums));
         k_qscatter2<kQsNT, kQsItems, true, false><<<nb, kQsNT, 0, s>>>(k2, r2, nullptr, ws.vals.as<uint32_t>(), S, 16,
-                                                                        hist, nb);
+                                                                        hist, nb, sums, nsums);
         MSH_HIP(hipGetLastError());
         return MSH_OK;
     }
-    k_qscatter<kQsNT, kQsItems, false, true><<<nb, kQsNT, 0, s>>>(ws.keys.ptr, A, S, 0, hist, nb);
+    k_qscatter<kQsNT, kQsItems, false, true><<<nb, kQsNT, 0, s>>>(ws.keys.ptr, A, S, 0, hist, nb, sums, nsums);
     MSH_HIP(hipGetLastError());
     k_qhist64<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(A, S, 8, hist, nb);
     MSH_HIP(hipGetLastError());
-    MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
-    k_qscatter<kQsNT, kQsItems, true, true><<<nb, kQsNT, 0, s>>>(A, B, S, 8, hist, nb);
+    MSH_TRY(scan_chunks(hist, (size_t)nb * 256, ws, s, &sums, &nsums, kQsMaxSums));
+    k_qscatter<kQsNT, kQsItems, true, true><<<nb, kQsNT, 0, s>>>(A, B, S, 8, hist, nb, sums, nsums);
     MSH_HIP(hipGetLastError());
     k_qhist64<kQsNT, kQsItems><<<nb, kQsNT, 0, s>>>(B, S, 16, hist, nb);
     MSH_HIP(hipGetLastError());
-    MSH_TRY(exclusive_scan_u32(hist, (size_t)nb * 256, ws, s));
-    k_qscatter<kQsNT, kQsItems, true, false><<<nb, kQsNT, 0, s>>>(B, ws.vals.ptr, S, 16, hist, nb);
+    MSH_TRY(scan_chunks(hist, (size_t)nb * 256, ws, s, &sums, &nsums, kQsMaxSums));
+    k_qscatter<kQsNT, kQsItems, true, false><<<nb, kQsNT, 0, s>>>(B, ws.vals.ptr, S, 16, hist, nb, sums, nsums);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }
