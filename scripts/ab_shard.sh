@@ -7,9 +7,12 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 VS=${VARIANTS:-$(ls build/variants | sed 's/\.so$//')}
+RVS=$(echo $VS | tr ' ' '\n' | tac | tr '\n' ' ')
 for r in $(seq 1 ${ROUNDS:-2}); do
+  # odd rounds in the given order, even rounds reversed (ABBA: no variant always follows the same one)
+  ORDER=$VS; [ $((r % 2)) -eq 0 ] && ORDER=$RVS
   for qn in ${QS:-12500000 100000000}; do
-    for v in $VS; do
+    for v in $ORDER; do
       MESH_AMD_LIB=$PWD/build/variants/$v.so timeout -k 10 300 python bench.py --queries $qn --steps ${VSTEPS:-10} \
         --warmup 2 --no-cpu >> gpurun_out/abs_${v}_$qn.log 2>&1
       rc=$?
