@@ -248,11 +248,14 @@ int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_
 //                (key << 32 | row: one 8-B store per element, so a digit run of a tile is twice as long in
 //                bytes as two 4-B arrays);
 //   pass 2       packed in, packed out;   pass 3  packed in, rows only out (the keys are not needed after it).
-// Tiles of kQsNT x 16 elements: with 1024-thread blocks a tile's 256 digit runs average 64 elements (512 B
+// Tiles of kQsNT x 16 elements: with 512-thread blocks a tile's 256 digit runs average 32 elements (256 B
 // packed), so the scattered stores are mostly whole lines.  HBM bytes per element: 24 (rows) + 4 (keys) in
 // k_qkeys; 4 + 8 in pass 1; 8 (histogram) + 8 + 8 in pass 2; 8 + 8 + 4 in pass 3.
+// 512-thread blocks, 8192-key tiles: 73 KB of LDS, so two blocks per CU overlap each other's load, rank and write
+// phases (1024 threads and 16384-key tiles took 145 KB, one block per CU): C3 100M rows 1.94-1.98 -> 1.77 ms per sort,
+// 12.5M rows 0.267 -> 0.226 ms (profiles/r05_ab_sort_fold_nt.jsonl); a stable sort, so the same order either way
 #ifndef MSH_QSORT_NT
-#define MSH_QSORT_NT 1024
+#define MSH_QSORT_NT 512
 #endif
 // Query order along the Hilbert curve of the 256^3 cells instead of the Morton curve: C3 100M 1985-1990 ->
 // 2033-2058 M q/s, 12.5M rows 1390 -> 1401-1416 M q/s (profiles/r05_ab_leaders_sort_resume.jsonl)
@@ -261,42 +264,57 @@ int radix_sort_pairs(uint32_t* keys, uint32_t* vals, uint32_t* keys_alt, uint32_
 #endif
 constexpr int kQsNT = MSH_QSORT_NT;
 
-// 24-bit Hilbert index of a cell of the 256^3 grid (Skilling, "Programming the Hilbert curve", 2004: the axes to
-// the transposed form, then the transposed bits interleaved, axis 0 first at each level).  Consecutive indices are
-// face-adjacent cells, so a tile of consecutive queries never jumps across the box the way a Morton tile does at
-// the octree's block boundaries.
-__device__ inline uint32_t hilbert24(uint32_t x, uint32_t y, uint32_t z) {
-    uint32_t X[3] = {x, y, z};
-#pragma unroll
-    for (uint32_t Q = 128; Q > 1; Q >>= 1) {
-        const uint32_t P = Q - 1;
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            if (X[i] & Q) {
-                X[0] ^= P;
-            } else {
-                const uint32_t t = (X[0] ^ X[i]) & P;
-                X[0] ^= t;
-                X[i] ^= t;
-            }
-        }
+// 24-bit Hilbert index of a cell of the 256^3 grid: Skilling's transform ("Programming the Hilbert curve", 2004: the
+// axes to the transposed form, then the transposed bits interleaved, axis 0 first at each level; numpy copy in
+// scripts/sort_debug.py hilbert24) run as the state machine it amounts to.  Consecutive indices are face-adjacent
+// cells, so a tile of consecutive queries never jumps across the box the way a Morton tile does at the octree's
+// block boundaries.  kHilbertTable[state * 8 + octant] = index digit | next state << 3 over the Morton code's 3-bit
+// octants from the top; scripts/hilbert_table.py derives the 24 states from the transform and checks the table
+// against it on all 2^24 cells (tests/test_hilbert_table.py).  k_qkeys expands it to two octants per step in LDS
+// (hilbert_pairs): four dependent LDS reads per key instead of ~200 VALU operations of the transform (C3 100M rows:
+// 0.59 -> 0.56 ms per key launch, profiles/r05_ab_hilbert_lut.jsonl).
+__constant__ uint8_t kHilbertTable[192] = {8, 17, 27, 2, 39, 46, 52, 5,
+ 56, 71, 73, 86, 91, 20, 10, 13,
+ 48, 1, 103, 110, 115, 18, 12, 21,
+ 126, 129, 29, 26, 79, 80, 140, 3,
+ 148, 43, 37, 34, 127, 128, 78, 81,
+ 156, 45, 35, 42, 31, 6, 160, 105,
+ 72, 87, 139, 4, 57, 70, 50, 53,
+ 0, 171, 111, 76, 49, 58, 102, 61,
+ 180, 143, 83, 184, 69, 54, 66, 97,
+ 16, 123, 9, 74, 47, 60, 38, 77,
+ 132, 95, 85, 14, 67, 144, 82, 33,
+ 142, 55, 185, 96, 93, 116, 90, 11,
+ 188, 107, 175, 176, 101, 98, 62, 65,
+ 164, 109, 119, 22, 99, 106, 152, 41,
+ 174, 177, 63, 64, 117, 114, 92, 19,
+ 30, 125, 161, 122, 7, 172, 104, 75,
+ 130, 25, 133, 166, 179, 136, 84, 191,
+ 94, 15, 141, 28, 145, 32, 138, 51,
+ 146, 155, 149, 36, 137, 24, 190, 167,
+ 154, 157, 147, 44, 169, 182, 120, 135,
+ 162, 165, 121, 134, 187, 108, 168, 183,
+ 118, 173, 23, 124, 153, 170, 40, 59,
+ 178, 113, 131, 88, 181, 158, 68, 151,
+ 186, 163, 89, 112, 189, 100, 150, 159};
+constexpr int kHilbertPairs = 24 * 64;
+// pairs[state * 64 + two octants] = two index digits | next state << 6, built by the block from kHilbertTable
+__device__ inline void hilbert_pairs(uint16_t* pairs, int tid, int nt) {
+    for (int i = tid; i < kHilbertPairs; i += nt) {
+        const uint32_t e1 = kHilbertTable[(i >> 6) * 8 + ((i >> 3) & 7)];
+        const uint32_t e2 = kHilbertTable[(e1 >> 3) * 8 + (i & 7)];
+        pairs[i] = (uint16_t)(((e1 & 7u) << 3) | (e2 & 7u) | ((e2 >> 3) << 6));
     }
-    X[1] ^= X[0];
-    X[2] ^= X[1];
-    uint32_t t = 0;
+}
+__device__ inline uint32_t hilbert24(uint32_t m, const uint16_t* pairs) {
+    uint32_t st = 0, h = 0;
 #pragma unroll
-    for (uint32_t Q = 128; Q > 1; Q >>= 1)
-        if (X[2] & Q) t ^= Q - 1;
-    X[0] ^= t;
-    X[1] ^= t;
-    X[2] ^= t;
-    auto spread = [](uint32_t v) {  // bit k -> bit 3k (8 bits)
-        v = (v | (v << 8)) & 0x0000F00Fu;
-        v = (v | (v << 4)) & 0x000C30C3u;
-        v = (v | (v << 2)) & 0x00249249u;
-        return v;
-    };
-    return (spread(X[0]) << 2) | (spread(X[1]) << 1) | spread(X[2]);
+    for (int L = 3; L >= 0; --L) {
+        const uint32_t e = pairs[st * 64 + ((m >> (6 * L)) & 63u)];
+        h = (h << 6) | (e & 63u);
+        st = e >> 6;
+    }
+    return h;
 }
 constexpr int kQsItems = 16;
 // Most chunk sums a scatter block scans itself (scan_chunks; at most 2 per thread), else the recursive scan.  Each
@@ -352,8 +370,10 @@ __global__ __launch_bounds__(NT) void k_qkeys(const double* __restrict__ q, size
                                               uint32_t* __restrict__ hist, unsigned nb) {
     constexpr int NW = NT / 64;
     __shared__ uint32_t h[NW][256];
+    __shared__ uint16_t pairs[MSH_QORDER_HILBERT ? kHilbertPairs : 1];
     const int tid = threadIdx.x, w = tid >> 6;
     for (int i = tid; i < NW * 256; i += NT) (&h[0][0])[i] = 0;
+    if (MSH_QORDER_HILBERT) hilbert_pairs(pairs, tid, NT);
     __syncthreads();
     const size_t base = (size_t)blockIdx.x * (NT * ITEMS);
 #pragma unroll 4
@@ -361,16 +381,7 @@ __global__ __launch_bounds__(NT) void k_qkeys(const double* __restrict__ q, size
         const size_t i = base + (size_t)k * NT + tid;
         if (i < n) {
             uint32_t key = query_morton30(q[3 * i], q[3 * i + 1], q[3 * i + 2], lx, ly, lz, hx, hy, hz) >> lo_bit;
-            if (MSH_QORDER_HILBERT) {  // the same 256^3 cells (lo_bit == 6) in Hilbert order
-                auto axis = [](uint32_t m, int k) {  // every third bit of the 24-bit code, from bit k
-                    uint32_t v = (m >> k) & 0x00249249u;
-                    v = (v | (v >> 2)) & 0x000C30C3u;
-                    v = (v | (v >> 4)) & 0x0000F00Fu;
-                    v = (v | (v >> 8)) & 0x000000FFu;
-                    return v;
-                };
-                key = hilbert24(axis(key, 2), axis(key, 1), axis(key, 0));
-            }
+            if (MSH_QORDER_HILBERT) key = hilbert24(key, pairs);  // the same 256^3 cells (lo_bit == 6), Hilbert order
             keys[i] = key;
             atomicAdd(&h[w][key & 255u], 1u);
         }
@@ -501,7 +512,7 @@ __global__ __launch_bounds__(NT) void k_qscatter(const void* __restrict__ in, vo
 }
 
 // Split-array form of the middle passes (MSH_QSORT_SPLIT): keys and rows in two u32 arrays, so a histogram pass
-// reads 4 B per element instead of the packed 8 B (16384-key tiles keep a digit run at 256 B per array).
+// reads 4 B per element instead of the packed 8 B (a digit run of an 8192-key tile averages 128 B per array).
 template <int NT, int ITEMS>
 __global__ __launch_bounds__(NT) void k_qhist32(const uint32_t* __restrict__ keys, size_t n, int shift,
                                                 uint32_t* __restrict__ hist, unsigned nb) {
