@@ -319,7 +319,8 @@ __device__ inline uint32_t hilbert24(uint32_t m, const uint16_t* pairs) {
 constexpr int kQsItems = 16;
 // Most chunk sums a scatter block scans itself (scan_chunks; at most 2 per thread), else the recursive scan.  Each
 // block pays for loading and scanning them, so only small sorts fold: C3 12.5M rows (48 sums) 0.278 -> 0.267 ms per
-// sort, 100M rows (382 sums) 1.95 -> 2.00 ms (profiles/r05_ab_sort_scan_fold.jsonl); 128 sums = 33.5M rows.
+// sort, 100M rows (382 sums) 1.95 -> 2.00 ms (profiles/r05_ab_sort_scan_fold.jsonl; 16384-key tiles then); with
+// 8192-key tiles 128 sums = 16.8M rows.
 #ifndef MSH_QSORT_FOLD_MAX
 #define MSH_QSORT_FOLD_MAX 128
 #endif
