@@ -336,7 +336,9 @@ def test_c3_replication_roundtrip():
 def test_query_order_equals_stable_argsort():
     # the closest-point path's query order (msh_tree_query_order: Hilbert indices of the 24-bit Morton cells + the
     # 3-pass LDS radix sort) equals numpy's stable argsort of the same keys (scripts/sort_debug.order_keys, the kernel's
-    # fp32 arithmetic): on the C3 stream (100M rows), a ragged size, a size below one tile and rows with NaN / inf
+    # fp32 arithmetic): on the C3 stream (100M rows), a ragged size, a size below one tile, rows with NaN / inf, and the
+    # sizes around the scan forms (8192-key tiles: 131,073 rows = 2 chunk sums and 16,777,216 = 128, both scanned in
+    # the scatter blocks; 16,777,217 = 129, the recursive scan)
     import torch
     from mesh_amd import _native, spatialsearch
     from scripts.sort_debug import order_keys, sort_box
@@ -347,7 +349,7 @@ def test_query_order_equals_stable_argsort():
     bad = W.c3_stream(50_000, "cuda:0", seed=7)
     bad[::7, 0] = float("nan")
     bad[3::11, 2] = float("inf")
-    for x in (q, q[:12_345_677], q[:1000], bad):
+    for x in (q, q[:12_345_677], q[:1000], bad, q[:131_073], q[:16_777_216], q[:16_777_217]):
         p = torch.empty(x.shape[0], dtype=torch.int32, device="cuda:0")
         # on torch's stream: the rows come from torch's generator, whose kernels the tree's own (non-blocking)
         # stream would not wait for
