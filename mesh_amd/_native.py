@@ -236,8 +236,9 @@ class Handle(object):
         return inf
 
     def set_entry_cut(self, G=-1):
-        """msh_tree_set_entry_cut: G < 0 automatic grid (default), 0 none, > 0 G^3 cells; built lazily by the
-        next closest-point query."""
+        """msh_tree_set_entry_cut: G < 0 automatic grid (default), 0 none, > 0 G^3 cells; built by the next
+        closest-point query whatever its size (without this call, the automatic grid waits until the handle's
+        queries number at least 1/16 of its cells)."""
         check(lib().msh_tree_set_entry_cut(self.ptr, int(G)))
 
     CUT_STATES = {0: "pending", 1: "built", 2: "off", 3: "failed"}

@@ -475,9 +475,10 @@ struct WsOrder {
 // shape), MSH_CUT_PER_LEAF cells per leaf up to 2^MSH_CUT_MAX_LOG2 cells (below; round 3 with leader phases:
 // G = 64 / 126 / 160: 1718 / 1742-1765 / 1782 M q/s against 1789-1800 at G = 200); the cell centres are answered
 // by the tree itself, then every cell's start entries are cut from the root.  Trees under kCutMinLeaves
-// leaves start at the root (their top levels are few).  Built lazily by the first closest-point query
-// (ensure_entry_cut), so ray-only, visibility and normals-metric trees never pay its memory or build time;
-// msh_tree_set_entry_cut chooses the grid or turns it off.
+// leaves start at the root (their top levels are few).  Built lazily (ensure_entry_cut): the automatic grid once the
+// handle's closest-point calls have brought kCutAutoRows rows per cell... in all, so ray-only, visibility and
+// normals-metric trees and a few small calls never pay its memory or build time; msh_tree_set_entry_cut chooses the
+// grid (built by the next closest-point call) or turns it off.
 constexpr size_t kCutMinLeaves = 4096;
 enum { kCutPending = 0, kCutBuilt = 1, kCutOff = 2, kCutFailed = 3 };
 
@@ -509,8 +510,11 @@ static void free_entry_cut(msh_tree* t) {
 #ifndef MSH_CUT_MAX_LOG2
 #define MSH_CUT_MAX_LOG2 26
 #endif
+static size_t auto_cut_cells(const msh_tree* t) {
+    return std::min<size_t>((size_t)MSH_CUT_PER_LEAF * t->T, (size_t)1 << MSH_CUT_MAX_LOG2);
+}
 static int build_entry_cut(msh_tree* t) {
-    const size_t cells = std::min<size_t>((size_t)MSH_CUT_PER_LEAF * t->T, (size_t)1 << MSH_CUT_MAX_LOG2);
+    const size_t cells = auto_cut_cells(t);
     const int G = t->cut_req > 0 ? t->cut_req : std::max(16, (int)std::lround(std::cbrt((double)cells)));
     double half[3], H = 0.0, lo[3], w[3];
     for (int k = 0; k < 3; ++k) {
@@ -592,14 +596,22 @@ static int build_entry_cut(msh_tree* t) {
     return st;
 }
 
-// First closest-point query of a handle: build its entry cut.  The cut is an optimisation, so a failure (device
-// memory, most likely: 4.4 GB plus ~3.4 GB of temporaries on C3) is not the query's: the partial buffers are
-// freed, the error is cleared, the handle remembers the failure and its queries start at the root.
-static void ensure_entry_cut(msh_tree* t) {
+// Closest-point call of S rows on a handle whose cut is pending: build it -- the automatic grid only once the handle
+// has answered at least one row per kCutAutoCellsPerRow cells (C3: 4.2M rows for G = 400's 64M cells; C2 55k), so a
+// few small calls on a large mesh walk from the root instead of paying ~64 ms and 4.4 GB (+3.4 GB of temporaries)
+// on their first call; after msh_tree_set_entry_cut, at the next call.  The cut is an optimisation, so a failure
+// (device memory, most likely) is not the query's: the partial buffers are freed, the error is cleared, the handle
+// remembers the failure and its queries start at the root.
+constexpr size_t kCutAutoCellsPerRow = 16;
+static void ensure_entry_cut(msh_tree* t, size_t S) {
     if (t->cut_state != kCutPending) return;
     if (!cut_applies(t)) {
         t->cut_state = kCutOff;
         return;
+    }
+    if (!t->cut_force && t->cut_req < 0) {
+        t->cut_rows += S;
+        if (t->cut_rows * kCutAutoCellsPerRow < auto_cut_cells(t)) return;
     }
     t->cut_state = kCutOff;  // while it is built: the cell-centre queries start at the root
     const std::string keep = g_err;
@@ -1604,10 +1616,14 @@ int msh_tree_set_entry_cut(msh_tree* t, int G) {
     if (G > 4096) { set_error("msh_tree_set_entry_cut: G = %d cells per axis (at most 4096)", G); return MSH_EINVAL; }
     const int want = G < 0 ? -1 : G;
     for (msh_tree* r : t->replicas) MSH_TRY(msh_tree_set_entry_cut(r, G));
-    if (want == t->cut_req && t->cut_state != kCutFailed) return MSH_OK;
+    if (want == t->cut_req && t->cut_state != kCutFailed) {
+        t->cut_force = true;  // a pending grid is built by the next call whatever its size
+        return MSH_OK;
+    }
     free_entry_cut(t);
     t->cut_req = want;
     t->cut_state = kCutPending;
+    t->cut_force = true;
     return MSH_OK;
 }
 
@@ -1646,18 +1662,22 @@ int msh_tree_get_info(const msh_tree* t, msh_tree_info* info) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// one sorted closest-point launch over d_q (validated; the entry cut already settled by the caller)
+static int nearest_run(msh_tree* t, const double* d_q, size_t S, const SlotOut& o, hipStream_t s) {
+    WsOrder order(t, s);
+    QueryOrder ord;
+    MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord, true));
+    return launch_nearest(t, ord, S, o, s);
+}
+
 int msh_tree_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part, double* d_pt,
                             void* stream) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_device"));
     MSH_TRY(check_count(S, "msh_tree_nearest_device"));
     if (S == 0) return MSH_OK;
     if (!d_q || !d_face || !d_pt) { set_error("msh_tree_nearest_device: null argument"); return MSH_EINVAL; }
-    ensure_entry_cut(t);
-    hipStream_t s = pick(t, stream);
-    WsOrder order(t, s);
-    QueryOrder ord;
-    MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord, true));
-    return launch_nearest(t, ord, S, SlotOut{d_face, d_part, d_pt, nullptr, nullptr}, s);
+    ensure_entry_cut(t, S);
+    return nearest_run(t, d_q, S, SlotOut{d_face, d_part, d_pt, nullptr, nullptr}, pick(t, stream));
 }
 
 int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, double* d_pt, double* d_w,
@@ -1665,24 +1685,22 @@ int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint3
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_bary_device"));
     MSH_TRY(check_count(S, "msh_tree_nearest_bary_device"));
     if (S == 0) return MSH_OK;
-    if (!d_w) { set_error("msh_tree_nearest_bary_device: null weights"); return MSH_EINVAL; }
-    ensure_entry_cut(t);
-    hipStream_t s = pick(t, stream);
-    WsOrder order(t, s);
-    QueryOrder ord;
-    MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord, true));
-    return launch_nearest(t, ord, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_w}, s);
+    if (!d_q || !d_face || !d_pt || !d_w) { set_error("msh_tree_nearest_bary_device: null argument"); return MSH_EINVAL; }
+    ensure_entry_cut(t, S);
+    return nearest_run(t, d_q, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_w}, pick(t, stream));
 }
 
+// the whole call's rows settle the entry cut once, before its chunks run
 static int nearest_host(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
     MSH_TRY(use_device(t->device));
-    ensure_entry_cut(t);
+    ensure_entry_cut(t, S);
     // rows: q (24 B in) | face (4 B out) | part (4 B out) | point (24 B out)
     const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, part, 4}, {nullptr, pt, 24}};
     return pipelined(t, S, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
-        return msh_tree_nearest_device(t, reinterpret_cast<const double*>(d[0]), n, reinterpret_cast<uint32_t*>(d[1]),
-                                       part ? reinterpret_cast<uint32_t*>(d[2]) : nullptr,
-                                       reinterpret_cast<double*>(d[3]), t->stream);
+        return nearest_run(t, reinterpret_cast<const double*>(d[0]), n,
+                           SlotOut{reinterpret_cast<uint32_t*>(d[1]), part ? reinterpret_cast<uint32_t*>(d[2]) : nullptr,
+                                   reinterpret_cast<double*>(d[3]), nullptr, nullptr},
+                           t->stream);
     });
 }
 
@@ -1703,13 +1721,14 @@ int msh_tree_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face
     if (!q || !face || !pt || !w) { set_error("msh_tree_nearest_bary: null argument"); return MSH_EINVAL; }
     return fan_out(t, S, 76, [&](msh_tree* h, size_t r0, size_t S_h) {
         MSH_TRY(use_device(h->device));
-        ensure_entry_cut(h);
+        ensure_entry_cut(h, S_h);
         const std::vector<HostArr> arrs = {{q + 3 * r0, nullptr, 24}, {nullptr, face + r0, 4}, {nullptr, pt + 3 * r0, 24},
                                            {nullptr, w + 3 * r0, 24}};
         return pipelined(h, S_h, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
-            return msh_tree_nearest_bary_device(h, reinterpret_cast<const double*>(d[0]), n,
-                                                reinterpret_cast<uint32_t*>(d[1]), reinterpret_cast<double*>(d[2]),
-                                                reinterpret_cast<double*>(d[3]), h->stream);
+            return nearest_run(h, reinterpret_cast<const double*>(d[0]), n,
+                               SlotOut{reinterpret_cast<uint32_t*>(d[1]), nullptr, reinterpret_cast<double*>(d[2]),
+                                       nullptr, reinterpret_cast<double*>(d[3])},
+                               h->stream);
         });
     });
 }
@@ -1720,7 +1739,7 @@ int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* n
     *nodes = 0;
     *leaves = 0;
     if (S == 0) return MSH_OK;
-    ensure_entry_cut(t);
+    ensure_entry_cut(t, S);
     hipStream_t s = t->stream;
     unsigned long long h[48] = {0};
     {
@@ -2514,6 +2533,7 @@ static int replicate_tree(msh_tree* t) {
         }
         if (st == MSH_OK) {
             r->cut_req = t->cut_req;
+            r->cut_force = t->cut_force;
             r->build_ms = t->build_ms;
             t->replicas.push_back(r);
         }

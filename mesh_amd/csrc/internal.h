@@ -160,6 +160,8 @@ struct msh_tree {
     // 0 off), state (0 pending, 1 built, 2 off / not applicable, 3 failed), GPU build time
     int cut_req = -1;
     int cut_state = 0;
+    bool cut_force = false;   // msh_tree_set_entry_cut was called: build at the next query, whatever its size
+    uint64_t cut_rows = 0;    // closest-point rows answered while the automatic cut waits (ensure_entry_cut)
     double cut_ms = 0.0;
     double cut_lo[3] = {0, 0, 0}, cut_iw[3] = {0, 0, 0};
     msh::Workspace ws;

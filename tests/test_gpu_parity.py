@@ -234,20 +234,25 @@ def test_entry_cut_bit_exact(oracle):
 
 
 def test_entry_cut_lazy_and_failure_fallback(oracle):
-    # The cut is built by the first closest-point query, never by the build, by rays or by the normals metric;
-    # a cut that cannot be built (here 4096^3 cells: more than one query call holds) is not an error: the handle
-    # records the failure and its queries start at the root with the same answers.
+    # The automatic cut is built by closest-point calls once they have brought one row per 16 of its cells (C2: 881,664
+    # cells, 55,104 rows), never by the build, by rays or by the normals metric, and a call after set_entry_cut builds
+    # it whatever its size; a cut that cannot be built (here 4096^3 cells: more than one query call holds) is not an
+    # error: the handle records the failure and its queries start at the root with the same answers.
     from mesh_amd import aabb_normals, spatialsearch
     v, f = W.c2_mesh()  # 13,776 faces: above the 4096-face floor
-    q, _ = W.surface_samples(v, f, 20000, seed=51, sigma=0.02)
+    q, _ = W.surface_samples(v, f, 40000, seed=51, sigma=0.02)
     t = spatialsearch.aabbtree_compute(v, f)
     assert t.entry_cut_info()["state"] == "pending"
     nrm = np.tile([[0.0, 0.0, 1.0]], (q.shape[0], 1))
     spatialsearch.aabbtree_nearest_alongnormal(t, q, nrm)
     assert t.entry_cut_info()["state"] == "pending" and t.entry_cut_info()["bytes"] == 0
-    ref = _nearest_tree(t, q)
+    ref = _nearest_tree(t, q)  # 40,000 rows: below the volume, walks from the root
+    assert t.entry_cut_info()["state"] == "pending" and t.entry_cut_info()["bytes"] == 0
+    again = _nearest_tree(t, q)  # 80,000 rows in all: the cut is built by this call
     info = t.entry_cut_info()
     assert info["state"] == "built" and info["bytes"] == info["G"] ** 3 * 68 and info["build_ms"] > 0
+    for a, b in zip(ref, again):
+        assert np.array_equal(a, b)
     t.set_entry_cut(4096)
     got = _nearest_tree(t, q)
     info = t.entry_cut_info()
@@ -256,11 +261,12 @@ def test_entry_cut_lazy_and_failure_fallback(oracle):
         assert np.array_equal(a, b)
     bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[:2000])
     assert np.array_equal(got[0][:2000], bf) and np.array_equal(got[1][:2000], bp) and np.array_equal(got[2][:2000], bpt)
-    # back to the automatic grid: rebuilt by the next query
+    # back to the automatic grid: rebuilt by the next query (an explicit request: whatever its size)
     t.set_entry_cut(-1)
     assert t.entry_cut_info()["state"] == "pending"
-    again = _nearest_tree(t, q)
+    again = _nearest_tree(t, q[:1000])
     assert t.entry_cut_info()["state"] == "built"
+    again = _nearest_tree(t, q)
     for a, b in zip(ref, again):
         assert np.array_equal(a, b)
     h = aabb_normals.aabbtree_n_compute(v, f, 0.1)
@@ -303,7 +309,8 @@ def test_entry_cut_rebuild_memory_flat():
 def test_c3_replication_roundtrip():
     # north_star's replication path on one GPU: the C3 tree packed into one device blob (what rank 0
     # broadcasts), unpacked on the same device (what every other rank does), answers the C3 stream bit for
-    # bit like the source handle; the receiver builds its own entry cut on its first query
+    # bit like the source handle; the receiver builds its own entry cut on its first query (5M rows: above the
+    # automatic cut's volume, 1 row per 16 of its 64M cells)
     import torch
     from mesh_amd import _native, spatialsearch
     from mesh_amd.distributed import nearest_device
@@ -318,7 +325,7 @@ def test_c3_replication_roundtrip():
     a, b = src.info(), dst.info()
     for k in ("n_points", "n_faces", "n_nodes", "bytes", "max_depth", "node_bytes", "leaf_bytes"):
         assert getattr(a, k) == getattr(b, k), k
-    q = W.c3_stream(4_000_000, "cuda:0")
+    q = W.c3_stream(5_000_000, "cuda:0")
     outs = []
     for t in (src, dst):
         o = (torch.empty(q.shape[0], dtype=torch.int32, device="cuda:0"),
