@@ -33,8 +33,9 @@ def main():
     for name, v in c.items():
         for pre, (rd, wr) in KNOWN.items():
             if name.startswith(pre):
-                out[name] = {"fetch_raw_over_read": v["FETCH_SIZE"] * 1024 / (rd * a.rows),
-                             "write_over_written": v["WRITE_SIZE"] * 1024 / (wr * a.rows)}
+                n = v.get("_dispatches", 1)  # the record holds totals over the run's dispatches
+                out[name] = {"dispatches": n, "fetch_raw_over_read": v["FETCH_SIZE"] / n * 1024 / (rd * a.rows),
+                             "write_over_written": v["WRITE_SIZE"] / n * 1024 / (wr * a.rows)}
     print(json.dumps(out, indent=1))
 
 
