@@ -39,6 +39,24 @@ sys.path.insert(0, ROOT)
 
 METRIC = "closest-point queries/sec vs 1M-face mesh at 1/2/4/8 MI355X + HBM GB/s"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate over the 8 XCDs
+
+
+def waves_per_simd(isa):
+    """Resident waves per SIMD of a 256-thread-block kernel with `vgpr` VGPRs and `lds` bytes of LDS per block
+    (gfx950: 512 VGPRs per SIMD lane, 160 KB of LDS per CU, 4 SIMDs per CU; at most 8 waves per SIMD)."""
+    vg, lds = int(isa.get("vgpr") or 0), int(isa.get("lds") or 0)
+    by_vgpr = 512 // vg if vg else 8
+    by_lds = (163840 // lds) * 4 // 4 if lds else 8  # blocks per CU x 4 waves per block / 4 SIMDs
+    return min(8, by_vgpr, by_lds)
+
+
+def issue_frac(tr):
+    """VALU-busy fraction of the traversal kernel's SIMDs from the PMC record: each resident wave issues VALU in
+    wave_cycles_valu_frac of its cycles, and waves_per_simd waves share a SIMD's VALU."""
+    if not tr or tr.get("wave_cycles_valu_frac") is None or "vgpr" not in (tr.get("isa") or {}):
+        return None
+    return min(1.0, tr["wave_cycles_valu_frac"] * waves_per_simd(tr["isa"]))
 
 
 def parse():
@@ -54,9 +72,23 @@ def parse():
                     help="CPU baseline: fixed sample of queries per host thread (1 thread: ~12 s)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--secondary", choices=("auto", "on", "off"), default="auto",
-                    help="C5 visibility and C4 batch lines beside value (auto: when N > 1, the configs north_star "
-                         "shards across GPUs)")
+                    help="C5 visibility and C4 batch lines beside value (auto: when the collective path runs, the "
+                         "configs north_star shards across GPUs)")
+    ap.add_argument("--dist", action="store_true",
+                    help="the collective path at any N, N = 1 included: the nccl (RCCL) process group, the tree's "
+                         "RCCL broadcast unpacked on every rank (the source too), the ResultRing all-gathers, the "
+                         "no-allgather / weak lines and the sharded C4 / C5 secondaries.  Launch under "
+                         "torch.distributed.run (a plain launch gets a one-rank rendezvous on 127.0.0.1)")
     return ap.parse_args()
+
+
+def free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
 
 def host_threads():
@@ -113,7 +145,7 @@ def cpu_baseline(v, f, per_thread, stream_rows):
             obj("all", "OpenMP over queries on %d host threads" % out["all"][2]))
 
 
-def secondary(timed, world, rank, dev, steps):
+def secondary(timed, world, rank, dev, steps, coll):
     """BASELINE configs[4] and [3] through their multi-GPU splits (north_star: C5 rays sharded across the GPUs,
     C4 meshes split by range), reported beside `value`, never as it.  Each is timed like the headline (barrier +
     sync around K steps, max over ranks), after one untimed step:
@@ -133,8 +165,11 @@ def secondary(timed, world, rank, dev, steps):
     out = {}
     v5, f5 = W.c5_mesh()
     t5 = spatialsearch.aabbtree_compute(v5, f5) if rank == 0 else None
-    if world > 1:
-        t5 = replicate_tree(t5, src=0)
+    if coll:
+        r5 = replicate_tree(t5, src=0, unpack_on_src=world == 1)
+        if r5 is not t5 and t5 is not None:
+            t5.free()
+        t5 = r5
     vn = torch.from_numpy(Mesh(v=v5, f=f5).estimate_vertex_normals()).to(dev)
     cams = torch.from_numpy(W.fibonacci_cameras(64, 3.0)).to(dev)
     P, C = v5.shape[0], 64
@@ -201,9 +236,14 @@ def main():
     if world != args.gpus:
         sys.exit("bench.py: --gpus %d but WORLD_SIZE %d (launch N>1 with torch.distributed.run --nproc-per-node N)"
                  % (args.gpus, world))
+    # coll: the multi-GPU code path (process group, broadcast, all-gathers); always for N > 1, and at N = 1 with
+    # --dist, so one GPU runs exactly what an 8-GPU node runs
+    coll = world > 1 or args.dist
+    if coll and "MASTER_ADDR" not in os.environ:  # --dist without torch.distributed.run: a one-rank rendezvous
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(free_port()), RANK="0", WORLD_SIZE="1")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if coll:
         dist.init_process_group("nccl", device_id=dev)
 
     from mesh_amd import _native, spatialsearch
@@ -222,12 +262,17 @@ def main():
         tree = spatialsearch.aabbtree_compute(v, f)
     build_ms = tree.info().build_ms if tree is not None else 0.0
     bcast_ms = 0.0
-    if world > 1:
+    if coll:
         torch.cuda.synchronize()
         dist.barrier()
         t0 = time.perf_counter()
-        tree = replicate_tree(tree, src=0)
+        # at N = 1 the source unpacks the broadcast blob too, and the timed steps run on that handle
+        replica = replicate_tree(tree, src=0, unpack_on_src=world == 1)
         bcast_ms = (time.perf_counter() - t0) * 1e3
+        if replica is not tree:
+            if tree is not None:
+                tree.free()
+            tree = replica
 
     # ---- inputs resident in HBM: the whole stream on every rank, this rank's contiguous shard ----
     q_all = W.c3_stream(S, dev)
@@ -240,9 +285,9 @@ def main():
         return (torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
                 torch.empty((n, 3), dtype=torch.float64, device=dev))
 
-    slabs = [slab(rows) for _ in range(2 if world > 1 else 1)]
+    slabs = [slab(rows) for _ in range(2 if coll else 1)]
     ring = None
-    if world > 1:
+    if coll:
         ring = ResultRing(slabs, [slab(world * rows) for _ in range(2)])
 
     def answer(sl):
@@ -256,7 +301,7 @@ def main():
 
     def timed(run, steps, rg=None):
         """barrier + sync, `steps` calls of run (every gather drained), sync + barrier; max over ranks"""
-        if world > 1:
+        if coll:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -265,10 +310,10 @@ def main():
         if rg is not None:
             rg.drain()
         torch.cuda.synchronize()
-        if world > 1:
+        if coll:
             dist.barrier()
         el = time.perf_counter() - t0
-        if world > 1:
+        if coll:
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -300,7 +345,7 @@ def main():
     # ---- N > 1, reported beside value (never as value): the same steps without the exchange, and the
     # weak-scaling line (every rank answers the whole stream; the world x S answers are all-gathered) ----
     elapsed_no_ag = elapsed_weak = None
-    if world > 1:
+    if coll:
         elapsed_no_ag = timed(lambda: answer(slabs[0]), args.steps)
         if not args.no_weak:
             del ring, slabs
@@ -319,8 +364,8 @@ def main():
             torch.cuda.empty_cache()
 
     sec = None
-    if args.secondary == "on" or (args.secondary == "auto" and world > 1):
-        sec = secondary(timed, world, rank, dev, args.steps)
+    if args.secondary == "on" or (args.secondary == "auto" and coll):
+        sec = secondary(timed, world, rank, dev, args.steps, coll)
 
     # ---- instrumented traversal (untimed): algorithmic bytes of this rank's shard ----
     nodes, leaves = _native.ctypes.c_uint64(0), _native.ctypes.c_uint64(0)
@@ -336,7 +381,7 @@ def main():
     bytes_per_query_s8d = 56 + 64 * n_node + 80 * n_leaf
 
     if rank != 0:
-        if world > 1:
+        if coll:
             dist.barrier()
             dist.destroy_process_group()
         return
@@ -384,6 +429,15 @@ def main():
                                    "and dependent-load latency (`latency`)") if achieved > HBM_PEAK_GBS else None,
                      # latency side: what bounds the kernel (node steps issued per second, live; lane
                      # occupancy and memory waits from the same build's SQ counters)
+                     # two more ceilings for the same kernel (the HBM `frac` above prices cache-served re-reads as
+                     # HBM bytes): the algorithmic bytes against the aggregate L2 rate (MI355X_MICROARCH.md §L2,
+                     # ~34.5 TB/s), and the VALU pipe's busy fraction from the same build's SQ counters
+                     # (wave-cycles issuing VALU x resident waves per SIMD)
+                     "l2": achieved / L2_PEAK_GBS,
+                     "l2_peak": L2_PEAK_GBS,
+                     "issue": issue_frac(tr),
+                     "issue_note": "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES of k_knn x resident waves per SIMD (from its "
+                                   "VGPR and LDS use; profiles/pmc_traffic.json at the same build id)" if tr else None,
                      "latency": {"node_steps_per_s": S_loc * n_node / avg_kernel_s,
                                  "leaf_tests_per_s": S_loc * n_leaf / avg_kernel_s,
                                  "lanes_active_valu": tr.get("lanes_active_valu") if tr else None,
@@ -400,6 +454,9 @@ def main():
         "entry_cut": {"state": cut["state"], "G": cut["G"], "bytes": cut["bytes"]},
         "build_id": build_id,
         "bvh_broadcast_ms": bcast_ms,
+        # the multi-GPU code path ran (process group, RCCL broadcast + unpack, all-gathers): N > 1, or --dist at N = 1
+        "collectives": ("nccl (RCCL), world %d%s" % (world, ", the source unpacks the broadcast blob" if world == 1
+                                                      else "")) if coll else None,
     }
     if elapsed_no_ag is not None:
         out["value_without_allgather"] = total_q / elapsed_no_ag
@@ -414,7 +471,7 @@ def main():
         out["cpu_baseline"], out["cpu_baseline_allcores"] = cpu_baseline(
             v, f, args.cpu_queries, lambda k: np.ascontiguousarray(q_all[:k].cpu().numpy()))
     print(json.dumps(out), flush=True)
-    if world > 1:
+    if coll:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -57,7 +57,7 @@ typedef struct msh_tree_info {
     uint64_t bytes;      /* device bytes owned by the handle (mesh + BVH) */
     double eps;
     float scene_lo[3], scene_hi[3];
-    double build_ms;     /* GPU time of the LBVH build (Morton + radix sort + emission + refit) */
+    double build_ms;     /* GPU time of the build (Morton + radix sort + emission + re-split + oriented boxes) */
     uint64_t n_meshes;   /* meshes in a batched tree (msh_batch_build), 1 otherwise */
     uint32_t node_bytes; /* bytes of one internal node as stored in HBM (one traversal step reads it) */
     uint32_t leaf_bytes; /* bytes of one leaf record (triangle: 9 x f64 + face id; point: 3 x f64 + id) */
@@ -81,7 +81,8 @@ int msh_version(void);
  * measured (bench.py roofline.traffic). */
 const char* msh_build_id(void);
 int msh_device_count(int* n);
-/* Device used by subsequent builds on the calling thread (default: current HIP device). */
+/* Device used by subsequent builds on the calling thread (default: current HIP device).  It also drops the
+ * thread's device list (msh_set_devices / msh_set_device_list): later trees are built on this device alone. */
 int msh_set_device(int device);
 /* In-process multi-device handles (SURVEY §8(b) msh_set_devices; the reference's drop-in call
  * Mesh.closest_faces_and_points -> AabbTree.nearest, mesh.py:454-455 / search.py:26-30, has no device argument).
@@ -91,7 +92,9 @@ int msh_set_device(int device);
  * ranges) then split their rows over the devices, one host thread and one chunk pipeline per device, so each
  * device's host link carries its share.  Calls below 32 MB of rows stay on the first device.  The answers equal
  * the one-device answers bit for bit (disjoint row ranges of the same arrays).  *_device entry points, batched
- * trees and the intersection tests stay on the handle's own device.
+ * trees and the intersection tests stay on the handle's own device.  Untested across devices: the GPU box this
+ * library is tested on has one device, so the peer copy and the per-device pipelines have run only as replicas on
+ * one device, and the devices' pageable <-> pinned staging copies share one host copy pool (one job at a time).
  *   msh_set_devices(G): devices d, d + 1, ..., d + G - 1 from the current device d (G = 1: one device again);
  *   msh_set_device_list(devices, G): an explicit list (an entry may repeat: several replicas on one device);
  *   msh_tree_devices: the devices of a handle (G = 1 + replicas; devices may be NULL);
@@ -103,7 +106,9 @@ int msh_device_plan(uint64_t S, int G, uint64_t* begins);
 
 /* ---- spatialsearch (spatialsearchmodule.cpp) ---- */
 /* aabbtree_compute(v, f) -> capsule: spatialsearchmodule.cpp:74-127 (TreeAndTri build :108-123).
- * GPU LBVH build: Morton codes of triangle centroids, LDS radix sort, Karras emission, atomic refit. */
+ * GPU LBVH build: Morton codes of triangle centroids, LDS radix sort, Karras emission, subtrees of <= 2^16
+ * leaves re-split top down along the surface, and 64-B nodes holding both children's oriented boxes (exact fp64
+ * extents rounded outward, quantised outward); no refit pass. */
 int msh_tree_build(const double* v, size_t P, const uint32_t* f, size_t T, msh_tree** out);
 /* visibility_compute(v=, f=, extra_v=, extra_f=) builds over main + extra triangles:
  * py_visibility.cpp:114-163.  extra may be NULL/0. */
@@ -131,10 +136,10 @@ int msh_tree_nearest_bary(msh_tree* tree, const double* q, size_t S, uint32_t* f
 int msh_tree_nearest_bary_device(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_face, double* d_pt,
                                  double* d_w, void* stream);
 
-/* The order in which the closest-point path visits the S query rows (d_perm[slot] = row): stable by the top
- * 24 bits of their 30-bit Morton codes in the tree's scene box widened by 10 % (query Morton codes + the LDS radix
- * sort, 3 passes of 8 bits).  No reference counterpart (test and diagnostic entry point).  Asynchronous on
- * `stream`. */
+/* The order in which the closest-point path visits the S query rows (d_perm[slot] = row): stable by the
+ * Hilbert index of each row's cell in a 256^3 grid over the tree's scene box widened by 10 % per side (the cell is
+ * the top 24 bits of the row's 30-bit Morton code, mapped to the Hilbert curve of the same cells; then 3 LDS radix
+ * passes of 8 bits).  No reference counterpart (test and diagnostic entry point).  Asynchronous on `stream`. */
 int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_perm, void* stream);
 
 /* Entry cut of a triangle tree (no reference counterpart: derived acceleration data).  A grid
@@ -153,10 +158,12 @@ int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* 
  *   G > 0: G^3 cells.
  * Calling it (any G != 0, also the current one) makes the next closest-point call build the grid if it is not
  * built yet; changing G frees the current cut first.  A cut that cannot be
- * built (device memory) is not an error: the handle records the failure (state 3) and queries start at the
- * root. */
+ * built (device memory) is not an error: its queries start at the root; an automatic grid is tried again after
+ * another threshold of rows (at most twice, state 0 meanwhile), then the handle records the failure (state 3), as
+ * it does at once for a grid asked for with msh_tree_set_entry_cut. */
 int msh_tree_set_entry_cut(msh_tree* tree, int G);
-/* state: 0 not built yet, 1 built, 2 off (G = 0, or a tree it does not apply to), 3 build failed;
+/* state: 0 not built yet, 1 built, 2 off (G = 0, or a tree it does not apply to), 3 build failed (a handle with
+ * replicas reports a replica's failed or pending state over its own);
  * G: cells per axis of the built cut (0 if none); bytes: device bytes it holds; build_ms: GPU time of its
  * build (cell-centre queries + cut + hints).  Any output pointer may be NULL. */
 int msh_tree_entry_cut_info(const msh_tree* tree, int* state, int* G, uint64_t* bytes, double* build_ms);
@@ -313,7 +320,9 @@ size_t msh_host_pool_bytes(void);
  *    plus two page-locked host slabs).
  * msh_device_pool_trim frees all three (idle entries only: memory held by live handles stays with them);
  * msh_device_pool_bytes reports the device bytes they hold (any pointer may be NULL).  A process that
- * shares the GPU with other allocators (torch) calls the trim after freeing its handles. */
+ * shares the GPU with other allocators (torch) calls the trim after freeing its handles.  A device allocation of
+ * the library that fails for memory first releases the idle workspace, the idle staging slabs' device slabs and
+ * the cached blocks of its device, then tries once more. */
 int msh_device_pool_trim(void);
 int msh_device_pool_bytes(uint64_t* workspace, uint64_t* staging, uint64_t* cached);
 

@@ -41,6 +41,8 @@ void set_error(const char* fmt, ...) {
     g_err = buf;
 }
 
+static void release_idle_device(int dev);  // idle pooled workspaces / staging slabs of a device (below)
+
 // Device allocations of the library (tree buffers, build temporaries, scratch) go through one process-wide cache: a
 // freed block is kept for the next request of a similar size on its device instead of being unmapped, so a caller
 // that builds a tree per call (Mesh.closest_faces_and_points; C4's batched build + query: ~11 GB of buffers per
@@ -66,8 +68,12 @@ class DevCache {
             }
         }
         e = hipMalloc(p, want);
-        if (e == hipErrorOutOfMemory) {  // the cached blocks of this device go first
+        if (e == hipErrorOutOfMemory) {
+            // everything the library holds idle on this device goes first: the idle query workspace and staging
+            // slabs (their blocks come back into this cache), then the cached blocks themselves.  No lock of
+            // this cache is held here, so the pools' lock -> cache lock order is kept.
             (void)hipGetLastError();
+            release_idle_device(dev);
             trim_device(dev);
             e = hipMalloc(p, want);
         }
@@ -264,6 +270,12 @@ class WsPool {
         size_t n = 0;
         for (auto& kv : idle_) n += kv.second.bytes();
         return n;
+    }
+    // the idle workspace of one device (the caller is on that device)
+    void trim_device(int dev) {
+        Workspace ws;
+        take(dev, ws);
+        ws.release();
     }
 
   private:
@@ -620,7 +632,11 @@ static void ensure_entry_cut(msh_tree* t, size_t S) {
         t->cut_state = kCutBuilt;
     } else {
         (void)hipGetLastError();  // clear a sticky launch / allocation error of the failed build
-        t->cut_state = kCutFailed;
+        // an automatic grid is tried again after another threshold of rows (memory may have been freed by then),
+        // at most twice; a grid the caller asked for fails at once (msh_tree_set_entry_cut re-arms it)
+        const bool automatic = !t->cut_force && t->cut_req < 0;
+        t->cut_state = automatic && ++t->cut_fails <= 2 ? kCutPending : kCutFailed;
+        t->cut_rows = 0;
     }
     g_err = keep;
 }
@@ -682,9 +698,9 @@ static const size_t kSortMin = 4096;  // below this the query Morton sort costs 
 // launches without normals) the traversal reads row perm[i] itself and writes the inverse permutation
 // (ws.inv); otherwise the rows (and normals, when given) are gathered once into slot order
 // (ws.qs / ws.ns) with the inverse permutation (gathering the closest-point rows too measured 3 % slower on C3).
-// Queries are ordered by the top 24 bits of their 30-bit Morton code (256 cells per axis, 3 radix passes):
-// C3's 100M queries put ~6 in a cell, and the traversal runs the same node counts as with the full code
-// (sort 3.44 -> 3.08 ms, traversal unchanged).  The order within a cell is the caller's (stable sort).
+// Queries are ordered by the Hilbert index of their cell of a 256^3 grid (the top 24 bits of their 30-bit Morton
+// code, mapped through sort.hip's Hilbert state table; 3 radix passes): C3's 100M queries put ~6 in a cell, and the
+// traversal runs the same node counts as with the full code.  The order within a cell is the caller's (stable sort).
 constexpr int kQuerySortLo = 6;
 static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_t S, hipStream_t s,
                         QueryOrder* ord, bool allow_lazy = false) {
@@ -936,6 +952,21 @@ class StagePool {
             kv.second.clear();
         }
     }
+    // the idle sets' device slabs of one device (the caller is on that device); their pinned host slabs stay
+    void trim_device(int dev) {
+        std::vector<void*> drop;
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            for (StageSet& s : idle_[dev]) {
+                for (int b = 0; b < 3; ++b) {
+                    if (s.d[b]) drop.push_back(s.d[b]);
+                    s.d[b] = nullptr;
+                }
+                s.dbytes = 0;
+            }
+        }
+        for (void* p : drop) (void)dfree(p);
+    }
 
   private:
     std::mutex mu_;
@@ -944,6 +975,11 @@ class StagePool {
 static StagePool& stage_pool() {
     static StagePool* p = new StagePool;  // never destroyed: the runtime may be gone at static destruction
     return *p;
+}
+
+static void release_idle_device(int dev) {
+    ws_pool().trim_device(dev);
+    stage_pool().trim_device(dev);
 }
 // the handle holds the leased set for one call (stage_setup grows it in place)
 struct StageLease {
@@ -1431,7 +1467,8 @@ int msh_device_count(int* n) {
     return MSH_OK;
 }
 
-int msh_set_device(int device) {
+// the calling thread's device, without touching its device list (msh_set_device_list selects its first entry here)
+static int select_device(int device) {
     int c = 0;
     MSH_TRY(msh_device_count(&c));
     if (device < 0 || device >= c) {
@@ -1440,6 +1477,14 @@ int msh_set_device(int device) {
     }
     g_device = device;
     return use_device(device);
+}
+
+// One device: the device list of msh_set_devices / msh_set_device_list is dropped too, so later trees are built
+// on `device` alone and never replicated onto devices the caller no longer asked for.
+int msh_set_device(int device) {
+    MSH_TRY(select_device(device));
+    g_devices.clear();
+    return MSH_OK;
 }
 
 int msh_set_device_list(const int* devices, int G) {
@@ -1453,10 +1498,11 @@ int msh_set_device_list(const int* devices, int G) {
         }
     if (G <= 1) {
         g_devices.clear();
-        return G == 1 ? msh_set_device(devices[0]) : MSH_OK;
+        return G == 1 ? select_device(devices[0]) : MSH_OK;
     }
+    MSH_TRY(select_device(devices[0]));
     g_devices.assign(devices, devices + G);
-    return msh_set_device(devices[0]);
+    return MSH_OK;
 }
 
 int msh_set_devices(int G) {
@@ -1630,7 +1676,15 @@ int msh_tree_set_entry_cut(msh_tree* t, int G) {
 int msh_tree_entry_cut_info(const msh_tree* t, int* state, int* G, uint64_t* bytes, double* build_ms) {
     if (!t) { set_error("msh_tree_entry_cut_info: null tree handle"); return MSH_EINVAL; }
     const uint64_t n = t->d_cut ? (uint64_t)t->cut_G * t->cut_G * t->cut_G : 0;
-    if (state) *state = t->cut_state == kCutPending && !cut_applies(t) ? kCutOff : t->cut_state;
+    auto shown = [](const msh_tree* h) { return h->cut_state == kCutPending && !cut_applies(h) ? kCutOff : h->cut_state; };
+    if (state) {
+        // the handle's state, or the worst of its replicas' (failed, then still pending) when one differs
+        *state = shown(t);
+        for (const msh_tree* r : t->replicas) {
+            const int rs = shown(r);
+            if (rs == kCutFailed || (rs == kCutPending && *state != kCutFailed)) *state = rs;
+        }
+    }
     if (G) *G = t->d_cut ? t->cut_G : 0;
     if (bytes) *bytes = n * (kCutK * sizeof(uint2) + sizeof(int));
     if (build_ms) *build_ms = t->cut_ms;
@@ -1691,9 +1745,12 @@ int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint3
 }
 
 // the whole call's rows settle the entry cut once, before its chunks run
-static int nearest_host(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt) {
+// (S_call: the rows of the whole call, over every replica -- each replica's automatic cut counts them all, so a
+// G-device handle builds its cuts at the call a one-device handle would)
+static int nearest_host(msh_tree* t, const double* q, size_t S, uint32_t* face, uint32_t* part, double* pt,
+                        size_t S_call) {
     MSH_TRY(use_device(t->device));
-    ensure_entry_cut(t, S);
+    ensure_entry_cut(t, S_call);
     // rows: q (24 B in) | face (4 B out) | part (4 B out) | point (24 B out)
     const std::vector<HostArr> arrs = {{q, nullptr, 24}, {nullptr, face, 4}, {nullptr, part, 4}, {nullptr, pt, 24}};
     return pipelined(t, S, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
@@ -1710,7 +1767,7 @@ int msh_tree_nearest(msh_tree* t, const double* q, size_t S, uint32_t* face, uin
     if (S == 0) return MSH_OK;
     if (!q || !face || !pt) { set_error("msh_tree_nearest: null argument"); return MSH_EINVAL; }
     return fan_out(t, S, 56, [&](msh_tree* h, size_t r0, size_t n) {
-        return nearest_host(h, q + 3 * r0, n, face + r0, part ? part + r0 : nullptr, pt + 3 * r0);
+        return nearest_host(h, q + 3 * r0, n, face + r0, part ? part + r0 : nullptr, pt + 3 * r0, S);
     });
 }
 
@@ -1721,7 +1778,7 @@ int msh_tree_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* face
     if (!q || !face || !pt || !w) { set_error("msh_tree_nearest_bary: null argument"); return MSH_EINVAL; }
     return fan_out(t, S, 76, [&](msh_tree* h, size_t r0, size_t S_h) {
         MSH_TRY(use_device(h->device));
-        ensure_entry_cut(h, S_h);
+        ensure_entry_cut(h, S);
         const std::vector<HostArr> arrs = {{q + 3 * r0, nullptr, 24}, {nullptr, face + r0, 4}, {nullptr, pt + 3 * r0, 24},
                                            {nullptr, w + 3 * r0, 24}};
         return pipelined(h, S_h, arrs, [&](size_t, size_t n, const std::vector<char*>& d) {
@@ -2437,7 +2494,14 @@ static int batch_query(msh_tree* t, const double* d_q, size_t S, const SlotOut& 
     if (n == 0) return MSH_OK;
     MSH_TRY(check_count(n, fn));
     // a build still running is waited for on the device (ws_done); its temporaries go once it has passed
-    if (t->pending && hipEventQuery(t->pend_done) == hipSuccess) MSH_TRY(finish_pending(t));
+    if (t->pending) {
+        const hipError_t q = hipEventQuery(t->pend_done);
+        // done, or failed: finish_pending reports a failed build's error instead of answering from it
+        if (q != hipErrorNotReady) {
+            (void)hipGetLastError();
+            MSH_TRY(finish_pending(t));
+        }
+    }
     return batch_query_range(t, d_q, S, 0, t->B, o, pick(t, stream));
 }
 
@@ -2501,7 +2565,8 @@ int msh_batch_nearest_bary(msh_tree* t, const double* q, size_t S, uint32_t* fac
 // (msh_tree_blob_unpack) — the in-process form of bench.py's RCCL broadcast.  A replica on the handle's own device
 // (a repeated entry of the list) unpacks from the blob in place.
 static int replicate_tree(msh_tree* t) {
-    if (g_devices.size() <= 1) return MSH_OK;
+    // the list replicates trees built on its first device only (msh_set_device drops it; this is the backstop)
+    if (g_devices.size() <= 1 || t->device != g_devices[0]) return MSH_OK;
     size_t bytes = 0;
     MSH_TRY(msh_tree_blob_size(t, &bytes));
     MSH_TRY(use_device(t->device));

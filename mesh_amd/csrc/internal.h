@@ -162,6 +162,7 @@ struct msh_tree {
     int cut_state = 0;
     bool cut_force = false;   // msh_tree_set_entry_cut was called: build at the next query, whatever its size
     uint64_t cut_rows = 0;    // closest-point rows answered while the automatic cut waits (ensure_entry_cut)
+    int cut_fails = 0;        // failed automatic builds (retried after another threshold of rows, at most twice)
     double cut_ms = 0.0;
     double cut_lo[3] = {0, 0, 0}, cut_iw[3] = {0, 0, 0};
     msh::Workspace ws;

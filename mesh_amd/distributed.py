@@ -57,12 +57,13 @@ def blob_info(header_bytes):
     return {name: (list(getattr(inf, name)) if name == "origin" else getattr(inf, name)) for name, _ in inf._fields_}
 
 
-def replicate_tree(tree, src=0, device=None, group=None):
+def replicate_tree(tree, src=0, device=None, group=None, unpack_on_src=False):
     """Broadcast a built tree from rank `src` to every rank (RCCL over xGMI); returns this rank's handle.
 
     `tree` is the handle on `src` (ignored elsewhere).  The blob is packed into a torch uint8 tensor on
-    the rank's current CUDA (HIP) device, broadcast once, and unpacked in place on the receivers.
-    """
+    the rank's current CUDA (HIP) device, broadcast once, and unpacked in place on the receivers.  With
+    `unpack_on_src` the source also unpacks the broadcast blob and returns that new handle (the receiver side of
+    the transport, which then runs even at world size 1; the caller keeps `tree`)."""
     import torch
     import torch.distributed as dist
 
@@ -75,7 +76,7 @@ def replicate_tree(tree, src=0, device=None, group=None):
     torch.cuda.synchronize(dev)
     blob = broadcast_bytes(blob, src, group, device=dev)
     torch.cuda.synchronize(dev)
-    if rank == src:
+    if rank == src and not unpack_on_src:
         return tree
     kind = {0: "triangles", 1: "normals", 2: "points"}
     h = _native.blob_unpack(blob.data_ptr(), blob.numel(), dev.index, None)
@@ -209,6 +210,17 @@ def visibility_device(tree, cams, vis, ndc, normals=None, sensors=None, min_dist
         vis.data_ptr(), ndc.data_ptr(), _stream(cams, stream)))
 
 
+def _group(group=None):
+    """(world, rank, collective) of the calling process: the sharded helpers below take their collective path (the
+    all-gathers) whenever a process group is initialised, world size 1 included, so one GPU runs the same code as
+    a multi-GPU node; without a process group they answer everything locally."""
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        return 1, 0, False
+    return dist.get_world_size(group), dist.get_rank(group), True
+
+
 def gather_columns(local, total, group=None):
     """All-gather a 2-D tensor sharded along its LAST axis (this rank holds the columns
     shard_range(total, rank, world)) into the whole (rows, total) tensor on every rank."""
@@ -223,15 +235,14 @@ def visibility_sharded(tree, cams, normals=None, sensors=None, min_dist=1e-3, gr
     import torch
     import torch.distributed as dist
 
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world, rank, coll = _group(group)
     P = int(tree.info().n_points)
     C = cams.shape[0]
     v0, v1 = shard_range(P, rank, world)
     vis = torch.empty((C, v1 - v0), dtype=torch.int32, device=cams.device)
     ndc = torch.empty((C, v1 - v0), dtype=torch.float64, device=cams.device)
     visibility_device(tree, cams, vis, ndc, normals, sensors, min_dist, v0, v1 - v0)
-    if world == 1:
+    if not coll:
         return vis, ndc
     return gather_columns(vis, P, group), gather_columns(ndc, P, group)
 
@@ -242,15 +253,14 @@ def alongnormal_sharded(tree, p, n, group=None):
     import torch
     import torch.distributed as dist
 
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world, rank, coll = _group(group)
     S = p.shape[0]
     a, b = shard_range(S, rank, world)
     d = torch.empty(b - a, dtype=torch.float64, device=p.device)
     fc = torch.empty(b - a, dtype=torch.int32, device=p.device)
     pt = torch.empty((b - a, 3), dtype=torch.float64, device=p.device)
     alongnormal_device(tree, p[a:b].contiguous(), n[a:b].contiguous(), d, fc, pt)
-    if world == 1:
+    if not coll:
         return d, fc, pt
     return gather_results(d, S, group), gather_results(fc, S, group), gather_results(pt, S, group)
 
@@ -265,15 +275,14 @@ def batch_nearest_sharded(v, f, q, group=None, device=None):
     import torch.distributed as dist
     from .search import AabbTreeBatch
 
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    world, rank, coll = _group(group)
     B, S = q.shape[0], q.shape[1]
     b0, b1 = shard_range(B, rank, world)
     if b1 > b0:
         face, part, pt = AabbTreeBatch(v[b0:b1], f).nearest(q[b0:b1], nearest_part=True)
     else:
         face, part, pt = np.empty((0, S), np.uint32), np.empty((0, S), np.uint32), np.empty((0, S, 3))
-    if world == 1:
+    if not coll:
         return face, part, pt
     return gather_mesh_slabs((face, part, pt), B, group, device)
 

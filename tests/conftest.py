@@ -16,9 +16,11 @@ def pytest_configure(config):
 
 
 def _gpu_count():
+    # torch's device count does not initialise HIP on this image, so the pytest process has not used the GPU when
+    # tests/test_dist_gpu.py (the first GPU module) starts its torch.distributed child
     try:
-        from mesh_amd import _native
-        return _native.device_count()
+        import torch
+        return torch.cuda.device_count()
     except Exception:
         return 0
 

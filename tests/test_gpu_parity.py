@@ -1003,6 +1003,14 @@ def test_multi_device_replicas_equal_one_device():
             assert np.array_equal(np.asarray(x), np.asarray(y), equal_nan=np.asarray(x).dtype.kind == "f")
     t = spatialsearch.aabbtree_compute(v, f)
     assert N.tree_devices(t) == [0]
+    # msh_set_device drops the device list: no replica after set_devices([0, 0]) + set_device(0)
+    try:
+        N.set_devices([0, 0])
+        assert N.tree_devices(spatialsearch.aabbtree_compute(v, f)) == [0, 0]
+        N.set_device(0)
+        assert N.tree_devices(spatialsearch.aabbtree_compute(v, f)) == [0]
+    finally:
+        N.set_devices([0])
 
 
 def test_facade_entry_cut_policy():
