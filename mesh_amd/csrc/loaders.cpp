@@ -277,12 +277,17 @@ int msh_obj_arrays(const msh_obj* o, double* v, double* vt, double* vn, uint32_t
     }
     uint64_t s[9];
     msh_obj_sizes(o, s);
-    if (v) std::memcpy(v, o->v.data(), s[0] * 3 * sizeof(double));
-    if (vt) std::memcpy(vt, o->vt.data(), s[1] * s[2] * sizeof(double));
-    if (vn) std::memcpy(vn, o->vn.data(), s[3] * 3 * sizeof(double));
-    if (f) std::memcpy(f, o->f.data(), s[4] * 3 * sizeof(uint32_t));
-    if (ft) std::memcpy(ft, o->ft.data(), s[5] * 3 * sizeof(uint32_t));
-    if (fn) std::memcpy(fn, o->fn.data(), s[6] * 3 * sizeof(uint32_t));
+    // an empty array has no storage (data() may be null): nothing to copy (memcpy's arguments must not be null,
+    // even for 0 bytes; UBSan, scripts/asan_check.sh)
+    auto put = [](void* dst, const void* src, size_t bytes) {
+        if (dst && bytes) std::memcpy(dst, src, bytes);
+    };
+    put(v, o->v.data(), s[0] * 3 * sizeof(double));
+    put(vt, o->vt.data(), s[1] * s[2] * sizeof(double));
+    put(vn, o->vn.data(), s[3] * 3 * sizeof(double));
+    put(f, o->f.data(), s[4] * 3 * sizeof(uint32_t));
+    put(ft, o->ft.data(), s[5] * 3 * sizeof(uint32_t));
+    put(fn, o->fn.data(), s[6] * 3 * sizeof(uint32_t));
     return MSH_OK;
 }
 
@@ -595,10 +600,13 @@ int msh_ply_arrays(const msh_ply* o, double* v, double* tri, double* color, doub
         set_error("msh_ply_arrays: null argument");
         return MSH_EINVAL;
     }
-    if (v) std::memcpy(v, o->v.data(), o->v.size() * sizeof(double));
-    if (tri) std::memcpy(tri, o->tri.data(), o->tri.size() * sizeof(double));
-    if (color && o->has_color) std::memcpy(color, o->color.data(), o->color.size() * sizeof(double));
-    if (normals && o->has_normals) std::memcpy(normals, o->normals.data(), o->normals.size() * sizeof(double));
+    auto put = [](void* dst, const std::vector<double>& src) {  // empty: no storage, nothing to copy
+        if (dst && !src.empty()) std::memcpy(dst, src.data(), src.size() * sizeof(double));
+    };
+    put(v, o->v);
+    put(tri, o->tri);
+    if (o->has_color) put(color, o->color);
+    if (o->has_normals) put(normals, o->normals);
     return MSH_OK;
 }
 

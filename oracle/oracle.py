@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+LIB_PATH = os.environ.get("ORACLE_LIB", os.path.join(_HERE, "_build", "liboracle.so"))  # ORACLE_LIB: sanitizer build
 
 _c_double_p = ctypes.POINTER(ctypes.c_double)
 _c_u32_p = ctypes.POINTER(ctypes.c_uint32)
