@@ -431,7 +431,6 @@ static void free_tree(msh_tree* t) {
     if (t->d_vorder) (void)dfree(t->d_vorder);
     if (t->d_vorder_shard) (void)dfree(t->d_vorder_shard);
     if (t->d_cut) (void)dfree(t->d_cut);
-    if (t->d_cut_hint) (void)dfree(t->d_cut_hint);
     for (int b = 0; b < 3; ++b) {
         if (b < 2 && t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
         if (t->d_stage[b]) (void)dfree(t->d_stage[b]);
@@ -499,23 +498,21 @@ static bool cut_applies(const msh_tree* t) {
 }
 
 static void free_entry_cut(msh_tree* t) {
-    if (t->d_cut || t->d_cut_hint) {
+    if (t->d_cut) {
         (void)hipSetDevice(t->device);
         if (t->ws_done) (void)hipEventSynchronize(t->ws_done);  // no launch may still read the cut
-        if (t->d_cut) (void)dfree(t->d_cut);
-        if (t->d_cut_hint) (void)dfree(t->d_cut_hint);
+        (void)dfree(t->d_cut);
     }
     t->d_cut = nullptr;
-    t->d_cut_hint = nullptr;
     t->cut_G = 0;
     t->cut_ms = 0.0;
 }
 
-// cells per leaf and the cap of the automatic grid, C3 (1,003,520 faces) in M q/s: 8 per leaf, 2^23 cells: G = 200,
-// 46.9 node visits per query, 2156-2213; 16, 2^25: G = 252, 45.2 visits, 2238; 32, 2^25: G = 318 (2.2 GB, built in
-// 35 ms), 43.6 visits, 2247-2290 (profiles/r05_ab_noleaders_cut.jsonl); in another session 32: 2261-2286, 64, 2^26:
-// G = 400 (4.4 GB, 65 ms), 42.2 visits, 2293-2321, 128, 2^27: G = 505 (8.8 GB, 165 ms), 41.0 visits, 2297-2333
-// (profiles/r05_ab_cut_size.jsonl).  The grid is derived data of a kept tree: 64 per leaf.
+// cells per leaf and the cap of the automatic grid, C3 (1,003,520 faces) in M q/s, round 5 (8 entries + hint per
+// 68-B cell): 8 per leaf, 2^23 cells: G = 200, 46.9 node visits per query, 2156-2213; 16, 2^25: G = 252, 45.2 visits,
+// 2238; 32, 2^25: G = 318, 43.6 visits, 2247-2290 (profiles/r05_ab_noleaders_cut.jsonl); in another session 32:
+// 2261-2286, 64, 2^26: G = 400, 42.2 visits, 2293-2321, 128, 2^27: G = 505, 41.0 visits, 2297-2333
+// (profiles/r05_ab_cut_size.jsonl).  The grid is derived data of a kept tree: 64 per leaf, 32-B records (C3: 2.05 GB).
 #ifndef MSH_CUT_PER_LEAF
 #define MSH_CUT_PER_LEAF 64
 #endif
@@ -525,9 +522,35 @@ static void free_entry_cut(msh_tree* t) {
 static size_t auto_cut_cells(const msh_tree* t) {
     return std::min<size_t>((size_t)MSH_CUT_PER_LEAF * t->T, (size_t)1 << MSH_CUT_MAX_LOG2);
 }
+// record bytes per cell: 32 (4-B entries) for trees of <= 2^20 leaves, else 64
+static size_t cut_rec_bytes(const msh_tree* t) { return t->T <= kEnt4MaxLeaves ? 32 : 64; }
+
+// Grid of the cut and its levels: G = G0 2^L.  The coarsest grid's cell centres are answered exactly by the tree
+// (G0^3 queries) and cut from the root; each finer level starts every cell from the record of the coarser cell
+// that contains it (nearest.hip k_cut_level), so no level walks from the root and only G0^3 centres are traversed.
+// The automatic grid takes L = 3 (C3: G0 = 50, G = 400); an explicit G takes the largest L <= 3 with G0 = G / 2^L
+// an integer >= 8 (L = 0: one level, every centre answered, as round 5 built every grid).
+static void cut_levels(const msh_tree* t, int* G, int* L) {
+    if (t->cut_req > 0) {
+        *G = t->cut_req;
+        *L = 0;
+        while (*L < 3 && (*G % (2 << *L)) == 0 && (*G >> (*L + 1)) >= 8) ++*L;
+        return;
+    }
+    const double g = std::cbrt((double)auto_cut_cells(t));
+    const int g0 = (int)std::lround(g / 8.0);
+    if (g0 >= 8) {
+        *G = 8 * g0;
+        *L = 3;
+    } else {
+        *G = std::max(16, (int)std::lround(g));
+        *L = 0;
+    }
+}
+
 static int build_entry_cut(msh_tree* t) {
-    const size_t cells = auto_cut_cells(t);
-    const int G = t->cut_req > 0 ? t->cut_req : std::max(16, (int)std::lround(std::cbrt((double)cells)));
+    int G = 0, L = 0;
+    cut_levels(t, &G, &L);
     double half[3], H = 0.0, lo[3], w[3];
     for (int k = 0; k < 3; ++k) {
         half[k] = 0.5 * ((double)t->scene_hi[k] - (double)t->scene_lo[k]);
@@ -537,17 +560,21 @@ static int build_entry_cut(msh_tree* t) {
         set_error("entry cut: degenerate scene box");
         return MSH_EINVAL;
     }
+    double ext[3];
     for (int k = 0; k < 3; ++k) {
         const double m = 0.5 * ((double)t->scene_hi[k] + (double)t->scene_lo[k]);
         const double e = 1.25 * std::max(half[k], 0.05 * H);
         lo[k] = m - e;
-        w[k] = 2.0 * e / G;
+        ext[k] = 2.0 * e;
+        w[k] = ext[k] / G;
     }
     const size_t n = (size_t)G * G * G;
     if (n > 0xFFFFFFFFull) {
         set_error("entry cut: %d^3 cells exceed one query call", G);
         return MSH_ENOMEM;
     }
+    const bool e4 = t->T <= kEnt4MaxLeaves;
+    const size_t rb = cut_rec_bytes(t);
     hipStream_t s = t->stream;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     MSH_HIP(hipEventCreate(&e0));
@@ -557,29 +584,49 @@ static int build_entry_cut(msh_tree* t) {
         MSH_HIP(e);
     }
     (void)hipEventRecord(e0, s);
-    uint2* cut = nullptr;
-    int* hint = nullptr;
+    uint32_t* cut = nullptr;
     int st = MSH_OK;
     {
-        DevBuf dq, df, dp, dinv;
+        // level 0: the G0^3 centres answered exactly (walks from the root: no cut is installed while it is built)
+        const int G0 = G >> L;
+        const size_t n0 = (size_t)G0 * G0 * G0;
+        double w0[3] = {ext[0] / G0, ext[1] / G0, ext[2] / G0};
+        DevBuf dq, df, dp, dinv, dhint, prev, cur;
         do {
-            if ((st = dq.reserve(n * 3 * sizeof(double))) != MSH_OK) break;
-            if ((st = df.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
-            if ((st = dp.reserve(n * 3 * sizeof(double))) != MSH_OK) break;
-            if ((st = cut_centres(G, lo, w, dq.as<double>(), s)) != MSH_OK) break;
-            // the centres' own walks start at the root (no cut is installed while it is built)
-            if ((st = msh_tree_nearest_device(t, dq.as<double>(), n, df.as<uint32_t>(), nullptr, dp.as<double>(), s)) != MSH_OK)
-                break;
-            e = dmalloc(&cut, n * kCutK * sizeof(uint2));
-            if (e == hipSuccess) e = dmalloc(&hint, n * sizeof(int));
-            if (e != hipSuccess) {
-                set_error("hipMalloc entry cut (%zu cells): %s", n, hipGetErrorString(e));
-                st = MSH_ENOMEM;
-                break;
-            }
-            if ((st = cut_build(t, G, lo, w, dp.as<double>(), cut, s)) != MSH_OK) break;
+            if ((st = dq.reserve(n0 * 3 * sizeof(double))) != MSH_OK) break;
+            if ((st = df.reserve(n0 * sizeof(uint32_t))) != MSH_OK) break;
+            if ((st = dp.reserve(n0 * 3 * sizeof(double))) != MSH_OK) break;
+            if ((st = dhint.reserve(n0 * sizeof(int))) != MSH_OK) break;
             if ((st = dinv.reserve(t->T * sizeof(uint32_t))) != MSH_OK) break;
-            if ((st = cut_hints(t, df.as<uint32_t>(), n, dinv.as<uint32_t>(), hint, s)) != MSH_OK) break;
+            if ((st = cut_centres(G0, lo, w0, dq.as<double>(), s)) != MSH_OK) break;
+            if ((st = msh_tree_nearest_device(t, dq.as<double>(), n0, df.as<uint32_t>(), nullptr, dp.as<double>(), s)) !=
+                MSH_OK)
+                break;
+            if ((st = cut_hints(t, df.as<uint32_t>(), n0, dinv.as<uint32_t>(), dhint.as<int>(), s)) != MSH_OK) break;
+            // levels 0 .. L: records of the G0 2^l grid; the last one is the cut
+            const uint32_t* parent = nullptr;
+            for (int l = 0; l <= L && st == MSH_OK; ++l) {
+                const int Gl = G0 << l;
+                const size_t nl = (size_t)Gl * Gl * Gl;
+                const double wl[3] = {ext[0] / Gl, ext[1] / Gl, ext[2] / Gl};
+                uint32_t* out = nullptr;
+                if (l == L) {
+                    e = dmalloc(&cut, nl * rb);
+                    if (e != hipSuccess) {
+                        set_error("hipMalloc entry cut (%zu cells): %s", nl, hipGetErrorString(e));
+                        st = MSH_ENOMEM;
+                        break;
+                    }
+                    out = cut;
+                } else {
+                    if ((st = cur.reserve(nl * rb)) != MSH_OK) break;
+                    out = cur.as<uint32_t>();
+                }
+                st = cut_level(t, Gl, lo, wl, parent, l == 0 ? dhint.as<int>() : nullptr, out, e4, s);
+                parent = out;
+                std::swap(prev, cur);  // this level's records become the next level's parents
+            }
+            if (st != MSH_OK) break;
             (void)hipEventRecord(e1, s);
             if ((e = hipStreamSynchronize(s)) != hipSuccess) {
                 set_error("entry cut build: %s", hipGetErrorString(e));
@@ -593,15 +640,14 @@ static int build_entry_cut(msh_tree* t) {
         (void)hipEventElapsedTime(&ms, e0, e1);
         t->cut_ms = ms;
         t->d_cut = cut;
-        t->d_cut_hint = hint;
+        t->cut_wide = e4 ? 0 : 1;
         t->cut_G = G;
         for (int k = 0; k < 3; ++k) {
             t->cut_lo[k] = lo[k];
             t->cut_iw[k] = 1.0 / w[k];
         }
-    } else {
-        if (cut) (void)dfree(cut);
-        if (hint) (void)dfree(hint);
+    } else if (cut) {
+        (void)dfree(cut);
     }
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
@@ -1686,7 +1732,7 @@ int msh_tree_entry_cut_info(const msh_tree* t, int* state, int* G, uint64_t* byt
         }
     }
     if (G) *G = t->d_cut ? t->cut_G : 0;
-    if (bytes) *bytes = n * (kCutK * sizeof(uint2) + sizeof(int));
+    if (bytes) *bytes = n * (t->cut_wide ? 64 : 32);
     if (build_ms) *build_ms = t->cut_ms;
     return MSH_OK;
 }

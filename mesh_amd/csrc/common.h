@@ -399,14 +399,13 @@ __host__ __device__ inline RayF make_rayf(const D3& o, const D3& d, double M, bo
     return r;
 }
 
-// Both children of a node: does the ray's parameter range meet the child's oriented box, and at which
-// entry parameter (the near-first key of the visibility traversal).
-__host__ __device__ inline void ray_child_slabs(const NodeV& nd, const RayF& r, bool& h0, bool& h1, float& s0, float& s1) {
-    if (r.wide) {
-        h0 = h1 = true;
-        s0 = s1 = r.slo;
-        return;
-    }
+// Both children of a node: the ray's parameter interval [n_c, f_c] inside child c's oriented box, clipped to
+// [slo, shi] (before the 2^-20 widening of the tests below; `wide` rays: the whole range).
+__host__ __device__ inline void ray_child_range(const NodeV& nd, const RayF& r, float& n0, float& f0, float& n1,
+                                                float& f1) {
+    n0 = n1 = r.slo;
+    f0 = f1 = r.shi;
+    if (r.wide) return;
 #if defined(MUTATE_RAY_MARGIN)  // tests/csrc/bound_check.cpp's sensitivity check: must find violations
     const float mg = 0.f;
 #else
@@ -427,7 +426,6 @@ __host__ __device__ inline void ray_child_slabs(const NodeV& nd, const RayF& r, 
                             w1 & 0xffu, (w1 >> 8) & 0xffu, (w1 >> 16) & 0xffu, w1 >> 24,
                             w2 & 0xffu, (w2 >> 8) & 0xffu, (w2 >> 16) & 0xffu, w2 >> 24};
     const F2 pm = f2(mg, -mg);
-    float n0 = r.slo, f0 = r.shi, n1 = r.slo, f1 = r.shi;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const F2 inv = f2(rcp_f32(pd[k]));
@@ -440,11 +438,44 @@ __host__ __device__ inline void ray_child_slabs(const NodeV& nd, const RayF& r, 
         n1 = fmaxf(n1, fminf(t1.x, t1.y));
         f1 = fminf(f1, fmaxf(t1.x, t1.y));
     }
+}
+
+// Does the ray meet each child (the interval test widened by 2^-20 (|n| + |f|)), and at which entry parameter
+// (the near-first key of the visibility traversal).
+__host__ __device__ inline void ray_child_slabs(const NodeV& nd, const RayF& r, bool& h0, bool& h1, float& s0, float& s1) {
+    float n0, f0, n1, f1;
+    ray_child_range(nd, r, n0, f0, n1, f1);
     const float w = 9.5367431640625e-7f;  // 2^-20
     h0 = n0 <= f0 + w * (fabsf(n0) + fabsf(f0));
     h1 = n1 <= f1 + w * (fabsf(n1) + fabsf(f1));
     s0 = n0;
     s1 = n1;
+}
+
+// Lines (nearest_alongnormal): as ray_child_slabs, and for each child a lower bound of the squared distance from
+// the line's point p (parameter 0) to any real hit inside the child.  u = d / |d| is a unit direction, so the
+// parameter s of a hit x = p + s u is its signed distance from p; a real hit's s* lies in the widened interval
+// [n - e, f + e], e = 2^-20 (|n| + |f|) (the derivation above: the endpoints are within 3u relative of the exact
+// quotients, and e is 16x that), so |x - p| >= max(n - e, -(f + e), 0).  That bound, shrunk by 2^-20 and its square
+// by 2^-19 against the fp32 roundings of forming it, is the key: it is never larger than the exact distance of a
+// hit in the child (tests/csrc/bound_check.cpp checks it on the same rays as the slab test), and it is at least
+// the distance from p to the child's box, which the line's hits lie in.
+__host__ __device__ inline void ray_child_line_dist2(const NodeV& nd, const RayF& r, bool& h0, bool& h1, float& k0,
+                                                     float& k1) {
+    float n0, f0, n1, f1;
+    ray_child_range(nd, r, n0, f0, n1, f1);
+    const float w = 9.5367431640625e-7f;  // 2^-20
+    const float e0 = w * (fabsf(n0) + fabsf(f0)), e1 = w * (fabsf(n1) + fabsf(f1));
+    h0 = n0 <= f0 + e0;
+    h1 = n1 <= f1 + e1;
+#if defined(MUTATE_LINE_DIST)  // tests/csrc/bound_check.cpp's sensitivity check: the far end instead of the near one
+    const float g0 = fmaxf(fmaxf(f0, -n0), 0.f), g1 = fmaxf(fmaxf(f1, -n1), 0.f);
+#else
+    const float g0 = fmaxf(fmaxf(n0 - e0, -(f0 + e0)), 0.f) * (1.f - w);
+    const float g1 = fmaxf(fmaxf(n1 - e1, -(f1 + e1)), 0.f) * (1.f - w);
+#endif
+    k0 = g0 * g0 * (1.f - 2.f * w);
+    k1 = g1 * g1 * (1.f - 2.f * w);
 }
 
 // Per-lane traversal stack: entry sp lives in LDS (lds[sp * kBlock], lane-interleaved) for

@@ -151,10 +151,11 @@ struct msh_tree {
                e_down[3] = {nullptr, nullptr, nullptr};
     double build_ms = 0.0;
     int max_depth = 0;             // bound of the deepest leaf (root children = 1): k_karras prefix lengths
-    // entry cut (single triangle trees; nearest.hip build_entry_cut): a G^3 grid over the scene box widened by
-    // 1/4, kCutK start entries per cell; d_cut == nullptr: every query starts at the root
-    uint2* d_cut = nullptr;
-    int* d_cut_hint = nullptr;  // per cell: the leaf of the closest face of its centre (-1: none)
+    // entry cut (single triangle trees; api.cpp build_entry_cut): a G^3 grid over the scene box widened by 1/4, one
+    // record per cell -- its hint leaf and kCutK start entries, 32 B (4-B entries, trees of <= 2^20 leaves) or 64 B
+    // (cut_wide) --; d_cut == nullptr: every query starts at the root
+    uint32_t* d_cut = nullptr;
+    int cut_wide = 0;
     int cut_G = 0;
     // lazily built on the first closest-point query (msh_tree_set_entry_cut): requested grid (< 0 automatic,
     // 0 off), state (0 pending, 1 built, 2 off / not applicable, 3 failed), GPU build time
@@ -234,14 +235,16 @@ int gather_rows(const double* d_a, const double* d_b, const uint32_t* d_perm, si
 // caller row j <- slot inv[j] (record fields + nw doubles per row from d_w)
 int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32_t* d_inv, size_t S, const SlotOut& o,
                       hipStream_t s);
-// Entry cut of a single triangle tree: the start entries of every grid cell from the exact closest points
-// of the cell centres (d_pts, G^3 rows, answered by the tree itself), written to tree->d_cut (kCutK per cell)
-#ifndef MSH_CUT_K
-#define MSH_CUT_K 8
-#endif
-constexpr int kCutK = MSH_CUT_K;  // 4: 1773-1800 M q/s (49.5-51.2 visits), 16: 1285 (C3, profiles/r03_c3_entry_cut_ab.jsonl)
+// Entry cut of a single triangle tree, level by level (nearest.hip k_cut_level): the records of a G^3 grid from the
+// records of the G/2 grid (d_prec), or on the coarsest level from the root with the hint leaves d_phint of the
+// cell centres' exact answers; e4: 32-B records of 4-B entries (trees of <= 2^20 leaves), else 64-B records.
+// kCutK start entries per cell (the hint takes the record's eighth word; 8 entries of 8 B + a separate hint in
+// round 5; 4: 1773-1800 M q/s against 8, 16: 1285, C3, profiles/r03_c3_entry_cut_ab.jsonl)
+constexpr int kCutK = 7;
+constexpr size_t kEnt4MaxLeaves = (size_t)1 << 20;  // 4-B stack / cut entries: refs in [-2^20, 2^20), 21 bits
 int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s);
-int cut_build(msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, uint2* d_cut, hipStream_t s);
+int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const uint32_t* d_prec, const int* d_phint,
+              uint32_t* d_rec, bool e4, hipStream_t s);
 // d_hint[cell] = the leaf holding face d_face[cell] (d_inv: T scratch words)
 int cut_hints(const msh_tree* tree, const uint32_t* d_face, size_t n, uint32_t* d_inv, int* d_hint, hipStream_t s);
 // closest point: o.face, o.part (nullable), o.pt; with o.w (3 per row) the barycentric variant (part unused)

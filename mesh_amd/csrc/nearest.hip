@@ -100,10 +100,10 @@ struct KnnArgs {
     // field carries the winner's leaf index instead of its part code (leader_leaf)
     bool rec_leaf;
     bool list;      // closest-point modes: wave leaf list (trees of < 2^26 leaves) instead of per-lane queues
-    // entry cut (list path; single trees): a query inside the grid starts from its cell's entries instead of
-    // the root (build_entry_cut); nullptr: from the root
-    const uint2* cut;
-    const int* cut_hint;  // per cell: the leaf of its centre's closest face, the hint of unhinted phases
+    // entry cut (list path; single trees): a query inside the grid starts from its cell's record -- the cell's hint
+    // leaf and up to kCutK start entries -- instead of the root (build_entry_cut); nullptr: from the root
+    const uint32_t* cut;
+    int cut_wide;  // records of 64 B with 8-B entries (trees of > 2^20 leaves); else 32 B with 4-B entries
     int cut_G;
     double cut_lo[3], cut_iw[3];
     size_t nunits;  // work units of this phase (slots it covers)
@@ -268,7 +268,6 @@ struct Ent4 {
     __device__ static int ref(T e) { return __builtin_amdgcn_sbfe((int)e, 0, 21); }
     __device__ static float bound(T e) { return __uint_as_float(e & 0xFFE00000u); }
 };
-constexpr size_t kEnt4MaxLeaves = (size_t)1 << 20;  // refs in [-2^20, 2^20): 21 bits
 
 // A node's 64 B loaded into LDS ahead of its step (global_load_lds: no registers hold it while the lane appends
 // leaves or runs leaf rounds).  The wave's slot array holds 4 x 64 float4 (piece k of lane l at k * 64 + l); wsl =
@@ -642,21 +641,37 @@ __device__ inline size_t cut_cell(const KnnArgs& a, const D3& q) {
     if (!(ux >= 0.0 && ux < G && uy >= 0.0 && uy < G && uz >= 0.0 && uz < G)) return kNoCell;
     return ((size_t)(unsigned)uz * (size_t)a.cut_G + (unsigned)uy) * (size_t)a.cut_G + (unsigned)ux;
 }
+// the cell's record: word 0 its hint leaf (-1: none), then kCutK entries nearest-first -- 4-B entries in the stack's
+// own packing (Ent4: the bound's top 11 bits over a 21-bit ref; empty entries have the sign bit set) in a 32-B
+// record, or (ref, bound bits) pairs from word 2 of a 64-B record (empty: ref kCutEmpty)
+__device__ inline const uint32_t* cut_rec(const KnnArgs& a, size_t cell) {
+    return a.cut + cell * (a.cut_wide ? 16 : 8);
+}
 template <class Pol, class W>
 __device__ inline bool cut_start(const KnnArgs& a, size_t cell, const Pol& pol, W& w, typename W::Ent* __restrict__ lds,
                                  uint2* __restrict__ spill) {
-    const uint4* c = reinterpret_cast<const uint4*>(a.cut + cell * kCutK);
-    uint4 e[kCutK / 2];
+    const uint32_t* r = cut_rec(a, cell);
+    if (a.cut_wide) {
+        const uint4* c = reinterpret_cast<const uint4*>(r);
+        uint4 e[4];
 #pragma unroll
-    for (int j = 0; j < kCutK / 2; ++j) e[j] = c[j];
-    auto put = [&](uint32_t ref, uint32_t sb) {
-        if (ref == kCutEmpty) return;
-        w.push(ref, sb, lds, spill);
-    };
+        for (int j = 0; j < 4; ++j) e[j] = c[j];
+        auto put = [&](uint32_t ref, uint32_t sb) {
+            if (ref != kCutEmpty) w.push(ref, sb, lds, spill);
+        };
 #pragma unroll
-    for (int j = kCutK / 2 - 1; j >= 0; --j) {
-        put(e[j].z, e[j].w);
-        put(e[j].x, e[j].y);
+        for (int j = 3; j >= 1; --j) {
+            put(e[j].z, e[j].w);
+            put(e[j].x, e[j].y);
+        }
+        put(e[0].z, e[0].w);  // entry 0 (words 2, 3)
+    } else {
+        const uint4* c = reinterpret_cast<const uint4*>(r);
+        const uint4 e0 = c[0], e1 = c[1];
+        const uint32_t e[kCutK] = {e0.y, e0.z, e0.w, e1.x, e1.y, e1.z, e1.w};
+#pragma unroll
+        for (int j = kCutK - 1; j >= 0; --j)
+            if ((int)e[j] >= 0) w.push((uint32_t)Ent4::ref(e[j]), e[j] & 0xFFE00000u, lds, spill);
     }
     return w.pop(pol, lds, spill);
 }
@@ -714,10 +729,10 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
         int hint_leaf = -1;  // STATS
         const size_t cell = kList && fin ? cut_cell(a, q) : kNoCell;
         if constexpr (MODE == 0 || MODE == 3) {
-            if (kList && a.cut_hint && cell != kNoCell && a.phase != 2) {
-                // slots without a leader (super-leaders, leaders, unled launches) inside the grid: the leaf of
-                // the cell centre's closest face, within d(c) + r of q's own answer
-                const int lf = a.cut_hint[cell];
+            if (kList && a.cut && cell != kNoCell && a.phase != 2) {
+                // slots without a leader (super-leaders, leaders, unled launches) inside the grid: the cell's hint
+                // leaf (the closest face found for its centre), within U(c) + r of q's own answer
+                const int lf = (int)cut_rec(a, cell)[0];
                 if (STATS) hint_leaf = lf;
                 if (lf >= 0) {
                     pol.test(lf);
@@ -731,7 +746,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 if (STATS) hint_leaf = lf;
 #if MSH_FOLLOW_CELL
                 // followers inside the grid also test their cell's hint leaf (one call site: a loop of two)
-                const int lc = (kList && a.cut_hint && cell != kNoCell) ? a.cut_hint[cell] : -1;
+                const int lc = (kList && a.cut && cell != kNoCell) ? (int)cut_rec(a, cell)[0] : -1;
 #pragma nounroll
                 for (int j = 0; j < 2; ++j) {
                     const int h = j == 0 ? lf : (lc != lf ? lc : -1);
@@ -1451,7 +1466,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     // launch (C3 100M: 1985-1990 -> 2150-2179 M q/s without leader phases; one N = 8 shard of 12.5M rows 9.0 ->
     // 7.55 ms, profiles/r05_ab_leaders_sort_resume.jsonl); batched trees and trees without a cut keep them
     const bool lead = kLead > 1 && (MODE == 0 || MODE == 3) && a.res != nullptr && a.S >= 64 * (size_t)kLead &&
-                      a.T >= kLeadMinLeaves && !(a.list && a.cut_hint);
+                      a.T >= kLeadMinLeaves && !(a.list && a.cut);
     a.max_deferred = (unsigned)std::min<size_t>(a.S, (a.S / 16) + 65536);
     DevBuf& dbuf = ws.flags;
     MSH_TRY(dbuf.reserve((size_t)a.max_deferred * sizeof(DeferRec)));
@@ -1493,7 +1508,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         {
             TimedLaunch t1(STATS ? "knn_pass1_stats" : "knn_pass1", s);
             if (lead) {
-                if (a.list && a.cut_hint) {
+                if (a.list && a.cut) {
                     // cell hints serve every leader inside the entry cut's grid, so the super-leaders would only
                     // hint leaders outside it: one leader launch over every leader slot (phase 4; outside the
                     // grid unhinted) instead of a super-leader launch the chip cannot fill
@@ -1578,7 +1593,7 @@ static KnnArgs tree_args(const msh_tree* tree, size_t S) {
 static void cut_args(const msh_tree* tree, KnnArgs& a) {
     if (!tree->d_cut || tree->B != 1) return;
     a.cut = tree->d_cut;
-    a.cut_hint = tree->d_cut_hint;
+    a.cut_wide = tree->cut_wide;
     a.cut_G = tree->cut_G;
     for (int k = 0; k < 3; ++k) {
         a.cut_lo[k] = tree->cut_lo[k];
@@ -1654,41 +1669,107 @@ __global__ __launch_bounds__(kBlock) void k_cut_centres(int G, double lx, double
     q[3 * cell + 2] = lz + ((double)iz + 0.5) * wz;
 }
 
-// One thread per cell.  From the root, entries (internal nodes or ~leaves) are replaced by their children
-// whose bound from the centre c is within R^2 = ((d(c) + 2r) (1 + 1e-6))^2 (r = the cell's half-diagonal
-// + 0.1 %, so a query rounded into a neighbouring cell stays covered), in passes over the list, while the
-// list keeps at most kCutK entries; a child outside R is dropped (the cull is the traversal's own: bound >
-// fp32(R^2 (1 + 2^-40)) rounded up).  Out: entries nearest-first, (ref, max(s, 0)^2 rounded down to fp32 with
-// s = sqrt(bound) (1 - 1e-5) - r (1 + 1e-5)), unused ones kCutEmpty; a centre without an answer keeps the root.
-__global__ __launch_bounds__(kBlock) void k_cut_build(const BNode* __restrict__ nodes, double ox, double oy, double oz,
-                                                      double tm, int G, double lx, double ly, double lz, double wx,
-                                                      double wy, double wz, const double* __restrict__ pts,
-                                                      uint2* __restrict__ cut) {
+// One level of the entry cut, one thread per cell of a G^3 grid (cell (ix, iy, iz) = row (iz G + iy) G + ix).  The
+// cell starts from its parent's record -- the cell of the G/2 grid that contains it (G even) -- or, on the
+// coarsest level (prec == nullptr), from the root with the hint leaf phint[cell] of its centre's exact closest face.
+//   U(c) = the exact distance from the centre c to the best leaf seen: first the parent's hint leaf, then every
+//   leaf the expansion meets (CGAL's fp64 construction, as a query's leaf test).  R = (U(c) + 2r) (1 + 1e-6), r
+//   the cell's half-diagonal + 0.1 %.  For q in the cell, d(q) <= U(c) + r, so a subtree farther than R from c
+//   holds neither q's answer nor a tie.  The parent's entries cover every subtree within R_p of c_p, and R +
+//   |c - c_p| <= R_p (U(c) <= U(c_p) + |c - c_p|, |c - c_p| <= r = r_p / 2), so they cover the child's.
+//   Entries (internal nodes or ~leaves) are replaced by their children whose bound from c is within R, in passes
+//   over the list, while it keeps at most kCutK entries; a child outside R is dropped (the cull is the
+//   traversal's own: bound > fp32(R^2 (1 + 2^-40)) rounded up).  An entry's bound from c: its box bound when its
+//   parent node was expanded here, the smaller of its children's bounds when its own node was loaded, the exact
+//   squared distance for a leaf -- each a lower bound of the squared distance from c to what it holds.
+// Out (E4: 32-B records of 4-B entries, trees of <= 2^20 leaves; else 64-B records of (ref, bound bits)): word 0
+// the best leaf (the hint of unhinted slots), then the entries nearest-first with max(s, 0)^2 rounded down to
+// fp32, s = sqrt(bound) (1 - 1e-5) - r (1 + 1e-5): a lower bound of the squared distance from any q of the cell.
+// Round 5 answered every cell centre of the final grid exactly (64M traversals on C3) and cut each cell from the
+// root: 65 ms and 4.4 GB of 68-B cells, against a few ms per level and 2.05 GB here.
+template <bool E4>
+__global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ nodes, const TriRec* __restrict__ tris,
+                                                      double ox, double oy, double oz, double tm, int G, double lx,
+                                                      double ly, double lz, double wx, double wy, double wz,
+                                                      const uint32_t* __restrict__ prec, const int* __restrict__ phint,
+                                                      uint32_t* __restrict__ rec) {
+    constexpr int kw = E4 ? 8 : 16;  // record words
     const size_t n = (size_t)G * G * G;
     const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
     if (cell >= n) return;
     const size_t ix = cell % (size_t)G, iy = (cell / (size_t)G) % (size_t)G, iz = cell / ((size_t)G * G);
     const D3 c = D3{lx + ((double)ix + 0.5) * wx, ly + ((double)iy + 0.5) * wy, lz + ((double)iz + 0.5) * wz};
-    const D3 p = D3{pts[3 * cell], pts[3 * cell + 1], pts[3 * cell + 2]};
     const double r = 0.5 * sqrt(wx * wx + wy * wy + wz * wz) * 1.001;
-    const double R = (sqrt(sqdist(c, p)) + 2.0 * r) * (1.0 + 1e-6);
     int ref[kCutK];
-    float bd[kCutK];
-    int m = 1;
-    ref[0] = 0;
-    bd[0] = 0.f;
-    if (R < INFINITY) {  // NaN / inf (no answer): the root only
-        const float limf = __double2float_ru(R * R * kSlack);
-        const double o[3] = {ox, oy, oz};
-        const QF qf = make_qf(c, o, tm);
+    float bd[kCutK];  // bound from c; -1: not formed yet (an entry taken over from the parent)
+    int m = 0, best_leaf = -1;
+    if (prec) {
+        const size_t H = (size_t)(G / 2);
+        const uint32_t* p = prec + (((iz >> 1) * H + (iy >> 1)) * H + (ix >> 1)) * kw;
+        best_leaf = (int)p[0];
+#pragma unroll
+        for (int k = 0; k < kCutK; ++k) {
+            int e;
+            bool ok;
+            if (E4) {
+                e = Ent4::ref(p[1 + k]);
+                ok = (int)p[1 + k] >= 0;
+            } else {
+                e = (int)p[2 + 2 * k];
+                ok = (uint32_t)e != kCutEmpty;
+            }
+            if (ok) {
+                ref[m] = e;
+                bd[m] = -1.f;
+                ++m;
+            }
+        }
+    } else {
+        best_leaf = phint[cell];
+        ref[0] = 0;
+        bd[0] = -1.f;
+        m = 1;
+    }
+    uint32_t fdummy;
+    double U2 = INFINITY;  // squared distance from c to best_leaf
+    if (best_leaf >= 0) {
+        D3 ta, tb, tc, o;
+        int part;
+        load_tri(tris, best_leaf, ta, tb, tc, fdummy);
+        U2 = closest_on_triangle(c, ta, tb, tc, o, part);
+    }
+    auto limit = [&](double u2) {
+        const double R = (sqrt(u2) + 2.0 * r) * (1.0 + 1e-6);
+        return R < INFINITY ? __double2float_ru(R * R * kSlack) : INFINITY;
+    };
+    float limf = limit(U2);
+    const double o3[3] = {ox, oy, oz};
+    const QF qf = make_qf(c, o3, tm);
+    if (m > 0 && limf < INFINITY) {
         for (int pass = 0; pass < 256; ++pass) {
             bool changed = false;
             const int m0 = m;
             for (int k = 0; k < m0 && k < m; ++k) {
-                if (ref[k] < 0) continue;
+                if (ref[k] < 0) {  // a leaf: its exact distance, once; it may improve U(c) and the hint
+                    if (bd[k] < 0.f) {
+                        D3 ta, tb, tc, o;
+                        int part;
+                        load_tri(tris, ~ref[k], ta, tb, tc, fdummy);
+                        const double d2 = closest_on_triangle(c, ta, tb, tc, o, part);
+                        bd[k] = __double2float_rd(d2);
+                        if (d2 < U2) {
+                            U2 = d2;
+                            best_leaf = ~ref[k];
+                            limf = limit(U2);
+                        }
+                        changed = true;
+                    }
+                    continue;
+                }
                 const NodeV nd = load_node(nodes, ref[k]);
                 float d0, d1;
                 node_child_bounds(nd, qf, d0, d1);
+                if (bd[k] < 0.f) bd[k] = fminf(d0, d1);
                 const bool h0 = d0 <= limf, h1 = d1 <= limf;
                 const int cnt = (int)h0 + (int)h1;
                 if (m - 1 + cnt > kCutK) continue;
@@ -1702,24 +1783,34 @@ __global__ __launch_bounds__(kBlock) void k_cut_build(const BNode* __restrict__ 
                 const int c0 = nd.child(0), c1 = nd.child(1);
                 if (h0) {
                     ref[k] = c0;
-                    bd[k] = d0;
+                    bd[k] = c0 < 0 ? -1.f : d0;  // a leaf gets its exact distance in the next pass
                     if (h1) {
                         ref[m] = c1;
-                        bd[m] = d1;
+                        bd[m] = c1 < 0 ? -1.f : d1;
                         ++m;
                     }
                 } else {
                     ref[k] = c1;
-                    bd[k] = d1;
+                    bd[k] = c1 < 0 ? -1.f : d1;
                 }
             }
             if (!changed || m == 0) break;
         }
-        if (m == 0) {  // cannot happen for a consistent tree (c's own closest face is within R): keep the root
-            m = 1;
-            ref[0] = 0;
-            bd[0] = 0.f;
+        // entries kept under an earlier, larger R that the final one excludes
+        for (int k = 0; k < m;) {
+            if (bd[k] > limf) {
+                ref[k] = ref[m - 1];
+                bd[k] = bd[m - 1];
+                --m;
+            } else {
+                ++k;
+            }
         }
+    }
+    if (m == 0 && !(limf < INFINITY)) {  // no answer for c (cannot happen for a finite mesh): the root
+        ref[0] = 0;
+        bd[0] = 0.f;
+        m = 1;
     }
     for (int k = 1; k < m; ++k)  // nearest first
         for (int j = k; j > 0 && bd[j] < bd[j - 1]; --j) {
@@ -1730,14 +1821,24 @@ __global__ __launch_bounds__(kBlock) void k_cut_build(const BNode* __restrict__ 
             bd[j] = bd[j - 1];
             bd[j - 1] = tb;
         }
-    uint2* out = cut + cell * kCutK;
+    uint32_t* out = rec + cell * kw;
+    out[0] = (uint32_t)best_leaf;
+    if (!E4) out[1] = 0u;
     for (int k = 0; k < kCutK; ++k) {
-        uint2 e = make_uint2(kCutEmpty, 0u);
+        uint32_t ev = 0xFFFFFFFFu, rv = kCutEmpty, bb = 0u;
         if (k < m) {
-            const double sv = sqrt((double)bd[k]) * (1.0 - 1e-5) - r * (1.0 + 1e-5);
-            e = make_uint2((uint32_t)ref[k], __float_as_uint(sv > 0.0 ? __double2float_rd(sv * sv) : 0.f));
+            const double b = bd[k] > 0.f ? (double)bd[k] : 0.0;
+            const double sv = sqrt(b) * (1.0 - 1e-5) - r * (1.0 + 1e-5);
+            bb = __float_as_uint(sv > 0.0 ? __double2float_rd(sv * sv) : 0.f);
+            ev = Ent4::make((uint32_t)ref[k], bb);
+            rv = (uint32_t)ref[k];
         }
-        out[k] = e;
+        if (E4) {
+            out[1 + k] = ev;
+        } else {
+            out[2 + 2 * k] = rv;
+            out[3 + 2 * k] = bb;
+        }
     }
 }
 
@@ -1774,11 +1875,18 @@ int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream
     return MSH_OK;
 }
 
-int cut_build(msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, uint2* d_cut, hipStream_t s) {
+int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const uint32_t* d_prec, const int* d_phint,
+              uint32_t* d_rec, bool e4, hipStream_t s) {
     const size_t n = (size_t)G * G * G;
-    k_cut_build<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(
-        tree->d_nodes, tree->origin[0], tree->origin[1], tree->origin[2], tree_margin(tree->half_diag), G, lo[0], lo[1],
-        lo[2], w[0], w[1], w[2], d_pts, d_cut);
+    const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
+    const TriRec* tris = static_cast<const TriRec*>(tree->d_leaves);
+    const double tm = tree_margin(tree->half_diag);
+    if (e4)
+        k_cut_level<true><<<nb, kBlock, 0, s>>>(tree->d_nodes, tris, tree->origin[0], tree->origin[1], tree->origin[2], tm,
+                                               G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_prec, d_phint, d_rec);
+    else
+        k_cut_level<false><<<nb, kBlock, 0, s>>>(tree->d_nodes, tris, tree->origin[0], tree->origin[1], tree->origin[2], tm,
+                                                G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_prec, d_phint, d_rec);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }

@@ -152,16 +152,13 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
 struct AlongPol {
     const TriRec* __restrict__ tris;
     D3 p, n;      // the rays (p, n) and (p, -n); directions ray_dir(p, +-n) are formed per leaf test
-    RayF rf;      // the line, fp32 model
-    QF qf;        // p for the distance bound
+    RayF rf;      // the line, fp32 model (its parameter is the distance from p: the children's distance bounds)
     double best;  // distance
     uint32_t best_face;
     int best_leaf;  // the hit point is rebuilt from it at the end (hit()), not carried through the walk
     __device__ double lim2() const { return best == INFINITY ? INFINITY : best * best * kSlack; }
     __device__ void children(const NodeV& nd, bool& h0, bool& h1, float& k0, float& k1) const {
-        float s0, s1;
-        ray_child_slabs(nd, rf, h0, h1, s0, s1);
-        node_child_bounds(nd, qf, k0, k1);
+        ray_child_line_dist2(nd, rf, h0, h1, k0, k1);
         const double l = lim2();
         h0 = h0 && (double)k0 <= l;
         h1 = h1 && (double)k1 <= l;
@@ -277,10 +274,14 @@ __device__ inline unsigned dequeue_tile_r(unsigned* counters, unsigned ntiles, u
 
 __device__ inline bool finite_d3(const D3& x) { return isfinite(x.x) && isfinite(x.y) && isfinite(x.z); }
 
-// waves per SIMD: visibility 4 (127 VGPRs, no spills); alongnormal 3 (at 4 the fp64 leaf test spills 37 VGPRs:
-// C5 7.41 vs 6.62 ms)
+// waves per SIMD: visibility 4 (127 VGPRs, no spills); alongnormal 3 (164 VGPRs; at 4 the fp64 leaf test spills 37
+// VGPRs: C5 7.41 vs 6.62 ms in round 2, 5.74 vs 4.98 ms in round 6; one call site of the leaf test for both children
+// and both directions -- a loop -- spilled at 3 waves too: 5.99 ms, profiles/r06_c5_along_ab.jsonl)
+#ifndef MSH_ALONG_WAVES
+#define MSH_ALONG_WAVES 3
+#endif
 template <int MODE, bool STATS>  // MODE 0 alongnormal, 1 visibility
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? 3 : 4))) void k_rays(RayArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? MSH_ALONG_WAVES : 4))) void k_rays(RayArgs a) {
     unsigned n_nodes = 0, n_leaves = 0;
     __shared__ uint2 stk[kStack * kBlock];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -299,8 +300,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
             const D3 p = D3{a.p[3 * i], a.p[3 * i + 1], a.p[3 * i + 2]};
             const D3 n = D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]};
             const D3 dp = ray_dir(p, n), pr = vsub(p, org);
-            AlongPol pol{a.tris, p, n, make_rayf(pr, dp, a.M, true), make_qf(p, a.org, tree_margin(a.M)), INFINITY,
-                         MSH_NO_FACE, -1};
+            AlongPol pol{a.tris, p, n, make_rayf(pr, dp, a.M, true), INFINITY, MSH_NO_FACE, -1};
             if (finite_d3(p) && finite_d3(dp))
                 traverse_rays<AlongPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
             if (STATS) continue;

@@ -20,6 +20,14 @@ for s in $STAGES; do
     bench20) timeout -k 10 600 python bench.py --steps 20 --warmup 3 > gpurun_out/bench20.log 2>&1; ok bench20 $? ;;
     bench_dist)  # the multi-GPU code path at N = 1 (nccl process group, broadcast + unpack, all-gathers, secondaries)
       timeout -k 10 900 python -m torch.distributed.run --nnodes 1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 1 --dist --steps ${DSTEPS:-20} --warmup 3 --no-cpu > gpurun_out/bench_dist.log 2>&1; ok bench_dist $? ;;
+    c5ab)  # C5 ray-kernel A/B over build/variants/*.so in the order ORDER (names), one process per run
+      for n in ${ORDER:?set ORDER}; do
+        MESH_AMD_LIB=$PWD/build/variants/$n.so timeout -k 10 400 python scripts/c5_ab.py --reps ${REPS:-5} ${C5AB_ARGS:-} >> gpurun_out/c5ab.jsonl 2> gpurun_out/c5ab_$n.err; ok c5ab_$n $?
+      done ;;
+    benchab)  # C3 bench.py over build/variants/*.so in the order ORDER (names), one process per run
+      for n in ${ORDER:?set ORDER}; do
+        MESH_AMD_LIB=$PWD/build/variants/$n.so timeout -k 10 400 python bench.py --steps ${BSTEPS:-10} --warmup 2 --no-cpu >> gpurun_out/benchab.jsonl 2> gpurun_out/benchab_$n.err; ok benchab_$n $?
+      done ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; ok smoke $? ;;
     pytest) timeout -k 10 1200 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; ok pytest $? ;;
     bench_small) timeout -k 10 600 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_small.log 2>&1; ok bench_small $? ;;

@@ -51,6 +51,7 @@ int main(int argc, char** argv) {
         }
     };
     long viol = 0, checks = 0, tight = 0, skipped = 0, skipped_anchor = 0, ray_checks = 0, ray_viol = 0, ray_skipped = 0;
+    long line_checks = 0, line_viol = 0, line_tight = 0;
     double worst = 0.0;
     for (long tr = 0; tr < trials; ++tr) {
         // scene scale, node size relative to it, offset of the tree origin
@@ -218,6 +219,24 @@ int main(int argc, char** argv) {
                 float s0, s1;
                 ray_child_slabs(nd, rf, h[0], h[1], s0, s1);
                 ++ray_checks;
+                if (line) {
+                    // nearest_alongnormal's node test (ray_child_line_dist2): the child is taken and its key is at
+                    // most the squared distance from the line's point o to the point x' of the child it passes
+                    bool hl[2];
+                    float kl[2];
+                    ray_child_line_dist2(nd, rf, hl[0], hl[1], kl[0], kl[1]);
+                    const long double dist = fabsl((long double)s) *
+                        sqrtl((long double)d.x * d.x + (long double)d.y * d.y + (long double)d.z * d.z);
+                    ++line_checks;
+                    if (hl[ch] && (long double)kl[ch] > 0.5L * dist * dist) ++line_tight;
+                    if (!hl[ch] || (long double)kl[ch] > dist * dist) {
+                        ++viol;
+                        ++line_viol;
+                        if (line_viol <= 5)
+                            std::fprintf(stderr, "line violation: dk=%d sk=%d hit=%d key=%.9g dist2=%.17Lg s=%g\n", dk, sk,
+                                         (int)hl[ch], kl[ch], dist * dist, s);
+                    }
+                }
                 if (!h[ch]) {
                     ++viol;
                     ++ray_viol;
@@ -278,6 +297,7 @@ int main(int argc, char** argv) {
             }
         }
     }
+    std::printf("line_checks=%ld line_tight=%ld line_violations=%ld\n", line_checks, line_tight, line_viol);
     std::printf("trials=%ld skipped=%ld anchors_skipped=%ld checks=%ld tight=%ld ray_checks=%ld ray_skipped=%ld ray_violations=%ld "
                 "violations=%ld worst_rel=%g\n", trials, skipped, skipped_anchor, checks, tight, ray_checks, ray_skipped, ray_viol,
                 viol, worst);

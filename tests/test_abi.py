@@ -113,13 +113,16 @@ def test_bad_face_index_rejected_before_device():
     assert b"references vertex 7" in L.msh_last_error()
 
 
-@pytest.mark.parametrize("mutation", [None, "MUTATE_TREE_TERM", "MUTATE_QUERY_MARGIN", "MUTATE_RAY_MARGIN"])
+@pytest.mark.parametrize("mutation", [None, "MUTATE_TREE_TERM", "MUTATE_QUERY_MARGIN", "MUTATE_RAY_MARGIN",
+                                      "MUTATE_LINE_DIST"])
 def test_child_box_bound_is_conservative(tmp_path, mutation):
     """The traversal's fp32 child-box bound (common.h node_child_bounds with make_qf's margin) never exceeds
     the squared distance from the fp64 query to a point its box contains, and the ray kernels' fp32 slab
-    test (make_rayf / ray_child_slabs) takes every child a ray passes a point of: 300k random and
-    adversarial nodes/queries/rays on a host build of the kernels' own header.  The mutated builds (one
-    margin term dropped) must find violations, which shows the cases reach the margins."""
+    test (make_rayf / ray_child_slabs) takes every child a ray passes a point of, and nearest_alongnormal's
+    line test (ray_child_line_dist2) takes it with a key at most the squared distance along the line to that
+    point: 300k random and adversarial nodes/queries/rays on a host build of the kernels' own header.  The
+    mutated builds (one margin term dropped; the line key taken from the far end) must find violations, which
+    shows the cases reach the margins."""
     import subprocess
     exe = str(tmp_path / "bound_check")
     cmd = ["/opt/rocm/bin/hipcc", "-O2", "-std=c++17", "-ffp-contract=off", "--offload-arch=gfx950", "-x", "hip",

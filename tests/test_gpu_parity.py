@@ -203,14 +203,18 @@ def _nearest_tree(t, q):
     return face[0], part[0], pt
 
 
-def test_entry_cut_bit_exact(oracle):
-    # C3 mesh: walks from the entry cut (the default grid, a coarse 8^3 one) give the arrays of walks from the
-    # root (msh_tree_set_entry_cut(0)), on uniform queries reaching past the grid (+-1.25 around the unit
-    # sphere), near-surface queries and queries on cell faces of the default grid; 2000 rows match brute force
+def test_entry_cut_bit_exact(oracle, monkeypatch):
+    # C3 mesh: walks from the entry cut give the arrays of walks from the root (msh_tree_set_entry_cut(0)) -- the
+    # default grid (G = 400 = 50 x 2^3: three levels each cut from the coarser one's records, 32-B records of 4-B
+    # entries), a 64^3 grid (8 x 2^3), a one-level 8^3 grid (every centre answered, cut from the root), and the
+    # default grid read by the list path without the node prefetch (8-B stack entries: MESH_AMD_LEAF_LIST=2) --
+    # on uniform queries reaching past the grid (+-1.25 around the unit sphere), near-surface queries and queries on
+    # cell faces of the default grid; 2000 rows match brute force
     from mesh_amd import spatialsearch
     v, f = W.c3_mesh()
     rng = np.random.default_rng(41)
-    G = int(round(np.cbrt(min(64 * f.shape[0], 1 << 26))))  # api.cpp build_entry_cut's automatic grid
+    G = 8 * int(round(np.cbrt(min(64 * f.shape[0], 1 << 26)) / 8))  # api.cpp cut_levels' automatic grid
+    assert G == 400
     lo, w = -1.25, 2.5 / G  # scene box +-1 (icosphere vertices on the unit sphere), widened by 1/4
     on_faces = rng.uniform(-1.2, 1.2, (20_000, 3))
     on_faces[np.arange(20_000), rng.integers(0, 3, 20_000)] = lo + rng.integers(0, G + 1, 20_000) * w
@@ -218,12 +222,17 @@ def test_entry_cut_bit_exact(oracle):
     q = np.concatenate([rng.uniform(-1.4, 1.4, (150_000, 3)), surf, on_faces])
     t = spatialsearch.aabbtree_compute(v, f)
     outs = []
-    for g in (0, -1, 8):
+    for g in (0, -1, 64, 8):
         t.set_entry_cut(g)
         outs.append(_nearest_tree(t, q))
         info = t.entry_cut_info()
         assert info["state"] == ("off" if g == 0 else "built"), info
         assert info["G"] == (0 if g == 0 else (G if g < 0 else g))
+        assert info["bytes"] == info["G"] ** 3 * 32
+    t.set_entry_cut(-1)
+    monkeypatch.setenv("MESH_AMD_LEAF_LIST", "2")
+    outs.append(_nearest_tree(t, q))
+    monkeypatch.delenv("MESH_AMD_LEAF_LIST")
     for o in outs[1:]:
         for a, b in zip(outs[0], o):
             assert np.array_equal(a, b)
@@ -231,6 +240,26 @@ def test_entry_cut_bit_exact(oracle):
     bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[rows])
     assert np.array_equal(outs[1][0][rows], bf) and np.array_equal(outs[1][1][rows], bp)
     assert np.array_equal(outs[1][2][rows], bpt)
+
+
+def test_entry_cut_wide_records():
+    # Trees of more than 2^20 leaves keep 64-B cut records of 8-B entries (the 4-B packing holds 21-bit refs): C5's
+    # 5M-face mesh with one-level (24^3) and three-level (96^3 = 12 x 2^3) grids gives the arrays of walks from the root
+    from mesh_amd import spatialsearch
+    v, f = W.c5_mesh()
+    rng = np.random.default_rng(43)
+    surf, _ = W.surface_samples(v, f, 60_000, seed=44, sigma=0.01)
+    q = np.concatenate([rng.uniform(-1.5, 1.5, (60_000, 3)), surf])
+    t = spatialsearch.aabbtree_compute(v, f)
+    t.set_entry_cut(0)
+    ref = _nearest_tree(t, q)
+    for g in (24, 96):
+        t.set_entry_cut(g)
+        got = _nearest_tree(t, q)
+        info = t.entry_cut_info()
+        assert info["state"] == "built" and info["G"] == g and info["bytes"] == g ** 3 * 64, info
+        for a, b in zip(ref, got):
+            assert np.array_equal(a, b)
 
 
 def test_entry_cut_lazy_and_failure_fallback(oracle):
@@ -250,7 +279,7 @@ def test_entry_cut_lazy_and_failure_fallback(oracle):
     assert t.entry_cut_info()["state"] == "pending" and t.entry_cut_info()["bytes"] == 0
     again = _nearest_tree(t, q)  # 80,000 rows in all: the cut is built by this call
     info = t.entry_cut_info()
-    assert info["state"] == "built" and info["bytes"] == info["G"] ** 3 * 68 and info["build_ms"] > 0
+    assert info["state"] == "built" and info["bytes"] == info["G"] ** 3 * 32 and info["build_ms"] > 0
     for a, b in zip(ref, again):
         assert np.array_equal(a, b)
     t.set_entry_cut(4096)
