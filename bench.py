@@ -247,7 +247,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from mesh_amd import _native, spatialsearch
-    from mesh_amd.distributed import ResultRing, nearest_device, replicate_tree
+    from mesh_amd.distributed import NarrowRing, ResultRing, nearest_device, points_from_faces_device, replicate_tree
     import workloads as W
 
     _native.set_device(local)
@@ -319,6 +319,9 @@ def main():
             el = float(t.item())
         return el
 
+    # the tree answers warmup + steps batches of 100M rows: a kept tree, which asks for the fine entry cut (64 cells per
+    # face) at its first query instead of the coarse one the automatic policy builds first (api.cpp ensure_entry_cut)
+    tree.set_entry_cut(-1)
     for _ in range(args.warmup):  # the first query also builds the tree's entry cut (lazily, once)
         step()
     if ring is not None:
@@ -342,11 +345,47 @@ def main():
     g_ms, g_n = _native.timing_get("gather")
     u_ms, u_n = _native.timing_get("unpermute")
 
-    # ---- N > 1, reported beside value (never as value): the same steps without the exchange, and the
-    # weak-scaling line (every rank answers the whole stream; the world x S answers are all-gathered) ----
-    elapsed_no_ag = elapsed_weak = None
+    # ---- N > 1, reported beside value (never as value): the same steps without the exchange, with the narrow
+    # exchange (faces only, the other ranks' points rebuilt locally: NarrowRing), and the weak-scaling line (every
+    # rank answers the whole stream; the world x S answers are all-gathered) ----
+    elapsed_no_ag = elapsed_weak = elapsed_narrow = None
+    probe = None
     if coll:
         elapsed_no_ag = timed(lambda: answer(slabs[0]), args.steps)
+        if S % world == 0:
+            nring = NarrowRing(tree, q_all, S // world, [slab(S) for _ in range(2)])
+
+            def narrow_step():
+                nring.step(lambda fc, pa, pt: nearest_device(tree, q, fc, pa, pt, stream=stream))
+
+            narrow_step()
+            nring.drain()
+            elapsed_narrow = timed(narrow_step, args.steps, nring)
+            del nring
+            torch.cuda.empty_cache()
+        # the narrow exchange's rebuild on its own: the points and parts of 7/8 of the stream (what a rank of N = 8
+        # rebuilds per step) from (row, face), against this rank's answers of the same rows (N = 1: all of them)
+        if world == 1:
+            m = S - S // 8
+            answer(slabs[0])
+            fc, pa, pt = (x[:m] for x in slabs[0])
+            rp, rpt = torch.empty_like(pa), torch.empty_like(pt)
+            points_from_faces_device(tree, q[:m], fc, rp, rpt, stream=stream)
+            torch.cuda.synchronize()
+            equal = bool(torch.equal(rp, pa) and torch.equal(rpt.view(torch.int64), pt.view(torch.int64)))
+            _native.timing_reset()
+            _native.timing_enable(True)
+            for _ in range(args.steps):
+                points_from_faces_device(tree, q[:m], fc, rp, rpt, stream=stream)
+            torch.cuda.synchronize()
+            _native.timing_enable(False)
+            pms, pn = _native.timing_get("points_from_faces")
+            probe = {"rows": m, "ms": pms / max(pn, 1), "bit_equal_to_traversal": equal,
+                     "bytes_per_row_model": 24 + 4 + 4 + 80 + 24 + 4,
+                     "note": "msh_tree_points_from_faces_device over rows [0, 7/8 S) of the stream (q row + face in, "
+                             "face -> leaf map, the 80-B leaf, point + part out), HIP events on its stream"}
+            del rp, rpt
+            torch.cuda.empty_cache()
         if not args.no_weak:
             del ring, slabs
             torch.cuda.empty_cache()
@@ -363,8 +402,24 @@ def main():
             del wring, wslabs, wg
             torch.cuda.empty_cache()
 
-    sec = None
-    if args.secondary == "on" or (args.secondary == "auto" and coll):
+    # one-shot device caller (untimed for value): a fresh tree from the host mesh, its first 100M-row batch with the
+    # automatic entry cut (the coarse grid, built by that call), results in HBM -- build + cut + batch
+    one_shot = None
+    if world == 1:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        t1 = spatialsearch.aabbtree_compute(v, f)
+        nearest_device(t1, q, slabs[0][0][:S_loc], slabs[0][1][:S_loc], slabs[0][2][:S_loc], stream=stream)
+        torch.cuda.synchronize()
+        el1 = time.perf_counter() - t0
+        c1 = t1.entry_cut_info()
+        one_shot = {"ms": el1 * 1e3, "queries_per_s": S_loc / el1, "build_ms": t1.info().build_ms,
+                    "entry_cut": {"G": c1["G"], "bytes": c1["bytes"], "build_ms": c1["build_ms"]},
+                    "note": "wall time of aabbtree_compute (host mesh in) + one %d-row nearest_device call on the fresh "
+                            "tree (its automatic entry cut built by that call), inputs and outputs in HBM" % S_loc}
+        t1.free()
+        del t1
+
         sec = secondary(timed, world, rank, dev, args.steps, coll)
 
     # ---- instrumented traversal (untimed): algorithmic bytes of this rank's shard ----
@@ -462,6 +517,14 @@ def main():
         out["value_without_allgather"] = total_q / elapsed_no_ag
         out["ms_per_step_without_allgather"] = elapsed_no_ag / args.steps * 1e3
         out["allgather_bytes_per_step"] = world * rows * 32  # (face u32, part u32, point 3 x f64) of every shard
+    if elapsed_narrow is not None:
+        out["value_narrow_exchange"] = total_q / elapsed_narrow
+        out["ms_per_step_narrow_exchange"] = elapsed_narrow / args.steps * 1e3
+        out["narrow_exchange_bytes_per_step"] = S * 4  # the face array, all-gathered in place
+    if probe is not None:
+        out["narrow_rebuild_probe"] = probe
+    if one_shot is not None:
+        out["one_shot"] = one_shot
     if elapsed_weak is not None:
         out["value_weak_100M_per_gpu"] = world * S * args.steps / elapsed_weak
         out["ms_per_step_weak"] = elapsed_weak / args.steps * 1e3

@@ -136,6 +136,15 @@ int msh_tree_nearest_bary(msh_tree* tree, const double* q, size_t S, uint32_t* f
 int msh_tree_nearest_bary_device(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_face, double* d_pt,
                                  double* d_w, void* stream);
 
+/* The closest point (and part code) of each row q[i] on a GIVEN face face[i] -- the construction msh_tree_nearest
+ * stores for the face it finds (CGAL's closest point on the triangle, spatialsearchmodule.cpp:129-140 /
+ * nearest_point_triangle_3.h:22-154), so for rows answered with face f it reproduces the answer's point and part bit
+ * for bit.  face MSH_NO_FACE (or >= T): point NaN, part 0.  The narrow multi-GPU result exchange
+ * (mesh_amd/distributed.py NarrowRing) all-gathers faces only (4 B per row instead of 32) and rebuilds the other
+ * ranks' points with it.  Device pointers; asynchronous on `stream`; part may be NULL. */
+int msh_tree_points_from_faces_device(msh_tree* tree, const double* d_q, size_t S, const uint32_t* d_face,
+                                      uint32_t* d_part, double* d_pt, void* stream);
+
 /* The order in which the closest-point path visits the S query rows (d_perm[slot] = row): stable by the
  * Hilbert index of each row's cell in a 256^3 grid over the tree's scene box widened by 10 % per side (the cell is
  * the top 24 bits of the row's 30-bit Morton code, mapped to the Hilbert curve of the same cells; then 3 LDS radix

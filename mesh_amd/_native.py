@@ -46,6 +46,7 @@ SIGNATURES = [
     ("msh_tree_nearest_stats", _i, [_vp, _vp, _sz, _c_u64_p, _c_u64_p]),
     ("msh_tree_nearest_bary", _i, [_vp, _c_double_p, _sz, _c_u32_p, _c_double_p, _c_double_p]),
     ("msh_tree_nearest_bary_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
+    ("msh_tree_points_from_faces_device", _i, [_vp, _vp, _sz, _vp, _vp, _vp, _vp]),
     ("msh_tree_set_entry_cut", _i, [_vp, _i]),
     ("msh_tree_query_order", _i, [_vp, _vp, _sz, _vp, _vp]),
     ("msh_tree_entry_cut_info", _i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i), _c_u64_p, ctypes.POINTER(ctypes.c_double)]),

@@ -431,6 +431,7 @@ static void free_tree(msh_tree* t) {
     if (t->d_vorder) (void)dfree(t->d_vorder);
     if (t->d_vorder_shard) (void)dfree(t->d_vorder_shard);
     if (t->d_cut) (void)dfree(t->d_cut);
+    if (t->d_face_leaf) (void)dfree(t->d_face_leaf);
     for (int b = 0; b < 3; ++b) {
         if (b < 2 && t->h_stage[b]) (void)hipHostFree(t->h_stage[b]);
         if (t->d_stage[b]) (void)dfree(t->d_stage[b]);
@@ -508,49 +509,54 @@ static void free_entry_cut(msh_tree* t) {
     t->cut_ms = 0.0;
 }
 
-// cells per leaf and the cap of the automatic grid, C3 (1,003,520 faces) in M q/s, round 5 (8 entries + hint per
-// 68-B cell): 8 per leaf, 2^23 cells: G = 200, 46.9 node visits per query, 2156-2213; 16, 2^25: G = 252, 45.2 visits,
-// 2238; 32, 2^25: G = 318, 43.6 visits, 2247-2290 (profiles/r05_ab_noleaders_cut.jsonl); in another session 32:
-// 2261-2286, 64, 2^26: G = 400, 42.2 visits, 2293-2321, 128, 2^27: G = 505, 41.0 visits, 2297-2333
-// (profiles/r05_ab_cut_size.jsonl).  The grid is derived data of a kept tree: 64 per leaf, 32-B records (C3: 2.05 GB).
+// The automatic grid comes in two sizes (round 6).  A coarse grid, 8 cells per leaf (at most 2^23 cells; C3: G = 200,
+// 256 MB), is built by the call that brings the handle's rows to 1/16 of its cells (C3: 500k rows); it costs a
+// one-shot caller ~10 ms.  The fine grid, 64 cells per leaf (at most 2^26; C3: G = 400, 2.05 GB), replaces it once the
+// handle has answered kFineRowsPerCell rows per fine cell (C3: ~1G rows): its ~70-ms build pays back after that many
+// queries (C3 100M-query batches: ~3 ms faster each than with the coarse grid).  msh_tree_set_entry_cut(t, -1) asks
+// for the fine grid at the next call (a caller that keeps the tree for many batches, as bench.py does).
+// Round-5 figures (68-B cells of 8 entries and a separate hint), C3 in M q/s: 8 per leaf, 2^23 cells: G = 200, 46.9
+// node visits per query, 2156-2213; 16, 2^25: G = 252, 45.2 visits, 2238; 32, 2^25: G = 318, 43.6 visits, 2247-2290
+// (profiles/r05_ab_noleaders_cut.jsonl); in another session 32: 2261-2286, 64, 2^26: G = 400, 42.2 visits,
+// 2293-2321, 128, 2^27: G = 505, 41.0 visits, 2297-2333 (profiles/r05_ab_cut_size.jsonl).  Round 6's 32-B records of
+// 7 entries at G = 400: 42.5 visits, 2322-2363 against 2301-2351 for the 68-B cells in one session
+// (profiles/r06_c3_cut_levels_ab.jsonl).
 #ifndef MSH_CUT_PER_LEAF
 #define MSH_CUT_PER_LEAF 64
 #endif
 #ifndef MSH_CUT_MAX_LOG2
 #define MSH_CUT_MAX_LOG2 26
 #endif
-static size_t auto_cut_cells(const msh_tree* t) {
-    return std::min<size_t>((size_t)MSH_CUT_PER_LEAF * t->T, (size_t)1 << MSH_CUT_MAX_LOG2);
+constexpr size_t kCutCoarsePerLeaf = 8;
+constexpr int kCutCoarseMaxLog2 = 23;
+constexpr size_t kFineRowsPerCell = 16;
+static size_t auto_cut_cells(const msh_tree* t, bool fine) {
+    return fine ? std::min<size_t>((size_t)MSH_CUT_PER_LEAF * t->T, (size_t)1 << MSH_CUT_MAX_LOG2)
+                : std::min<size_t>(kCutCoarsePerLeaf * t->T, (size_t)1 << kCutCoarseMaxLog2);
 }
 // record bytes per cell: 32 (4-B entries) for trees of <= 2^20 leaves, else 64
 static size_t cut_rec_bytes(const msh_tree* t) { return t->T <= kEnt4MaxLeaves ? 32 : 64; }
 
-// Grid of the cut and its levels: G = G0 2^L.  The coarsest grid's cell centres are answered exactly by the tree
-// (G0^3 queries) and cut from the root; each finer level starts every cell from the record of the coarser cell
-// that contains it (nearest.hip k_cut_level), so no level walks from the root and only G0^3 centres are traversed.
-// The automatic grid takes L = 3 (C3: G0 = 50, G = 400); an explicit G takes the largest L <= 3 with G0 = G / 2^L
-// an integer >= 8 (L = 0: one level, every centre answered, as round 5 built every grid).
-static void cut_levels(const msh_tree* t, int* G, int* L) {
-    if (t->cut_req > 0) {
-        *G = t->cut_req;
-        *L = 0;
-        while (*L < 3 && (*G % (2 << *L)) == 0 && (*G >> (*L + 1)) >= 8) ++*L;
-        return;
-    }
-    const double g = std::cbrt((double)auto_cut_cells(t));
-    const int g0 = (int)std::lround(g / 8.0);
-    if (g0 >= 8) {
-        *G = 8 * g0;
-        *L = 3;
-    } else {
-        *G = std::max(16, (int)std::lround(g));
-        *L = 0;
-    }
+// cells per axis of the grid to build: the caller's G, else the automatic fine or coarse grid
+static int cut_grid(const msh_tree* t, bool fine) {
+    if (t->cut_req > 0) return t->cut_req;
+    return std::max(16, (int)std::lround(std::cbrt((double)auto_cut_cells(t, fine))));
 }
 
-static int build_entry_cut(msh_tree* t) {
-    int G = 0, L = 0;
-    cut_levels(t, &G, &L);
+// The grid's cell centres are answered exactly by the tree (walks from the root: no cut is installed while one is
+// built), then every cell is cut from the root (nearest.hip k_cut_level).  Round 6 also tried a pyramid -- the
+// coarsest grid answered exactly, each finer level cut from the coarser one's records with hints taken from the 8
+// coarse cells around it -- which built C3's grid in 41 ms instead of ~70 but started queries from worse hints:
+// 49.4 node visits per query against 42.5, 2.02-2.06 G q/s against 2.32-2.36 (profiles/r06_c3_cut_levels_ab.jsonl).
+#ifndef MSH_CUT_CENTRE_STEPS
+#define MSH_CUT_CENTRE_STEPS 128
+#endif
+constexpr unsigned kCutCentreSteps = MSH_CUT_CENTRE_STEPS;
+}  // namespace msh
+static int nearest_run(msh_tree* t, const double* d_q, size_t S, const msh::SlotOut& o, hipStream_t s, unsigned stop_at);
+namespace msh {
+static int build_entry_cut(msh_tree* t, bool fine) {
+    const int G = cut_grid(t, fine);
     double half[3], H = 0.0, lo[3], w[3];
     for (int k = 0; k < 3; ++k) {
         half[k] = 0.5 * ((double)t->scene_hi[k] - (double)t->scene_lo[k]);
@@ -560,13 +566,11 @@ static int build_entry_cut(msh_tree* t) {
         set_error("entry cut: degenerate scene box");
         return MSH_EINVAL;
     }
-    double ext[3];
     for (int k = 0; k < 3; ++k) {
         const double m = 0.5 * ((double)t->scene_hi[k] + (double)t->scene_lo[k]);
         const double e = 1.25 * std::max(half[k], 0.05 * H);
         lo[k] = m - e;
-        ext[k] = 2.0 * e;
-        w[k] = ext[k] / G;
+        w[k] = 2.0 * e / G;
     }
     const size_t n = (size_t)G * G * G;
     if (n > 0xFFFFFFFFull) {
@@ -587,46 +591,30 @@ static int build_entry_cut(msh_tree* t) {
     uint32_t* cut = nullptr;
     int st = MSH_OK;
     {
-        // level 0: the G0^3 centres answered exactly (walks from the root: no cut is installed while it is built)
-        const int G0 = G >> L;
-        const size_t n0 = (size_t)G0 * G0 * G0;
-        double w0[3] = {ext[0] / G0, ext[1] / G0, ext[2] / G0};
-        DevBuf dq, df, dp, dinv, dhint, prev, cur;
+        DevBuf dq, df, dp, dinv, dhint;
         do {
-            if ((st = dq.reserve(n0 * 3 * sizeof(double))) != MSH_OK) break;
-            if ((st = df.reserve(n0 * sizeof(uint32_t))) != MSH_OK) break;
-            if ((st = dp.reserve(n0 * 3 * sizeof(double))) != MSH_OK) break;
-            if ((st = dhint.reserve(n0 * sizeof(int))) != MSH_OK) break;
+            if ((st = dq.reserve(n * 3 * sizeof(double))) != MSH_OK) break;
+            if ((st = df.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
+            if ((st = dp.reserve(n * 3 * sizeof(double))) != MSH_OK) break;
+            if ((st = dhint.reserve(n * sizeof(int))) != MSH_OK) break;
             if ((st = dinv.reserve(t->T * sizeof(uint32_t))) != MSH_OK) break;
-            if ((st = cut_centres(G0, lo, w0, dq.as<double>(), s)) != MSH_OK) break;
-            if ((st = msh_tree_nearest_device(t, dq.as<double>(), n0, df.as<uint32_t>(), nullptr, dp.as<double>(), s)) !=
-                MSH_OK)
+            if ((st = cut_centres(G, lo, w, dq.as<double>(), s)) != MSH_OK) break;
+            // the centres' walks stop after kCutCentreSteps node steps with their best face so far: U(c) is then an
+            // upper bound of d(c) and the hint a real candidate, which is all the cut needs (centres deep inside a
+            // closed surface, equidistant from much of it, no longer walk for thousands of steps or take pass 2)
+            if ((st = ::nearest_run(t, dq.as<double>(), n, SlotOut{df.as<uint32_t>(), nullptr, dp.as<double>(), nullptr,
+                                                              nullptr}, s, kCutCentreSteps)) != MSH_OK)
                 break;
-            if ((st = cut_hints(t, df.as<uint32_t>(), n0, dinv.as<uint32_t>(), dhint.as<int>(), s)) != MSH_OK) break;
-            // levels 0 .. L: records of the G0 2^l grid; the last one is the cut
-            const uint32_t* parent = nullptr;
-            for (int l = 0; l <= L && st == MSH_OK; ++l) {
-                const int Gl = G0 << l;
-                const size_t nl = (size_t)Gl * Gl * Gl;
-                const double wl[3] = {ext[0] / Gl, ext[1] / Gl, ext[2] / Gl};
-                uint32_t* out = nullptr;
-                if (l == L) {
-                    e = dmalloc(&cut, nl * rb);
-                    if (e != hipSuccess) {
-                        set_error("hipMalloc entry cut (%zu cells): %s", nl, hipGetErrorString(e));
-                        st = MSH_ENOMEM;
-                        break;
-                    }
-                    out = cut;
-                } else {
-                    if ((st = cur.reserve(nl * rb)) != MSH_OK) break;
-                    out = cur.as<uint32_t>();
-                }
-                st = cut_level(t, Gl, lo, wl, parent, l == 0 ? dhint.as<int>() : nullptr, out, e4, s);
-                parent = out;
-                std::swap(prev, cur);  // this level's records become the next level's parents
+            if ((st = cut_hints(t, df.as<uint32_t>(), n, dinv.as<uint32_t>(), dhint.as<int>(), s)) != MSH_OK) break;
+            dq.release();  // the centres' rows and points are not needed by the cut itself
+            dp.release();
+            e = dmalloc(&cut, n * rb);
+            if (e != hipSuccess) {
+                set_error("hipMalloc entry cut (%zu cells): %s", n, hipGetErrorString(e));
+                st = MSH_ENOMEM;
+                break;
             }
-            if (st != MSH_OK) break;
+            if ((st = cut_level(t, G, lo, w, dhint.as<int>(), cut, e4, s)) != MSH_OK) break;
             (void)hipEventRecord(e1, s);
             if ((e = hipStreamSynchronize(s)) != hipSuccess) {
                 set_error("entry cut build: %s", hipGetErrorString(e));
@@ -654,35 +642,74 @@ static int build_entry_cut(msh_tree* t) {
     return st;
 }
 
-// Closest-point call of S rows on a handle whose cut is pending: build it -- the automatic grid only once the handle
-// has answered at least one row per kCutAutoCellsPerRow cells (C3: 4.2M rows for G = 400's 64M cells; C2 55k), so a
-// few small calls on a large mesh walk from the root instead of paying ~64 ms and 4.4 GB (+3.4 GB of temporaries)
-// on their first call; after msh_tree_set_entry_cut, at the next call.  The cut is an optimisation, so a failure
-// (device memory, most likely) is not the query's: the partial buffers are freed, the error is cleared, the handle
-// remembers the failure and its queries start at the root.
+// Closest-point call of S rows: settle the handle's cut first.  The automatic policy (above auto_cut_cells): the
+// coarse grid once the handle has answered one row per kCutAutoCellsPerRow of its cells (C3: 500k rows; a few small
+// calls on a large mesh walk from the root instead of paying for it), the fine grid once it has answered
+// kFineRowsPerCell rows per fine cell; after msh_tree_set_entry_cut, the grid asked for at the next call.  The cut is
+// an optimisation, so a failure (device memory, most likely) is not the query's: the partial buffers are freed, the
+// error is cleared and queries start at the root (or from the coarse grid, if the fine one failed).
 constexpr size_t kCutAutoCellsPerRow = 16;
 static void ensure_entry_cut(msh_tree* t, size_t S) {
-    if (t->cut_state != kCutPending) return;
+    if (t->cut_state == kCutOff || t->cut_state == kCutFailed) return;
     if (!cut_applies(t)) {
-        t->cut_state = kCutOff;
+        if (t->cut_state == kCutPending) t->cut_state = kCutOff;
         return;
     }
-    if (!t->cut_force && t->cut_req < 0) {
+    const bool automatic = !t->cut_force && t->cut_req < 0;
+    bool fine = t->cut_req < 0;  // an automatic request: the fine grid (explicit -1, or the volume reached)
+    if (automatic) {
         t->cut_rows += S;
-        if (t->cut_rows * kCutAutoCellsPerRow < auto_cut_cells(t)) return;
+        const size_t coarse_rows = auto_cut_cells(t, false) / kCutAutoCellsPerRow;
+        const size_t fine_rows = auto_cut_cells(t, true) * kFineRowsPerCell;
+        if (t->cut_state == kCutBuilt) {  // a coarse grid: upgrade once the volume pays for the fine one
+            if (t->cut_fine || t->cut_rows < fine_rows) return;
+        } else if (t->cut_rows < coarse_rows) {
+            return;
+        }
+        fine = t->cut_rows >= fine_rows;
+    } else if (t->cut_state == kCutBuilt) {
+        return;
     }
-    t->cut_state = kCutOff;  // while it is built: the cell-centre queries start at the root
     const std::string keep = g_err;
-    const int st = build_entry_cut(t);
+    // while a grid is built, the cell-centre queries walk from the root (an installed coarse grid stays meanwhile
+    // out of use: its walks would give the same answers; the build's own queries must not rebuild it)
+    uint32_t* old = t->d_cut;
+    const int old_G = t->cut_G, old_wide = t->cut_wide;
+    const double old_ms = t->cut_ms;
+    double old_lo[3], old_iw[3];
+    for (int k = 0; k < 3; ++k) {
+        old_lo[k] = t->cut_lo[k];
+        old_iw[k] = t->cut_iw[k];
+    }
+    t->d_cut = nullptr;
+    t->cut_state = kCutOff;
+    const int st = build_entry_cut(t, fine);
     if (st == MSH_OK) {
+        if (old) {
+            if (t->ws_done) (void)hipEventSynchronize(t->ws_done);
+            (void)dfree(old);
+        }
         t->cut_state = kCutBuilt;
+        t->cut_fine = fine;
     } else {
         (void)hipGetLastError();  // clear a sticky launch / allocation error of the failed build
-        // an automatic grid is tried again after another threshold of rows (memory may have been freed by then),
-        // at most twice; a grid the caller asked for fails at once (msh_tree_set_entry_cut re-arms it)
-        const bool automatic = !t->cut_force && t->cut_req < 0;
-        t->cut_state = automatic && ++t->cut_fails <= 2 ? kCutPending : kCutFailed;
-        t->cut_rows = 0;
+        if (old) {  // a failed upgrade keeps the coarse grid
+            t->d_cut = old;
+            t->cut_G = old_G;
+            t->cut_wide = old_wide;
+            t->cut_ms = old_ms;
+            for (int k = 0; k < 3; ++k) {
+                t->cut_lo[k] = old_lo[k];
+                t->cut_iw[k] = old_iw[k];
+            }
+            t->cut_state = kCutBuilt;
+            t->cut_fine = true;  // no second try
+        } else {
+            // an automatic grid is tried again after another threshold of rows (memory may have been freed by then),
+            // at most twice; a grid the caller asked for fails at once (msh_tree_set_entry_cut re-arms it)
+            t->cut_state = automatic && ++t->cut_fails <= 2 ? kCutPending : kCutFailed;
+            t->cut_rows = 0;
+        }
     }
     g_err = keep;
 }
@@ -1708,8 +1735,10 @@ int msh_tree_set_entry_cut(msh_tree* t, int G) {
     if (G > 4096) { set_error("msh_tree_set_entry_cut: G = %d cells per axis (at most 4096)", G); return MSH_EINVAL; }
     const int want = G < 0 ? -1 : G;
     for (msh_tree* r : t->replicas) MSH_TRY(msh_tree_set_entry_cut(r, G));
-    if (want == t->cut_req && t->cut_state != kCutFailed) {
-        t->cut_force = true;  // a pending grid is built by the next call whatever its size
+    // the same grid again: a pending grid is built by the next call whatever its size (an automatic request on a
+    // handle holding the coarse automatic grid asks for the fine one, below)
+    if (want == t->cut_req && t->cut_state != kCutFailed && !(want < 0 && t->cut_state == kCutBuilt && !t->cut_fine)) {
+        t->cut_force = true;
         return MSH_OK;
     }
     free_entry_cut(t);
@@ -1763,11 +1792,11 @@ int msh_tree_get_info(const msh_tree* t, msh_tree_info* info) {
 
 // ---------------------------------------------------------------------------------------------
 // one sorted closest-point launch over d_q (validated; the entry cut already settled by the caller)
-static int nearest_run(msh_tree* t, const double* d_q, size_t S, const SlotOut& o, hipStream_t s) {
+static int nearest_run(msh_tree* t, const double* d_q, size_t S, const SlotOut& o, hipStream_t s, unsigned stop_at = 0) {
     WsOrder order(t, s);
     QueryOrder ord;
     MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord, true));
-    return launch_nearest(t, ord, S, o, s);
+    return launch_nearest(t, ord, S, o, s, stop_at);
 }
 
 int msh_tree_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part, double* d_pt,
@@ -1778,6 +1807,30 @@ int msh_tree_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* 
     if (!d_q || !d_face || !d_pt) { set_error("msh_tree_nearest_device: null argument"); return MSH_EINVAL; }
     ensure_entry_cut(t, S);
     return nearest_run(t, d_q, S, SlotOut{d_face, d_part, d_pt, nullptr, nullptr}, pick(t, stream));
+}
+
+int msh_tree_points_from_faces_device(msh_tree* t, const double* d_q, size_t S, const uint32_t* d_face, uint32_t* d_part,
+                                      double* d_pt, void* stream) {
+    MSH_TRY(check_tree(t, kTriangles, "msh_tree_points_from_faces_device"));
+    MSH_TRY(check_count(S, "msh_tree_points_from_faces_device"));
+    if (S == 0) return MSH_OK;
+    if (!d_q || !d_face || !d_pt) { set_error("msh_tree_points_from_faces_device: null argument"); return MSH_EINVAL; }
+    hipStream_t s = pick(t, stream);
+    if (!t->d_face_leaf) {
+        uint32_t* inv = nullptr;
+        MSH_HIP(dmalloc(&inv, t->T * sizeof(uint32_t)));
+        const int st = face_leaf_map(t, inv, s);
+        if (st != MSH_OK) {
+            (void)hipStreamSynchronize(s);
+            (void)dfree(inv);
+            return st;
+        }
+        MSH_HIP(hipStreamSynchronize(s));  // the map is complete before any stream reads it
+        t->d_face_leaf = inv;
+    }
+    // no workspace is used (tree leaves and the map only), so no WsOrder: a rebuild of other ranks' points on a side
+    // stream overlaps the next batch's traversal
+    return points_from_faces(t, t->d_face_leaf, d_q, S, d_face, d_part, d_pt, s);
 }
 
 int msh_tree_nearest_bary_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, double* d_pt, double* d_w,

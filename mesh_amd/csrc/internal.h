@@ -156,6 +156,7 @@ struct msh_tree {
     // (cut_wide) --; d_cut == nullptr: every query starts at the root
     uint32_t* d_cut = nullptr;
     int cut_wide = 0;
+    uint32_t* d_face_leaf = nullptr;  // face -> leaf (msh_tree_points_from_faces_device; built on first use)
     int cut_G = 0;
     // lazily built on the first closest-point query (msh_tree_set_entry_cut): requested grid (< 0 automatic,
     // 0 off), state (0 pending, 1 built, 2 off / not applicable, 3 failed), GPU build time
@@ -164,6 +165,7 @@ struct msh_tree {
     bool cut_force = false;   // msh_tree_set_entry_cut was called: build at the next query, whatever its size
     uint64_t cut_rows = 0;    // closest-point rows answered while the automatic cut waits (ensure_entry_cut)
     int cut_fails = 0;        // failed automatic builds (retried after another threshold of rows, at most twice)
+    bool cut_fine = false;    // the built grid is the fine automatic one (or a requested one): no upgrade
     double cut_ms = 0.0;
     double cut_lo[3] = {0, 0, 0}, cut_iw[3] = {0, 0, 0};
     msh::Workspace ws;
@@ -235,20 +237,27 @@ int gather_rows(const double* d_a, const double* d_b, const uint32_t* d_perm, si
 // caller row j <- slot inv[j] (record fields + nw doubles per row from d_w)
 int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32_t* d_inv, size_t S, const SlotOut& o,
                       hipStream_t s);
-// Entry cut of a single triangle tree, level by level (nearest.hip k_cut_level): the records of a G^3 grid from the
-// records of the G/2 grid (d_prec), or on the coarsest level from the root with the hint leaves d_phint of the
-// cell centres' exact answers; e4: 32-B records of 4-B entries (trees of <= 2^20 leaves), else 64-B records.
-// kCutK start entries per cell (the hint takes the record's eighth word; 8 entries of 8 B + a separate hint in
-// round 5; 4: 1773-1800 M q/s against 8, 16: 1285, C3, profiles/r03_c3_entry_cut_ab.jsonl)
+// Entry cut of a single triangle tree (nearest.hip k_cut_level): the records of a G^3 grid from the hint leaves d_hint
+// of the cell centres' exact answers; e4: 32-B records of 4-B entries (trees of <= 2^20 leaves), else 64-B records.
+// kCutK start entries per cell (the hint takes the record's eighth word; round 5: 8 entries of 8 B + a separate hint;
+// 4 entries: 1773-1800 M q/s against 8, 16: 1285, C3, profiles/r03_c3_entry_cut_ab.jsonl)
 constexpr int kCutK = 7;
 constexpr size_t kEnt4MaxLeaves = (size_t)1 << 20;  // 4-B stack / cut entries: refs in [-2^20, 2^20), 21 bits
 int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s);
-int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const uint32_t* d_prec, const int* d_phint,
-              uint32_t* d_rec, bool e4, hipStream_t s);
+int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const int* d_hint, uint32_t* d_rec, bool e4,
+              hipStream_t s);
+// d_inv[face] = the leaf holding it (T words)
+int face_leaf_map(const msh_tree* tree, uint32_t* d_inv, hipStream_t s);
+// closest point (and part) of each row q[i] on face d_face[i] (the traversal's answer construction); d_inv from
+// face_leaf_map
+int points_from_faces(const msh_tree* tree, const uint32_t* d_inv, const double* d_q, size_t S, const uint32_t* d_face,
+                      uint32_t* d_part, double* d_pt, hipStream_t s);
 // d_hint[cell] = the leaf holding face d_face[cell] (d_inv: T scratch words)
 int cut_hints(const msh_tree* tree, const uint32_t* d_face, size_t n, uint32_t* d_inv, int* d_hint, hipStream_t s);
 // closest point: o.face, o.part (nullable), o.pt; with o.w (3 per row) the barycentric variant (part unused)
-int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s);
+// stop_at > 0: every query stops after that many node steps with its best so far (no pass 2; any face is an answer)
+int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s,
+                   unsigned stop_at = 0);
 // batched trees: n = (meshes) * S queries, slot i answered on mesh mesh0 + i / S (the batched sort is mesh-major)
 int launch_nearest_batch(const msh_tree* tree, const QueryOrder& ord, size_t n, size_t S, const SlotOut& o,
                          hipStream_t s, size_t mesh0 = 0);

@@ -89,6 +89,9 @@ struct KnnArgs {
     int spill_depth;
     unsigned long long* stats;
     unsigned budget;
+    // > 0: a lane stops after this many node steps with its best so far as its answer, and there is no pass 2 (the
+    // entry cut's cell centres: any face is a valid upper bound there, build_entry_cut)
+    unsigned stop_at;
     // leader / follower ordering (sorted closest-point launches, MODE 0 and 3): phase 0 = every slot,
     // unhinted; phase 1 = leader slots (i % kLead == 0); phase 2 = the other slots, each starting from the
     // leaf of the nearest leader's closest point in its 64-slot window (see leader_leaf)
@@ -842,12 +845,16 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 // records are written after the tile's loop, so the loop holds no copy of the construction
                 if (want_defer && nq == 0) {
                     want_defer = false;
-                    dslot = atomicAdd(a.n_deferred, 1u);
-                    if (dslot < a.max_deferred) {
-                        active = false;
-                        deferred = true;
+                    if (a.stop_at) {
+                        active = false;  // answered with its best so far
+                    } else {
+                        dslot = atomicAdd(a.n_deferred, 1u);
+                        if (dslot < a.max_deferred) {
+                            active = false;
+                            deferred = true;
+                        }
+                        // deferred list full: finish here without a budget
                     }
-                    // deferred list full: finish here without a budget
                 }
                 const bool can = active && !want_defer && nq < kPend;
                 const bool any = __ballot(can) != 0ull;
@@ -1068,7 +1075,11 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     ++steps;
                     if (STATS) ++tot;
                     if (active && steps >= max_steps) active = false;  // each node is entered once: corrupt tree
-                    if (active && steps == a.budget) {
+                    if (active && steps == a.budget && a.stop_at) {
+                        if (STATS) n_leaves += nq;
+                        test_queue(kLeafQ);
+                        active = false;  // answered with its best so far
+                    } else if (active && steps == a.budget) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
                         if (slot < a.max_deferred) {
                             if (STATS) n_leaves += nq;
@@ -1488,6 +1499,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         // wave-cooperative pass 2 instead of holding its tile for up to T serial steps (C1, 840 faces:
         // traversal 1.15 -> 0.56 ms; with no leader phases below, 0.29 ms)
         a.budget = std::min<unsigned>(a.budget, (unsigned)std::max<size_t>(64, a.T / 16));
+        if (a.stop_at) a.budget = a.stop_at;
         a.nunits = nunits;
         a.ntiles = (unsigned)((nunits + 63) / 64);
         const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, ncu * kKnnBlocksPerCU);
@@ -1528,7 +1540,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
                 MSH_TRY(pass1(0, a.S, STATS ? "knn_all_stats" : "knn_all"));
             }
         }
-        {
+        if (!a.stop_at) {
             TimedLaunch t2(STATS ? "knn_pass2_stats" : "knn_pass2", s);
             k_knn_coop<MODE, STATS><<<nblk2, kBlock, 0, s>>>(a);
             MSH_HIP(hipGetLastError());
@@ -1601,9 +1613,11 @@ static void cut_args(const msh_tree* tree, KnnArgs& a) {
     }
 }
 
-int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s) {
+int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s,
+                   unsigned stop_at) {
     KnnArgs a = tree_args(tree, S);
     cut_args(tree, a);
+    a.stop_at = stop_at;
     SlotOut oo = o;
     oo.dist = nullptr;
     if (o.w) {
@@ -1669,30 +1683,23 @@ __global__ __launch_bounds__(kBlock) void k_cut_centres(int G, double lx, double
     q[3 * cell + 2] = lz + ((double)iz + 0.5) * wz;
 }
 
-// One level of the entry cut, one thread per cell of a G^3 grid (cell (ix, iy, iz) = row (iz G + iy) G + ix).  The
-// cell starts from its parent's record -- the cell of the G/2 grid that contains it (G even) -- or, on the
-// coarsest level (prec == nullptr), from the root with the hint leaf phint[cell] of its centre's exact closest face.
-//   U(c) = the exact distance from the centre c to the best leaf seen: first the parent's hint leaf, then every
-//   leaf the expansion meets (CGAL's fp64 construction, as a query's leaf test).  R = (U(c) + 2r) (1 + 1e-6), r
-//   the cell's half-diagonal + 0.1 %.  For q in the cell, d(q) <= U(c) + r, so a subtree farther than R from c
-//   holds neither q's answer nor a tie.  The parent's entries cover every subtree within R_p of c_p, and R +
-//   |c - c_p| <= R_p (U(c) <= U(c_p) + |c - c_p|, |c - c_p| <= r = r_p / 2), so they cover the child's.
-//   Entries (internal nodes or ~leaves) are replaced by their children whose bound from c is within R, in passes
-//   over the list, while it keeps at most kCutK entries; a child outside R is dropped (the cull is the
-//   traversal's own: bound > fp32(R^2 (1 + 2^-40)) rounded up).  An entry's bound from c: its box bound when its
-//   parent node was expanded here, the smaller of its children's bounds when its own node was loaded, the exact
-//   squared distance for a leaf -- each a lower bound of the squared distance from c to what it holds.
-// Out (E4: 32-B records of 4-B entries, trees of <= 2^20 leaves; else 64-B records of (ref, bound bits)): word 0
-// the best leaf (the hint of unhinted slots), then the entries nearest-first with max(s, 0)^2 rounded down to
-// fp32, s = sqrt(bound) (1 - 1e-5) - r (1 + 1e-5): a lower bound of the squared distance from any q of the cell.
-// Round 5 answered every cell centre of the final grid exactly (64M traversals on C3) and cut each cell from the
-// root: 65 ms and 4.4 GB of 68-B cells, against a few ms per level and 2.05 GB here.
+// The entry cut, one thread per cell of a G^3 grid (cell (ix, iy, iz) = row (iz G + iy) G + ix), from the root, with
+// U(c) = the exact distance from the centre c to its closest face (hint[cell], from the centre's own query).
+// R = (U(c) + 2r) (1 + 1e-6), r the cell's half-diagonal + 0.1 %.  For q in the cell, d(q) <= U(c) + r, so a subtree
+// farther than R from c holds neither q's answer nor a tie.  Entries (internal nodes or ~leaves) are replaced by their
+// children whose bound from c is within R, in passes over the list, while it keeps at most kCutK entries; a child
+// outside R is dropped (the cull is the traversal's own: bound > fp32(R^2 (1 + 2^-40)) rounded up).  An entry's bound
+// from c: its box bound when its parent node was expanded, raised to the smaller of its children's bounds when its own
+// node is loaded, the exact squared distance for a leaf -- each a lower bound of the squared distance from c to what
+// it holds.
+// Out (E4: 32-B records of 4-B entries, trees of <= 2^20 leaves; else 64-B records of (ref, bound bits)): word 0 the
+// hint leaf, then the entries nearest-first with max(s, 0)^2 rounded down to fp32, s = sqrt(bound) (1 - 1e-5) - r
+// (1 + 1e-5): a lower bound of the squared distance from any q of the cell.
 template <bool E4>
 __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ nodes, const TriRec* __restrict__ tris,
                                                       double ox, double oy, double oz, double tm, int G, double lx,
                                                       double ly, double lz, double wx, double wy, double wz,
-                                                      const uint32_t* __restrict__ prec, const int* __restrict__ phint,
-                                                      uint32_t* __restrict__ rec) {
+                                                      const int* __restrict__ hint, uint32_t* __restrict__ rec) {
     constexpr int kw = E4 ? 8 : 16;  // record words
     const size_t n = (size_t)G * G * G;
     const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1701,48 +1708,26 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
     const D3 c = D3{lx + ((double)ix + 0.5) * wx, ly + ((double)iy + 0.5) * wy, lz + ((double)iz + 0.5) * wz};
     const double r = 0.5 * sqrt(wx * wx + wy * wy + wz * wz) * 1.001;
     int ref[kCutK];
-    float bd[kCutK];  // bound from c; -1: not formed yet (an entry taken over from the parent)
-    int m = 0, best_leaf = -1;
-    if (prec) {
-        const size_t H = (size_t)(G / 2);
-        const uint32_t* p = prec + (((iz >> 1) * H + (iy >> 1)) * H + (ix >> 1)) * kw;
-        best_leaf = (int)p[0];
-#pragma unroll
-        for (int k = 0; k < kCutK; ++k) {
-            int e;
-            bool ok;
-            if (E4) {
-                e = Ent4::ref(p[1 + k]);
-                ok = (int)p[1 + k] >= 0;
-            } else {
-                e = (int)p[2 + 2 * k];
-                ok = (uint32_t)e != kCutEmpty;
-            }
-            if (ok) {
-                ref[m] = e;
-                bd[m] = -1.f;
-                ++m;
-            }
-        }
-    } else {
-        best_leaf = phint[cell];
-        ref[0] = 0;
-        bd[0] = -1.f;
-        m = 1;
-    }
+    float bd[kCutK];  // bound from c; -1: not formed yet (the root; a leaf until its exact test)
+    int stuck[kCutK];  // list size at which the entry could not be expanded (0: not stuck): retried only once smaller
+    const int best_leaf = hint[cell];
+    ref[0] = 0;
+    bd[0] = -1.f;
+    stuck[0] = 0;
+    int m = 1;
     uint32_t fdummy;
-    double U2 = INFINITY;  // squared distance from c to best_leaf
+    double U2 = INFINITY;  // squared distance from c to its closest face
     if (best_leaf >= 0) {
         D3 ta, tb, tc, o;
         int part;
         load_tri(tris, best_leaf, ta, tb, tc, fdummy);
         U2 = closest_on_triangle(c, ta, tb, tc, o, part);
     }
-    auto limit = [&](double u2) {
-        const double R = (sqrt(u2) + 2.0 * r) * (1.0 + 1e-6);
-        return R < INFINITY ? __double2float_ru(R * R * kSlack) : INFINITY;
-    };
-    float limf = limit(U2);
+    float limf = INFINITY;
+    {
+        const double R = (sqrt(U2) + 2.0 * r) * (1.0 + 1e-6);
+        if (R < INFINITY) limf = __double2float_ru(R * R * kSlack);
+    }
     const double o3[3] = {ox, oy, oz};
     const QF qf = make_qf(c, o3, tm);
     if (m > 0 && limf < INFINITY) {
@@ -1750,43 +1735,51 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
             bool changed = false;
             const int m0 = m;
             for (int k = 0; k < m0 && k < m; ++k) {
-                if (ref[k] < 0) {  // a leaf: its exact distance, once; it may improve U(c) and the hint
+                if (ref[k] < 0) {  // a leaf: its exact distance, once; a leaf beyond R is dropped (its slot is free)
                     if (bd[k] < 0.f) {
                         D3 ta, tb, tc, o;
                         int part;
                         load_tri(tris, ~ref[k], ta, tb, tc, fdummy);
-                        const double d2 = closest_on_triangle(c, ta, tb, tc, o, part);
-                        bd[k] = __double2float_rd(d2);
-                        if (d2 < U2) {
-                            U2 = d2;
-                            best_leaf = ~ref[k];
-                            limf = limit(U2);
-                        }
+                        bd[k] = __double2float_rd(closest_on_triangle(c, ta, tb, tc, o, part));
                         changed = true;
+                        if (bd[k] > limf) {
+                            ref[k] = ref[m - 1];
+                            bd[k] = bd[m - 1];
+                            stuck[k] = stuck[m - 1];
+                            --m;
+                            --k;  // the entry moved into slot k is looked at next
+                        }
                     }
                     continue;
                 }
+                if (stuck[k] && m >= stuck[k]) continue;  // no room has been freed since it was stuck: no reload
                 const NodeV nd = load_node(nodes, ref[k]);
                 float d0, d1;
                 node_child_bounds(nd, qf, d0, d1);
-                if (bd[k] < 0.f) bd[k] = fminf(d0, d1);
+                bd[k] = fmaxf(bd[k], fminf(d0, d1));
                 const bool h0 = d0 <= limf, h1 = d1 <= limf;
                 const int cnt = (int)h0 + (int)h1;
-                if (m - 1 + cnt > kCutK) continue;
+                if (m - 1 + cnt > kCutK) {
+                    stuck[k] = m;
+                    continue;
+                }
                 changed = true;
                 if (cnt == 0) {  // nothing within R below this entry
                     ref[k] = ref[m - 1];
                     bd[k] = bd[m - 1];
+                    stuck[k] = stuck[m - 1];
                     --m;
                     continue;
                 }
                 const int c0 = nd.child(0), c1 = nd.child(1);
+                stuck[k] = 0;
                 if (h0) {
                     ref[k] = c0;
                     bd[k] = c0 < 0 ? -1.f : d0;  // a leaf gets its exact distance in the next pass
                     if (h1) {
                         ref[m] = c1;
                         bd[m] = c1 < 0 ? -1.f : d1;
+                        stuck[m] = 0;
                         ++m;
                     }
                 } else {
@@ -1796,18 +1789,8 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
             }
             if (!changed || m == 0) break;
         }
-        // entries kept under an earlier, larger R that the final one excludes
-        for (int k = 0; k < m;) {
-            if (bd[k] > limf) {
-                ref[k] = ref[m - 1];
-                bd[k] = bd[m - 1];
-                --m;
-            } else {
-                ++k;
-            }
-        }
     }
-    if (m == 0 && !(limf < INFINITY)) {  // no answer for c (cannot happen for a finite mesh): the root
+    if (m == 0) {  // no answer for c, or (cannot happen for a consistent tree) nothing within R: the root
         ref[0] = 0;
         bd[0] = 0.f;
         m = 1;
@@ -1858,6 +1841,50 @@ __global__ __launch_bounds__(kBlock) void k_cut_hint(const uint32_t* __restrict_
     hint[c] = f < T ? (int)inv[f] : -1;
 }
 
+// The closest point and part code of each row on a GIVEN face: the fp64 construction the traversal's answer store
+// runs for its winning face (write_result), so for a row the traversal answered with face f this gives the
+// traversal's point and part bit for bit.  Rows with face MSH_NO_FACE (or >= T) get NaN and part 0, as the
+// traversal's non-finite rows do.  The narrow result exchange (mesh_amd/distributed.py NarrowRing) all-gathers
+// faces only and rebuilds the other ranks' points with it.  inv: face -> leaf (k_face_leaf).
+__global__ __launch_bounds__(kBlock) void k_points_from_faces(const TriRec* __restrict__ tris, const uint32_t* __restrict__ inv,
+                                                              size_t T, const double* __restrict__ q, size_t S,
+                                                              const uint32_t* __restrict__ face, uint32_t* __restrict__ part,
+                                                              double* __restrict__ pt) {
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= S) return;
+    const uint32_t f = face[i];
+    D3 o = D3{NAN, NAN, NAN};
+    int pc = 0;
+    if (f < T) {
+        D3 ta, tb, tc;
+        uint32_t ff;
+        load_tri(tris, (int)inv[f], ta, tb, tc, ff);
+        closest_on_triangle(D3{q[3 * i], q[3 * i + 1], q[3 * i + 2]}, ta, tb, tc, o, pc);
+    }
+    if (part) part[i] = (uint32_t)pc;
+    pt[3 * i] = o.x;
+    pt[3 * i + 1] = o.y;
+    pt[3 * i + 2] = o.z;
+}
+
+int face_leaf_map(const msh_tree* tree, uint32_t* d_inv, hipStream_t s) {
+    const size_t T = tree->T;
+    k_face_leaf<<<(unsigned)((T + kBlock - 1) / kBlock), kBlock, 0, s>>>(static_cast<const TriRec*>(tree->d_leaves), T,
+                                                                          d_inv);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
+int points_from_faces(const msh_tree* tree, const uint32_t* d_inv, const double* d_q, size_t S, const uint32_t* d_face,
+                      uint32_t* d_part, double* d_pt, hipStream_t s) {
+    if (S == 0) return MSH_OK;
+    TimedLaunch tl("points_from_faces", s);
+    k_points_from_faces<<<(unsigned)((S + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+        static_cast<const TriRec*>(tree->d_leaves), d_inv, tree->T, d_q, S, d_face, d_part, d_pt);
+    MSH_HIP(hipGetLastError());
+    return MSH_OK;
+}
+
 int cut_hints(const msh_tree* tree, const uint32_t* d_face, size_t n, uint32_t* d_inv, int* d_hint, hipStream_t s) {
     const size_t T = tree->T;
     k_face_leaf<<<(unsigned)((T + kBlock - 1) / kBlock), kBlock, 0, s>>>(static_cast<const TriRec*>(tree->d_leaves), T,
@@ -1875,18 +1902,18 @@ int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream
     return MSH_OK;
 }
 
-int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const uint32_t* d_prec, const int* d_phint,
-              uint32_t* d_rec, bool e4, hipStream_t s) {
+int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const int* d_hint, uint32_t* d_rec, bool e4,
+              hipStream_t s) {
     const size_t n = (size_t)G * G * G;
     const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
     const TriRec* tris = static_cast<const TriRec*>(tree->d_leaves);
     const double tm = tree_margin(tree->half_diag);
     if (e4)
         k_cut_level<true><<<nb, kBlock, 0, s>>>(tree->d_nodes, tris, tree->origin[0], tree->origin[1], tree->origin[2], tm,
-                                               G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_prec, d_phint, d_rec);
+                                               G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_hint, d_rec);
     else
         k_cut_level<false><<<nb, kBlock, 0, s>>>(tree->d_nodes, tris, tree->origin[0], tree->origin[1], tree->origin[2], tm,
-                                                G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_prec, d_phint, d_rec);
+                                                G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_hint, d_rec);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }

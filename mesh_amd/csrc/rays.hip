@@ -167,6 +167,10 @@ struct AlongPol {
     __device__ bool done() const { return false; }
     // hit point and distance of the ray along +n (k = 0) or -n (k = 1); false: no hit
     __device__ bool along(int k, const D3& a, const D3& b, const D3& c, D3& hit, double& dist) const {
+        return along_pn(k, p, n, a, b, c, hit, dist);
+    }
+    __device__ static bool along_pn(int k, const D3& p, const D3& n, const D3& a, const D3& b, const D3& c, D3& hit,
+                                    double& dist) {
         const D3 d = ray_dir(p, k == 0 ? n : D3{-n.x, -n.y, -n.z});
         double t;
         const int kind = ray_tri(p, d, a, b, c, t);
@@ -206,6 +210,253 @@ struct AlongPol {
         return out;
     }
 };
+
+// nearest_alongnormal with the wave leaf list (K2's scheme, nearest.hip k_knn): a lane appends the leaf children that
+// pass its node test to a ring of (leaf << 6 | owner lane) entries in LDS shared by the wave and keeps walking (until
+// kAlongPend of its leaves wait); whenever 64 entries wait the wave tests them in a full round, one entry per lane --
+// the owner's (p, n) by ds_bpermute, both directions through one copy of the fp64 code -- and the results go back
+// through LDS: an atomic min of the distance's bits per owner, then among the entries that reached it an atomic min
+// of (face << 32 | leaf): the lexicographic (distance, face) rule of AlongPol::test.  Per-lane leaf tests ran with
+// 31 % of the lanes active per VALU instruction (PMC, profiles/r06_c5_pmc_*): the lanes without a leaf idled through
+// the two fp64 ray/triangle constructions of the lanes with one.
+#ifndef MSH_ALONG_PEND
+#define MSH_ALONG_PEND 1
+#endif
+#ifndef MSH_ALONG_LIST
+#define MSH_ALONG_LIST 0
+#endif
+constexpr int kAlongPend = MSH_ALONG_PEND;
+constexpr unsigned kARing = 256;  // ring entries per wave: < 64 left after a full round + <= 128 per step
+__device__ inline unsigned lanes_below_r(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+template <bool STATS>
+__device__ inline void traverse_along_list(const BNode* __restrict__ nodes, size_t T, AlongPol& pol, bool active,
+                                           uint2* __restrict__ lds, uint2* __restrict__ spill, uint32_t* __restrict__ ring,
+                                           unsigned long long* __restrict__ bd, unsigned long long* __restrict__ bfl,
+                                           unsigned& n_nodes, unsigned& n_leaves) {
+    const int lane = threadIdx.x & 63;
+    int node = 0, sp = 0;
+    int nq = 0;             // this lane's entries appended since all of them were last evaluated (a bound)
+    unsigned last_pos = 0;  // ring counter of this lane's newest entry
+    unsigned head = 0, tail = 0;
+    size_t guard = 0;
+    if (active && T == 1) {  // a single leaf: no node to walk
+        node = ~0;
+    }
+    auto run_rounds = [&](unsigned upto) {
+        while (head != upto) {
+            const unsigned n = min(64u, upto - head);
+            bd[lane] = (unsigned long long)__double_as_longlong(pol.best);
+            bfl[lane] = ~0ull;
+            const bool valid = (unsigned)lane < n;
+            const uint32_t en = ring[(head + (valid ? (unsigned)lane : 0u)) & (kARing - 1)];
+            const int src = (int)(en & 63u);
+            const int leaf = (int)(en >> 6);
+            const D3 p = D3{__shfl(pol.p.x, src), __shfl(pol.p.y, src), __shfl(pol.p.z, src)};
+            const D3 nn = D3{__shfl(pol.n.x, src), __shfl(pol.n.y, src), __shfl(pol.n.z, src)};
+            D3 a, b, c;
+            uint32_t face;
+            load_tri(pol.tris, leaf, a, b, c, face);
+            double dist = INFINITY;
+#pragma nounroll
+            for (int k = 0; k < 2; ++k) {
+                D3 hit;
+                double dk;
+                if (AlongPol::along_pn(k, p, nn, a, b, c, hit, dk) && dk < dist) dist = dk;
+            }
+            const unsigned long long kb = (unsigned long long)__double_as_longlong(dist);
+            asm volatile("" ::: "memory");
+            if (valid && dist < INFINITY) atomicMin(&bd[src], kb);
+            asm volatile("" ::: "memory");
+            if (valid && dist < INFINITY && bd[src] == kb) atomicMin(&bfl[src], ((unsigned long long)face << 32) | (unsigned)leaf);
+            asm volatile("" ::: "memory");
+            const unsigned long long nb = bd[lane], nf = bfl[lane];
+            const double nd = __longlong_as_double((long long)nb);
+            const uint32_t nface = (uint32_t)(nf >> 32);
+            if (nf != ~0ull && (nd < pol.best || (nd == pol.best && nface < pol.best_face))) {
+                pol.best = nd;
+                pol.best_face = nface;
+                pol.best_leaf = (int)(uint32_t)nf;
+            }
+            asm volatile("" ::: "memory");
+            if (STATS && valid) ++n_leaves;
+            head += n;
+        }
+        if ((int)(last_pos - head) < 0) nq = 0;  // every entry of this lane is evaluated
+    };
+    for (;;) {
+        const bool can = active && nq < kAlongPend;
+        const bool any = __ballot(can) != 0ull;
+        if (!any && tail == head) break;
+        int l0 = -1, l1 = -1;
+        if (can) {
+            if (node < 0) {  // a parked leaf (or the single leaf of a one-leaf tree)
+                l0 = ~node;
+                node = 0;
+                active = T > 1 && sp > 0;
+                if (active) {
+                    active = false;
+                    while (sp > 0) {
+                        --sp;
+                        const uint2 e = stack_get(lds, spill, sp);
+                        if (pol.keep(__uint_as_float(e.y))) {
+                            node = (int)e.x;
+                            active = true;
+                            break;
+                        }
+                    }
+                }
+            } else {
+                const NodeV nd = load_node(nodes, node);
+                if (STATS) ++n_nodes;
+                bool h0, h1;
+                float k0, k1;
+                pol.children(nd, h0, h1, k0, k1);
+                const int c0 = nd.child(0), c1 = nd.child(1);
+                const bool lf0 = h0 && c0 < 0, lf1 = h1 && c1 < 0;
+                const bool in0 = h0 && c0 >= 0, in1 = h1 && c1 >= 0;
+                if (lf0 && lf1 && nq + 1 >= kAlongPend) {  // room for one: queue the nearer, park the farther
+                    const bool first1 = k1 < k0;
+                    l0 = first1 ? ~c1 : ~c0;
+                    node = first1 ? c0 : c1;  // negative: a parked leaf, handed over by the next step
+                } else {
+                    if (lf0) l0 = ~c0;
+                    if (lf1) { if (l0 < 0) l0 = ~c1; else l1 = ~c1; }
+                    bool more = true;
+                    if (in0 && in1) {
+                        int nearc = c0, farc = c1;
+                        float kf = k1;
+                        if (k1 < k0) { nearc = c1; farc = c0; kf = k0; }
+                        stack_put(lds, spill, sp, make_uint2((unsigned)farc, __float_as_uint(kf)));
+                        ++sp;
+                        node = nearc;
+                    } else if (in0) {
+                        node = c0;
+                    } else if (in1) {
+                        node = c1;
+                    } else {
+                        more = false;
+                        while (sp > 0) {
+                            --sp;
+                            const uint2 e = stack_get(lds, spill, sp);
+                            if (pol.keep(__uint_as_float(e.y))) {
+                                node = (int)e.x;
+                                more = true;
+                                break;
+                            }
+                        }
+                    }
+                    active = more;
+                }
+                if (++guard >= T) active = false;  // each node is entered once: a corrupt tree
+            }
+        }
+        // append this step's leaves (at most two per lane) to the ring, in lane order
+        const unsigned long long m1 = __ballot(l0 >= 0), m2 = __ballot(l1 >= 0);
+        const unsigned pos = tail + lanes_below_r(m1) + lanes_below_r(m2);
+        if (l0 >= 0) {
+            ring[pos & (kARing - 1)] = ((uint32_t)l0 << 6) | (uint32_t)lane;
+            last_pos = pos;
+            ++nq;
+        }
+        if (l1 >= 0) {
+            ring[(pos + 1) & (kARing - 1)] = ((uint32_t)l1 << 6) | (uint32_t)lane;
+            last_pos = pos + 1;
+            ++nq;
+        }
+        tail += (unsigned)(__popcll(m1) + __popcll(m2));
+        const unsigned upto = any ? head + ((tail - head) & ~63u) : tail;
+        if (upto != head) run_rounds(upto);
+    }
+}
+
+// nearest_alongnormal with postponed leaf tests and no leaf list: a lane that reaches a leaf within reach keeps it
+// pending and stops; once every walking lane of the wave holds one, they all test their own leaf together (one call
+// site of the fp64 code), so the construction runs with every lane that has a leaf instead of one lane at a time.
+// A lane pends at most one leaf: its bound is never stale (the wave leaf list, which lets lanes walk on with up to
+// kAlongPend leaves waiting, walked 34.4 nodes per ray instead of 29.5 at kAlongPend >= 4; at 1 it ran 4.75 ms against
+// 5.02 for per-lane tests, profiles/r06_c5_along_list_pend_ab.jsonl, and this form needs neither its LDS ring nor the
+// owners' rows fetched by ds_bpermute).
+template <bool STATS>
+__device__ inline void traverse_along_pend(const BNode* __restrict__ nodes, size_t T, AlongPol& pol, bool active,
+                                           uint2* __restrict__ lds, uint2* __restrict__ spill, unsigned& n_nodes,
+                                           unsigned& n_leaves) {
+    int node = 0, sp = 0;
+    int pend = -1;  // this lane's leaf waiting for the wave's leaf phase
+    size_t guard = 0;
+    if (active && T == 1) {
+        pend = 0;
+        active = false;
+    }
+    for (;;) {
+        const bool can = active && pend < 0;
+        if (__ballot(can) == 0ull) {
+            if (__ballot(pend >= 0) == 0ull) break;
+            if (pend >= 0) {  // every walking lane holds a leaf: all of them test theirs
+                pol.test(pend);
+                if (STATS) ++n_leaves;
+                pend = -1;
+            }
+            continue;
+        }
+        if (!can) continue;
+        if (node < 0) {  // a parked leaf: it is this step's leaf; the walk goes on from the stack
+            pend = ~node;
+            node = 0;
+        } else {
+            const NodeV nd = load_node(nodes, node);
+            if (STATS) ++n_nodes;
+            bool h0, h1;
+            float k0, k1;
+            pol.children(nd, h0, h1, k0, k1);
+            const int c0 = nd.child(0), c1 = nd.child(1);
+            const bool lf0 = h0 && c0 < 0, lf1 = h1 && c1 < 0;
+            const bool in0 = h0 && c0 >= 0, in1 = h1 && c1 >= 0;
+            if (lf0 && lf1) {  // two leaves: the nearer now, the farther parked as the next step's node
+                const bool first1 = k1 < k0;
+                pend = first1 ? ~c1 : ~c0;
+                node = first1 ? c0 : c1;
+                if (++guard >= T) active = false;
+                continue;
+            }
+            if (lf0) pend = ~c0;
+            if (lf1) pend = ~c1;
+            if (in0 && in1) {
+                int nearc = c0, farc = c1;
+                float kf = k1;
+                if (k1 < k0) { nearc = c1; farc = c0; kf = k0; }
+                stack_put(lds, spill, sp, make_uint2((unsigned)farc, __float_as_uint(kf)));
+                ++sp;
+                node = nearc;
+                if (++guard >= T) active = false;
+                continue;
+            }
+            if (in0 || in1) {
+                node = in0 ? c0 : c1;
+                if (++guard >= T) active = false;
+                continue;
+            }
+            if (++guard >= T) {
+                active = false;
+                continue;
+            }
+        }
+        // nothing to descend into: the next entry of the stack within the bound (the pending leaf, if any, is tested
+        // before it is used: the bound may only tighten, so popping now with the older bound is conservative)
+        bool more = false;
+        while (sp > 0) {
+            --sp;
+            const uint2 e = stack_get(lds, spill, sp);
+            if (pol.keep(__uint_as_float(e.y))) {
+                node = (int)e.x;
+                more = true;
+                break;
+            }
+        }
+        active = more;
+    }
+}
 
 // any hit of the closed ray src + t d, t >= 0; key = entry parameter
 struct AnyPol {
@@ -284,8 +535,13 @@ template <int MODE, bool STATS>  // MODE 0 alongnormal, 1 visibility
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? MSH_ALONG_WAVES : 4))) void k_rays(RayArgs a) {
     unsigned n_nodes = 0, n_leaves = 0;
     __shared__ uint2 stk[kStack * kBlock];
+    // alongnormal: each wave's leaf ring + per-owner (distance bits, face << 32 | leaf) slots
+    __shared__ uint32_t rsh[MODE == 0 && MSH_ALONG_LIST ? 4 * (kARing + 64 * 4) : 1];
     const int tid = threadIdx.x, lane = tid & 63;
     uint2* lds = stk + tid;
+    uint32_t* ring = rsh + (MODE == 0 && MSH_ALONG_LIST ? (tid >> 6) * (kARing + 64 * 4) : 0);
+    [[maybe_unused]] unsigned long long* rbd = reinterpret_cast<unsigned long long*>(ring + kARing);
+    [[maybe_unused]] unsigned long long* rbfl = rbd + 64;
     uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
     const unsigned group = blockIdx.x & 7u;
     const D3 org = D3{a.org[0], a.org[1], a.org[2]};
@@ -295,15 +551,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
         tile = __shfl(tile, 0);
         if (tile >= a.ntiles) break;
         const size_t i = (size_t)tile * 64 + lane;
-        if (i >= a.S) continue;
         if (MODE == 0) {
-            const D3 p = D3{a.p[3 * i], a.p[3 * i + 1], a.p[3 * i + 2]};
-            const D3 n = D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]};
+            // every lane stays in the wave's loop (the leaf rounds use all 64); a lane past the rays only helps
+            const bool live = i < a.S;
+            const D3 p = live ? D3{a.p[3 * i], a.p[3 * i + 1], a.p[3 * i + 2]} : D3{0.0, 0.0, 0.0};
+            const D3 n = live ? D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]} : D3{0.0, 0.0, 1.0};
             const D3 dp = ray_dir(p, n), pr = vsub(p, org);
             AlongPol pol{a.tris, p, n, make_rayf(pr, dp, a.M, true), INFINITY, MSH_NO_FACE, -1};
-            if (finite_d3(p) && finite_d3(dp))
-                traverse_rays<AlongPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
-            if (STATS) continue;
+#if MSH_ALONG_LIST
+            traverse_along_list<STATS>(a.nodes, a.T, pol, live && finite_d3(p) && finite_d3(dp), lds, spill, ring, rbd,
+                                       rbfl, n_nodes, n_leaves);
+#else
+            traverse_along_pend<STATS>(a.nodes, a.T, pol, live && finite_d3(p) && finite_d3(dp), lds, spill, n_nodes,
+                                       n_leaves);
+#endif
+            if (STATS || !live) continue;
             const double dist = pol.best == INFINITY ? 1e100 : pol.best;
             const size_t r = a.perm ? (size_t)a.perm[i] : i;  // the caller's row (scattered store)
             a.out_dist[r] = dist;
@@ -313,6 +575,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
             a.out_pt[3 * r + 1] = h.y;
             a.out_pt[3 * r + 2] = h.z;
         } else {
+            if (i >= a.S) continue;
             const size_t ic = i / a.nv, k = i - ic * a.nv;
             const size_t iv = a.vorder ? (size_t)a.vorder[k] : a.v0 + k;  // vertex (global index)
             const size_t o = ic * a.nv + (iv - a.v0);                        // output element

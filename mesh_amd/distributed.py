@@ -160,6 +160,101 @@ class ResultRing(object):
             self._wait(b)
 
 
+def points_from_faces_device(tree, q, face, part, pt, stream=None):
+    """msh_tree_points_from_faces_device: the closest point (and part) of each row of q (S,3) f64 on the face given
+    in face (S,) int32 viewed as uint32 -- the construction the traversal stores for the face it finds, so rows
+    answered with that face get their points bit for bit.  part may be None.  Asynchronous on `stream`."""
+    _native.check(_native.lib().msh_tree_points_from_faces_device(
+        tree.ptr, q.data_ptr(), q.shape[0], face.data_ptr(), part.data_ptr() if part is not None else None,
+        pt.data_ptr(), _stream(q, stream)))
+
+
+class NarrowRing(object):
+    """The narrow form of ResultRing's exchange for closest-point batches: only the faces travel (4 B per row instead
+    of face + part + point, 32 B), and every rank rebuilds the other ranks' points and parts from (query row, face)
+    with msh_tree_points_from_faces_device, bit for bit the points their owners computed.  Every rank holds the
+    whole query stream of a batch (q_all, rank-major: rank r's rows are [r n, (r + 1) n)), as bench.py's C3 stream
+    and a broadcast query batch do.
+
+    gathered: two tuples (face (world n,) int32, part (world n,) int32, point (world n, 3) f64).  step(compute) calls
+    compute(face, part, point) with this rank's rows of buffer k % 2 (views: the answers land in place), starts the
+    in-place all-gather of the face array, and finishes batch k - 1 -- its gather waited for and the other ranks'
+    rows rebuilt on a side stream, so the rebuild overlaps batch k's traversal; result(b) / drain() wait for it."""
+
+    def __init__(self, tree, q_all, n, gathered, group=None, rebuild=None):
+        import torch
+        import torch.distributed as dist
+
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if len(gathered) != 2 or any(len(g) != 3 for g in gathered) or q_all.shape[0] != self.world * n:
+            raise ValueError("NarrowRing: two (face, part, point) buffers of world x n rows and a q_all of as many")
+        for g in gathered:
+            if g[0].shape[0] != self.world * n or g[1].shape[0] != self.world * n or tuple(g[2].shape) != (self.world * n, 3):
+                raise ValueError("NarrowRing: gathered buffers of %d rows expected" % (self.world * n))
+        self.tree, self.q_all, self.n, self.gathered, self.group = tree, q_all, n, gathered, group
+        # rebuild(q, face, part, point, stream): the other ranks' rows (default: msh_tree_points_from_faces_device);
+        # host tensors (the gloo tests) run it inline, without a side stream
+        self.rebuild = rebuild or (lambda q, f, pa, pt, st: points_from_faces_device(tree, q, f, pa, pt, stream=st))
+        self.side = torch.cuda.Stream(device=q_all.device) if q_all.is_cuda else None
+        self.gwork = [None, None]   # the face all-gather of the batch in buffer b
+        self.done = [None, None]    # event: buffer b's rebuild finished (on the side stream)
+        self.k = 0
+
+    def _own(self, b):
+        a, z = self.rank * self.n, (self.rank + 1) * self.n
+        return tuple(x[a:z] for x in self.gathered[b])
+
+    def _finish(self, b):
+        """wait for buffer b's face gather on the side stream and rebuild the other ranks' rows there"""
+        import contextlib
+        import torch
+        w = self.gwork[b]
+        if w is None:
+            return
+        self.gwork[b] = None
+        face, part, pt = self.gathered[b]
+        with (torch.cuda.stream(self.side) if self.side is not None else contextlib.nullcontext()):
+            w.wait()  # the side stream waits for the gather (host tensors: the gather completes)
+            a, z = self.rank * self.n, (self.rank + 1) * self.n
+            for lo, hi in ((0, a), (z, self.world * self.n)):
+                if hi > lo:
+                    self.rebuild(self.q_all[lo:hi], face[lo:hi], part[lo:hi], pt[lo:hi],
+                                 self.side.cuda_stream if self.side is not None else None)
+            if self.side is not None:
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+                self.done[b] = ev
+
+    def _ready(self, b):
+        """the current stream waits until buffer b's batch is complete (gathered and rebuilt)"""
+        import torch
+        self._finish(b)
+        if self.done[b] is not None:
+            torch.cuda.current_stream(self.q_all.device).wait_event(self.done[b])
+            self.done[b] = None
+
+    def step(self, compute):
+        import torch.distributed as dist
+
+        b = self.k & 1
+        self._ready(b)  # batch k - 2's buffer is free again
+        face, part, pt = self._own(b)
+        compute(face, part, pt)
+        self.gwork[b] = dist.all_gather_into_tensor(self.gathered[b][0], face, group=self.group, async_op=True)
+        self._finish(1 - b)  # batch k - 1: its rebuild overlaps this batch's traversal
+        self.k += 1
+        return b
+
+    def result(self, b):
+        self._ready(b)
+        return self.gathered[b]
+
+    def drain(self):
+        for b in (0, 1):
+            self._ready(b)
+
+
 def nearest_device(tree, q, face, part, pt, stream=None):
     """Device-resident closest-point query on torch tensors (q (S,3) f64, face/part (S,) int32 viewed as
     uint32, pt (S,3) f64), asynchronous on `stream` (default: torch's current stream)."""

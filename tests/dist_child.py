@@ -7,6 +7,8 @@ same data (no process group involved):
   * replicate_tree: RCCL broadcast of the packed tree blob, unpacked on the source too (the receiver side of the
     transport; the blob is msh_tree_blob_pack's) -> closest points equal to the original handle's;
   * ResultRing: three query batches, each all-gathered (all_gather_into_tensor, async) while the next one runs;
+  * NarrowRing (faces all-gathered in place) and the rebuild of points / parts from (row, face) it uses for the other
+    ranks' rows (msh_tree_points_from_faces_device, here on every row, MSH_NO_FACE rows included);
   * visibility_sharded / alongnormal_sharded (C5) and batch_nearest_sharded (C4) through their all-gathers.
 Writes a JSON report to argv[1].  The reference loops this split parallelises: spatialsearchmodule.cpp:212-217,
 visibility.cpp:136-173 (search.py:21-30 for C4's tree per mesh).
@@ -85,6 +87,33 @@ def main(out_path):
     ring.drain()
     check(2, ring.result(b))
     rep["ring_batches_equal"] = batches
+
+    # (2b) the narrow exchange: NarrowRing (faces all-gathered in place) for 3 steps of one batch, and the rebuild of
+    # points and parts from (row, face) -- at world 1 no other rank's rows exist, so it runs on every row here
+    from mesh_amd.distributed import NarrowRing, points_from_faces_device
+    nbuf = [(torch.empty(world * n, dtype=torch.int32, device=dev), torch.empty(world * n, dtype=torch.int32, device=dev),
+             torch.empty((world * n, 3), dtype=torch.float64, device=dev)) for _ in range(2)]
+    nring = NarrowRing(dup, q[:world * n], n, nbuf)
+    nb = []
+    for k in range(3):
+        b = nring.step(lambda fc, pa, pt: nearest_device(dup, q[:n], fc, pa, pt))
+        if k >= 1:
+            nb.append(same(nring.result(1 - b), tuple(x[:n] for x in want)))
+    nring.drain()
+    nb.append(same(nring.result(b), tuple(x[:n] for x in want)))
+    rep["narrow_batches_equal"] = nb
+    rpart = torch.empty_like(want[1])
+    rpt = torch.empty_like(want[2])
+    points_from_faces_device(dup, q, want[0], rpart, rpt)
+    nf = want[0].clone()
+    nf[::97] = -1  # MSH_NO_FACE rows: NaN points, part 0
+    npart = torch.empty_like(want[1])
+    npt = torch.empty_like(want[2])
+    points_from_faces_device(dup, q, nf, npart, npt)
+    torch.cuda.synchronize()
+    rep["rebuild_equal"] = bool(torch.equal(rpart, want[1]) and torch.equal(rpt, want[2]))
+    rep["rebuild_no_face"] = bool(torch.isnan(npt[::97]).all() and (npart[::97] == 0).all() and
+                                  torch.equal(npt[1::97], want[2][1::97]))
 
     # (3) C5: visibility and nearest_alongnormal through their sharded helpers (all-gathers at world 1)
     v5, f5 = W.geodesic_icosphere(30)

@@ -41,6 +41,8 @@ def test_collective_path_world1_bit_exact(tmp_path):
     assert rep["replica_is_new_handle"] and rep["replica_equal"]
     assert rep["replica_entry_cut"] == "built"  # the unpacked replica builds its own cut (derived data)
     assert rep["ring_batches_equal"] == [True, True, True]
+    assert rep["narrow_batches_equal"] == [True, True, True]
+    assert rep["rebuild_equal"] and rep["rebuild_no_face"]
     assert rep["visibility_equal"] and 0.05 < rep["visibility_visible_frac"] < 0.95
     assert rep["alongnormal_equal"] and rep["alongnormal_hit_frac"] > 0.9
     assert rep["c4_equal"] and rep["c4_dtypes"] == ["uint32", "uint32", "float64"]

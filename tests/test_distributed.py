@@ -255,3 +255,66 @@ def test_c3_stream_shards_world2():
     for _, _, whole, own in res:
         assert np.array_equal(whole, ref) and np.array_equal(own, ref)
     assert ref.min() >= -1.1 and ref.max() <= 1.1
+
+
+# ---- the narrow exchange: faces all-gathered in place, the other ranks' rows rebuilt from (row, face) ----
+def _worker_narrow(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mesh_amd.distributed import NarrowRing
+        n = 131
+        q_all = torch.arange(world * n * 3, dtype=torch.float64).reshape(world * n, 3) / 7.0
+
+        def rule(q, face):  # stands in for the closest-point construction on a given face
+            return (face * 3 + 1).to(torch.int32), q * 2.0 + face.to(torch.float64)[:, None]
+
+        def rebuild(q, face, part, pt, stream):
+            p, x = rule(q, face)
+            part.copy_(p)
+            pt.copy_(x)
+
+        gathered = [(torch.full((world * n,), -5, dtype=torch.int32), torch.full((world * n,), -5, dtype=torch.int32),
+                     torch.full((world * n, 3), -5.0, dtype=torch.float64)) for _ in range(2)]
+        ring = NarrowRing(None, q_all, n, gathered, rebuild=rebuild)
+        res = []
+        for k in range(4):
+            def compute(fc, pa, pt, k=k):
+                rows = torch.arange(rank * n, (rank + 1) * n)
+                fc.copy_((rows * 5 + k).to(torch.int32))
+                p, x = rule(q_all[rank * n:(rank + 1) * n], fc)
+                pa.copy_(p)
+                pt.copy_(x)
+            b = ring.step(compute)
+            if k >= 1:
+                g = ring.result(1 - b)
+                res.append((k - 1, [t.numpy().copy() for t in g]))
+        ring.drain()
+        res.append((3, [t.numpy().copy() for t in ring.result(b)]))
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_narrow_ring_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_narrow, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 131
+    q_all = np.arange(world * n * 3, dtype=np.float64).reshape(world * n, 3) / 7.0
+    for _, batches in res:
+        assert [k for k, _ in batches] == [0, 1, 2, 3]
+        for k, (face, part, pt) in batches:
+            want_f = (np.arange(world * n) * 5 + k).astype(np.int32)
+            assert (face == want_f).all()
+            assert (part == want_f * 3 + 1).all()
+            assert (pt == q_all * 2.0 + want_f[:, None]).all()

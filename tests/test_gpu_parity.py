@@ -205,15 +205,14 @@ def _nearest_tree(t, q):
 
 def test_entry_cut_bit_exact(oracle, monkeypatch):
     # C3 mesh: walks from the entry cut give the arrays of walks from the root (msh_tree_set_entry_cut(0)) -- the
-    # default grid (G = 400 = 50 x 2^3: three levels each cut from the coarser one's records, 32-B records of 4-B
-    # entries), a 64^3 grid (8 x 2^3), a one-level 8^3 grid (every centre answered, cut from the root), and the
-    # default grid read by the list path without the node prefetch (8-B stack entries: MESH_AMD_LEAF_LIST=2) --
+    # fine automatic grid (G = 400, 32-B records of 4-B entries), a 64^3 and an 8^3 grid, and the fine grid read by
+    # the list path without the node prefetch (8-B stack entries: MESH_AMD_LEAF_LIST=2) --
     # on uniform queries reaching past the grid (+-1.25 around the unit sphere), near-surface queries and queries on
     # cell faces of the default grid; 2000 rows match brute force
     from mesh_amd import spatialsearch
     v, f = W.c3_mesh()
     rng = np.random.default_rng(41)
-    G = 8 * int(round(np.cbrt(min(64 * f.shape[0], 1 << 26)) / 8))  # api.cpp cut_levels' automatic grid
+    G = int(round(np.cbrt(min(64 * f.shape[0], 1 << 26))))  # api.cpp cut_grid: the fine automatic grid
     assert G == 400
     lo, w = -1.25, 2.5 / G  # scene box +-1 (icosphere vertices on the unit sphere), widened by 1/4
     on_faces = rng.uniform(-1.2, 1.2, (20_000, 3))
@@ -244,7 +243,7 @@ def test_entry_cut_bit_exact(oracle, monkeypatch):
 
 def test_entry_cut_wide_records():
     # Trees of more than 2^20 leaves keep 64-B cut records of 8-B entries (the 4-B packing holds 21-bit refs): C5's
-    # 5M-face mesh with one-level (24^3) and three-level (96^3 = 12 x 2^3) grids gives the arrays of walks from the root
+    # 5M-face mesh with 24^3 and 96^3 grids gives the arrays of walks from the root
     from mesh_amd import spatialsearch
     v, f = W.c5_mesh()
     rng = np.random.default_rng(43)
@@ -263,23 +262,35 @@ def test_entry_cut_wide_records():
 
 
 def test_entry_cut_lazy_and_failure_fallback(oracle):
-    # The automatic cut is built by closest-point calls once they have brought one row per 16 of its cells (C2: 881,664
-    # cells, 55,104 rows), never by the build, by rays or by the normals metric, and a call after set_entry_cut builds
-    # it whatever its size; a cut that cannot be built (here 4096^3 cells: more than one query call holds) is not an
-    # error: the handle records the failure and its queries start at the root with the same answers.
+    # The automatic cut comes in two sizes: the coarse grid (8 cells per face: C2 48^3) is built by the closest-point
+    # call that brings the handle's rows to one per 16 of its cells (6,888), never by the build, by rays or by the
+    # normals metric; the fine one (64 per face: 96^3) after 16 rows per fine cell, or at the next call after
+    # set_entry_cut(-1) (a kept tree); a requested grid is built by the next call whatever its size; a cut that cannot
+    # be built (here 4096^3 cells: more than one query call holds) is not an error: the handle records the failure and
+    # its queries start at the root with the same answers.
     from mesh_amd import aabb_normals, spatialsearch
     v, f = W.c2_mesh()  # 13,776 faces: above the 4096-face floor
     q, _ = W.surface_samples(v, f, 40000, seed=51, sigma=0.02)
+    tref = spatialsearch.aabbtree_compute(v, f)
+    tref.set_entry_cut(0)
+    ref = _nearest_tree(tref, q)  # walks from the root
+    del tref
     t = spatialsearch.aabbtree_compute(v, f)
     assert t.entry_cut_info()["state"] == "pending"
     nrm = np.tile([[0.0, 0.0, 1.0]], (q.shape[0], 1))
     spatialsearch.aabbtree_nearest_alongnormal(t, q, nrm)
     assert t.entry_cut_info()["state"] == "pending" and t.entry_cut_info()["bytes"] == 0
-    ref = _nearest_tree(t, q)  # 40,000 rows: below the volume, walks from the root
+    _nearest_tree(t, q[:5000])  # 5,000 rows: below the coarse grid's volume, walks from the root
     assert t.entry_cut_info()["state"] == "pending" and t.entry_cut_info()["bytes"] == 0
-    again = _nearest_tree(t, q)  # 80,000 rows in all: the cut is built by this call
+    again = _nearest_tree(t, q)  # 45,000 rows in all: the coarse grid is built by this call
     info = t.entry_cut_info()
-    assert info["state"] == "built" and info["bytes"] == info["G"] ** 3 * 32 and info["build_ms"] > 0
+    assert info["state"] == "built" and info["G"] == 48 and info["bytes"] == 48 ** 3 * 32 and info["build_ms"] > 0
+    for a, b in zip(ref, again):
+        assert np.array_equal(a, b)
+    t.set_entry_cut(-1)  # a kept tree asks for the fine grid: built by the next call
+    again = _nearest_tree(t, q)
+    info = t.entry_cut_info()
+    assert info["state"] == "built" and info["G"] == 96 and info["bytes"] == 96 ** 3 * 32
     for a, b in zip(ref, again):
         assert np.array_equal(a, b)
     t.set_entry_cut(4096)
@@ -294,7 +305,7 @@ def test_entry_cut_lazy_and_failure_fallback(oracle):
     t.set_entry_cut(-1)
     assert t.entry_cut_info()["state"] == "pending"
     again = _nearest_tree(t, q[:1000])
-    assert t.entry_cut_info()["state"] == "built"
+    assert t.entry_cut_info()["state"] == "built" and t.entry_cut_info()["G"] == 96
     again = _nearest_tree(t, q)
     for a, b in zip(ref, again):
         assert np.array_equal(a, b)
@@ -339,7 +350,7 @@ def test_c3_replication_roundtrip():
     # north_star's replication path on one GPU: the C3 tree packed into one device blob (what rank 0
     # broadcasts), unpacked on the same device (what every other rank does), answers the C3 stream bit for
     # bit like the source handle; the receiver builds its own entry cut on its first query (5M rows: above the
-    # automatic cut's volume, 1 row per 16 of its 64M cells)
+    # coarse automatic grid's volume, 1 row per 16 of its 8M cells)
     import torch
     from mesh_amd import _native, spatialsearch
     from mesh_amd.distributed import nearest_device
