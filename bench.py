@@ -14,10 +14,16 @@ answers the whole 100M stream and the N x 100M answers are all-gathered: the rou
 The BVH build is setup (reported as build_ms); for N > 1 it is built on rank 0 and replicated with one RCCL
 broadcast.  For N > 1 (or --secondary on) two more lines ride along, beside `value` and never as it:
 `c5_visibility_sharded` (BASELINE configs[4]: 160M visibility rays per step, vertex ranges sharded) and
-`c4_batch_sharded` (configs[3]: 4096 meshes x 10k scan points per step, mesh ranges sharded), see secondary().  The entry cut is built by the first (warm-up) query, its time reported as entry_cut_ms.
+`c4_batch_sharded` (configs[3]: 4096 meshes x 10k scan points per step, mesh ranges sharded), see secondary().
+For N > 1 `value_narrow_exchange` repeats the steps with the narrow exchange (faces all-gathered, the other ranks'
+points rebuilt from (row, face): NarrowRing).  The tree asks for the fine entry cut (it answers many batches); the cut
+is built by the first (warm-up) query, its time reported as entry_cut_ms.  `one_shot` (N = 1) times a fresh tree's
+build + first batch with the default (coarse) cut.  --dist runs every collective path at N = 1 too (the nccl process
+group, the broadcast unpacked on the source, both exchanges, the secondaries), as an 8-GPU node's ranks do.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--queries Q]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+    python -m torch.distributed.run --nproc-per-node 1 ... bench.py --gpus 1 --dist
 
 Rank 0 prints ONE JSON line.  `roofline` is for the traversal kernel (k_knn) on rank 0's shard: algorithmic
 bytes per launch = S_rank * (56 + 64 * nodes/query + 80 * leaves/query) with the per-query

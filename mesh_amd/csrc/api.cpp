@@ -548,13 +548,6 @@ static int cut_grid(const msh_tree* t, bool fine) {
 // coarsest grid answered exactly, each finer level cut from the coarser one's records with hints taken from the 8
 // coarse cells around it -- which built C3's grid in 41 ms instead of ~70 but started queries from worse hints:
 // 49.4 node visits per query against 42.5, 2.02-2.06 G q/s against 2.32-2.36 (profiles/r06_c3_cut_levels_ab.jsonl).
-#ifndef MSH_CUT_CENTRE_STEPS
-#define MSH_CUT_CENTRE_STEPS 128
-#endif
-constexpr unsigned kCutCentreSteps = MSH_CUT_CENTRE_STEPS;
-}  // namespace msh
-static int nearest_run(msh_tree* t, const double* d_q, size_t S, const msh::SlotOut& o, hipStream_t s, unsigned stop_at);
-namespace msh {
 static int build_entry_cut(msh_tree* t, bool fine) {
     const int G = cut_grid(t, fine);
     double half[3], H = 0.0, lo[3], w[3];
@@ -599,22 +592,21 @@ static int build_entry_cut(msh_tree* t, bool fine) {
             if ((st = dhint.reserve(n * sizeof(int))) != MSH_OK) break;
             if ((st = dinv.reserve(t->T * sizeof(uint32_t))) != MSH_OK) break;
             if ((st = cut_centres(G, lo, w, dq.as<double>(), s)) != MSH_OK) break;
-            // the centres' walks stop after kCutCentreSteps node steps with their best face so far: U(c) is then an
-            // upper bound of d(c) and the hint a real candidate, which is all the cut needs (centres deep inside a
-            // closed surface, equidistant from much of it, no longer walk for thousands of steps or take pass 2)
-            if ((st = ::nearest_run(t, dq.as<double>(), n, SlotOut{df.as<uint32_t>(), nullptr, dp.as<double>(), nullptr,
-                                                              nullptr}, s, kCutCentreSteps)) != MSH_OK)
+            // (capping the centres' walks at 64 / 128 node steps, their best face so far an upper bound of d(c): the
+            // walks 32 -> 27 / 29.5 ms on C3, the queries from the grid 42.46 -> 43.45 / 42.61 node visits,
+            // profiles/r06_c3_cut_build_probe.jsonl; not kept)
+            if ((st = msh_tree_nearest_device(t, dq.as<double>(), n, df.as<uint32_t>(), nullptr, dp.as<double>(), s)) !=
+                MSH_OK)
                 break;
             if ((st = cut_hints(t, df.as<uint32_t>(), n, dinv.as<uint32_t>(), dhint.as<int>(), s)) != MSH_OK) break;
-            dq.release();  // the centres' rows and points are not needed by the cut itself
-            dp.release();
+            dq.release();  // the centres' rows are not needed by the cut itself
             e = dmalloc(&cut, n * rb);
             if (e != hipSuccess) {
                 set_error("hipMalloc entry cut (%zu cells): %s", n, hipGetErrorString(e));
                 st = MSH_ENOMEM;
                 break;
             }
-            if ((st = cut_level(t, G, lo, w, dhint.as<int>(), cut, e4, s)) != MSH_OK) break;
+            if ((st = cut_level(t, G, lo, w, dp.as<double>(), dhint.as<int>(), cut, e4, s)) != MSH_OK) break;
             (void)hipEventRecord(e1, s);
             if ((e = hipStreamSynchronize(s)) != hipSuccess) {
                 set_error("entry cut build: %s", hipGetErrorString(e));
@@ -671,8 +663,8 @@ static void ensure_entry_cut(msh_tree* t, size_t S) {
         return;
     }
     const std::string keep = g_err;
-    // while a grid is built, the cell-centre queries walk from the root (an installed coarse grid stays meanwhile
-    // out of use: its walks would give the same answers; the build's own queries must not rebuild it)
+    // while a grid is built its cell-centre queries start from the coarse grid, when one is installed (an upgrade),
+    // else from the root; the state is off meanwhile, so the build's own queries do not build again
     uint32_t* old = t->d_cut;
     const int old_G = t->cut_G, old_wide = t->cut_wide;
     const double old_ms = t->cut_ms;
@@ -681,7 +673,6 @@ static void ensure_entry_cut(msh_tree* t, size_t S) {
         old_lo[k] = t->cut_lo[k];
         old_iw[k] = t->cut_iw[k];
     }
-    t->d_cut = nullptr;
     t->cut_state = kCutOff;
     const int st = build_entry_cut(t, fine);
     if (st == MSH_OK) {
@@ -1792,11 +1783,11 @@ int msh_tree_get_info(const msh_tree* t, msh_tree_info* info) {
 
 // ---------------------------------------------------------------------------------------------
 // one sorted closest-point launch over d_q (validated; the entry cut already settled by the caller)
-static int nearest_run(msh_tree* t, const double* d_q, size_t S, const SlotOut& o, hipStream_t s, unsigned stop_at = 0) {
+static int nearest_run(msh_tree* t, const double* d_q, size_t S, const SlotOut& o, hipStream_t s) {
     WsOrder order(t, s);
     QueryOrder ord;
     MSH_TRY(sort_queries(t, d_q, nullptr, S, s, &ord, true));
-    return launch_nearest(t, ord, S, o, s, stop_at);
+    return launch_nearest(t, ord, S, o, s);
 }
 
 int msh_tree_nearest_device(msh_tree* t, const double* d_q, size_t S, uint32_t* d_face, uint32_t* d_part, double* d_pt,

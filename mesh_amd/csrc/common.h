@@ -342,6 +342,46 @@ __host__ __device__ inline void node_child_bounds(const NodeV& nd, const QF& q, 
     d1 = d.y;
 }
 
+// A node's 64 B loaded into LDS ahead of its step (global_load_lds: no registers hold it while the lane appends
+// leaves or runs leaf rounds).  The wave's slot array holds 4 x 64 float4 (piece k of lane l at k * 64 + l); wsl =
+// its LDS byte address (wave-uniform: M0), nb = this lane's first piece.
+__device__ inline void node_prefetch(const BNode* __restrict__ nodes, int i, uint32_t wsl) {
+    const float4* g = reinterpret_cast<const float4*>(nodes + i);
+    // One address register for the four pieces (immediate offsets 0, 16, 32, 48) and M0 stepped by scalar adds of
+    // 1024 - 16: the immediate offset moves the LDS destination too (tools/glds_offset_probe.hip: a lane's 16 B
+    // land at M0 + offset + 16 lane).  The builtin form (__builtin_amdgcn_global_load_lds per piece, no offsets)
+    // computed three more 64-bit addresses and reloaded three spilled M0 values per step: C3 0.6-0.7 % slower
+    // (profiles/r04_c3_prefetch_asm_lead_ab.jsonl).  The compiler does not see these loads; node_from_lds waits
+    // for them explicitly, and its own vmcnt waits stay conservative (the loads only add younger operations).
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_add_u32 m0, m0, 0x3f0\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off offset:16\n\t"
+        "s_add_u32 m0, m0, 0x3f0\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off offset:32\n\t"
+        "s_add_u32 m0, m0, 0x3f0\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off offset:48\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(wsl)
+        : "memory", "scc");
+}
+__device__ inline NodeV node_from_lds(const float4* nb) {
+    // the compiler does not order LDS reads after an LDS DMA: wait for it (vmcnt counts the DMA in issue order)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    NodeV n;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) n.q[k] = nb[k * 64];
+    return n;
+}
+
 // fp64 oriented-box tools for the ray and triangle kernels (fp32 frame and extents widen exactly to fp64).
 // Projections of a point relative to the tree origin onto the node frame.
 struct FrameD {
@@ -483,17 +523,20 @@ __host__ __device__ inline void ray_child_line_dist2(const NodeV& nd, const RayF
 // builtins so the compiler cannot fold the two cases into one generic (flat) access through a
 // pointer select: flat accesses to LDS go through the vector memory pipe and make every stack
 // push/pop wait for the outstanding node loads.
+// (D: the LDS depth; the ray kernels' alongnormal instantiation keeps a shallower one, rays.hip kAlongStack)
+template <int D = kStack>
 __device__ inline void stack_put(uint2* __restrict__ lds, uint2* __restrict__ spill, int sp, uint2 e) {
-    if (sp < kStack) {
+    if (sp < D) {
         lds[sp * kBlock] = e;
     } else {
-        unsigned long long* p = reinterpret_cast<unsigned long long*>(spill + (size_t)(sp - kStack) * kBlock);
+        unsigned long long* p = reinterpret_cast<unsigned long long*>(spill + (size_t)(sp - D) * kBlock);
         __builtin_nontemporal_store(((unsigned long long)e.y << 32) | e.x, p);
     }
 }
+template <int D = kStack>
 __device__ inline uint2 stack_get(const uint2* __restrict__ lds, const uint2* __restrict__ spill, int sp) {
-    if (sp < kStack) return lds[sp * kBlock];
-    const unsigned long long* p = reinterpret_cast<const unsigned long long*>(spill + (size_t)(sp - kStack) * kBlock);
+    if (sp < D) return lds[sp * kBlock];
+    const unsigned long long* p = reinterpret_cast<const unsigned long long*>(spill + (size_t)(sp - D) * kBlock);
     const unsigned long long v = __builtin_nontemporal_load(p);
     return make_uint2((unsigned)v, (unsigned)(v >> 32));
 }

@@ -237,15 +237,15 @@ int gather_rows(const double* d_a, const double* d_b, const uint32_t* d_perm, si
 // caller row j <- slot inv[j] (record fields + nw doubles per row from d_w)
 int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32_t* d_inv, size_t S, const SlotOut& o,
                       hipStream_t s);
-// Entry cut of a single triangle tree (nearest.hip k_cut_level): the records of a G^3 grid from the hint leaves d_hint
-// of the cell centres' exact answers; e4: 32-B records of 4-B entries (trees of <= 2^20 leaves), else 64-B records.
+// Entry cut of a single triangle tree (nearest.hip k_cut_level): the records of a G^3 grid from the cell centres' exact
+// answers (closest points d_pts, their leaves d_hint); e4: 32-B records of 4-B entries (trees of <= 2^20 leaves), else 64-B records.
 // kCutK start entries per cell (the hint takes the record's eighth word; round 5: 8 entries of 8 B + a separate hint;
 // 4 entries: 1773-1800 M q/s against 8, 16: 1285, C3, profiles/r03_c3_entry_cut_ab.jsonl)
 constexpr int kCutK = 7;
 constexpr size_t kEnt4MaxLeaves = (size_t)1 << 20;  // 4-B stack / cut entries: refs in [-2^20, 2^20), 21 bits
 int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s);
-int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const int* d_hint, uint32_t* d_rec, bool e4,
-              hipStream_t s);
+int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, const int* d_hint,
+              uint32_t* d_rec, bool e4, hipStream_t s);
 // d_inv[face] = the leaf holding it (T words)
 int face_leaf_map(const msh_tree* tree, uint32_t* d_inv, hipStream_t s);
 // closest point (and part) of each row q[i] on face d_face[i] (the traversal's answer construction); d_inv from
@@ -255,9 +255,7 @@ int points_from_faces(const msh_tree* tree, const uint32_t* d_inv, const double*
 // d_hint[cell] = the leaf holding face d_face[cell] (d_inv: T scratch words)
 int cut_hints(const msh_tree* tree, const uint32_t* d_face, size_t n, uint32_t* d_inv, int* d_hint, hipStream_t s);
 // closest point: o.face, o.part (nullable), o.pt; with o.w (3 per row) the barycentric variant (part unused)
-// stop_at > 0: every query stops after that many node steps with its best so far (no pass 2; any face is an answer)
-int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s,
-                   unsigned stop_at = 0);
+int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s);
 // batched trees: n = (meshes) * S queries, slot i answered on mesh mesh0 + i / S (the batched sort is mesh-major)
 int launch_nearest_batch(const msh_tree* tree, const QueryOrder& ord, size_t n, size_t S, const SlotOut& o,
                          hipStream_t s, size_t mesh0 = 0);

@@ -89,9 +89,6 @@ struct KnnArgs {
     int spill_depth;
     unsigned long long* stats;
     unsigned budget;
-    // > 0: a lane stops after this many node steps with its best so far as its answer, and there is no pass 2 (the
-    // entry cut's cell centres: any face is a valid upper bound there, build_entry_cut)
-    unsigned stop_at;
     // leader / follower ordering (sorted closest-point launches, MODE 0 and 3): phase 0 = every slot,
     // unhinted; phase 1 = leader slots (i % kLead == 0); phase 2 = the other slots, each starting from the
     // leaf of the nearest leader's closest point in its 64-slot window (see leader_leaf)
@@ -271,46 +268,6 @@ struct Ent4 {
     __device__ static int ref(T e) { return __builtin_amdgcn_sbfe((int)e, 0, 21); }
     __device__ static float bound(T e) { return __uint_as_float(e & 0xFFE00000u); }
 };
-
-// A node's 64 B loaded into LDS ahead of its step (global_load_lds: no registers hold it while the lane appends
-// leaves or runs leaf rounds).  The wave's slot array holds 4 x 64 float4 (piece k of lane l at k * 64 + l); wsl =
-// its LDS byte address (wave-uniform: M0), nb = this lane's first piece.
-__device__ inline void node_prefetch(const BNode* __restrict__ nodes, int i, uint32_t wsl) {
-    const float4* g = reinterpret_cast<const float4*>(nodes + i);
-    // One address register for the four pieces (immediate offsets 0, 16, 32, 48) and M0 stepped by scalar adds of
-    // 1024 - 16: the immediate offset moves the LDS destination too (tools/glds_offset_probe.hip: a lane's 16 B
-    // land at M0 + offset + 16 lane).  The builtin form (__builtin_amdgcn_global_load_lds per piece, no offsets)
-    // computed three more 64-bit addresses and reloaded three spilled M0 values per step: C3 0.6-0.7 % slower
-    // (profiles/r04_c3_prefetch_asm_lead_ab.jsonl).  The compiler does not see these loads; node_from_lds waits
-    // for them explicitly, and its own vmcnt waits stay conservative (the loads only add younger operations).
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_add_u32 m0, m0, 0x3f0\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off offset:16\n\t"
-        "s_add_u32 m0, m0, 0x3f0\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off offset:32\n\t"
-        "s_add_u32 m0, m0, 0x3f0\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off offset:48\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(g), "s"(wsl)
-        : "memory", "scc");
-}
-__device__ inline NodeV node_from_lds(const float4* nb) {
-    // the compiler does not order LDS reads after an LDS DMA: wait for it (vmcnt counts the DMA in issue order)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    NodeV n;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) n.q[k] = nb[k * 64];
-    return n;
-}
 
 // Per-lane depth-first walker.  lds: this lane's column of the LDS stack (stride kBlock).
 template <class E = Ent8>
@@ -845,16 +802,12 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 // records are written after the tile's loop, so the loop holds no copy of the construction
                 if (want_defer && nq == 0) {
                     want_defer = false;
-                    if (a.stop_at) {
-                        active = false;  // answered with its best so far
-                    } else {
-                        dslot = atomicAdd(a.n_deferred, 1u);
-                        if (dslot < a.max_deferred) {
-                            active = false;
-                            deferred = true;
-                        }
-                        // deferred list full: finish here without a budget
+                    dslot = atomicAdd(a.n_deferred, 1u);
+                    if (dslot < a.max_deferred) {
+                        active = false;
+                        deferred = true;
                     }
+                    // deferred list full: finish here without a budget
                 }
                 const bool can = active && !want_defer && nq < kPend;
                 const bool any = __ballot(can) != 0ull;
@@ -1075,11 +1028,7 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                     ++steps;
                     if (STATS) ++tot;
                     if (active && steps >= max_steps) active = false;  // each node is entered once: corrupt tree
-                    if (active && steps == a.budget && a.stop_at) {
-                        if (STATS) n_leaves += nq;
-                        test_queue(kLeafQ);
-                        active = false;  // answered with its best so far
-                    } else if (active && steps == a.budget) {
+                    if (active && steps == a.budget) {
                         const unsigned slot = atomicAdd(a.n_deferred, 1u);
                         if (slot < a.max_deferred) {
                             if (STATS) n_leaves += nq;
@@ -1499,7 +1448,6 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         // wave-cooperative pass 2 instead of holding its tile for up to T serial steps (C1, 840 faces:
         // traversal 1.15 -> 0.56 ms; with no leader phases below, 0.29 ms)
         a.budget = std::min<unsigned>(a.budget, (unsigned)std::max<size_t>(64, a.T / 16));
-        if (a.stop_at) a.budget = a.stop_at;
         a.nunits = nunits;
         a.ntiles = (unsigned)((nunits + 63) / 64);
         const unsigned nblk = std::min<unsigned>((a.ntiles + 3) / 4, ncu * kKnnBlocksPerCU);
@@ -1540,7 +1488,7 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
                 MSH_TRY(pass1(0, a.S, STATS ? "knn_all_stats" : "knn_all"));
             }
         }
-        if (!a.stop_at) {
+        {
             TimedLaunch t2(STATS ? "knn_pass2_stats" : "knn_pass2", s);
             k_knn_coop<MODE, STATS><<<nblk2, kBlock, 0, s>>>(a);
             MSH_HIP(hipGetLastError());
@@ -1613,11 +1561,9 @@ static void cut_args(const msh_tree* tree, KnnArgs& a) {
     }
 }
 
-int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s,
-                   unsigned stop_at) {
+int launch_nearest(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s) {
     KnnArgs a = tree_args(tree, S);
     cut_args(tree, a);
-    a.stop_at = stop_at;
     SlotOut oo = o;
     oo.dist = nullptr;
     if (o.w) {
@@ -1684,14 +1630,16 @@ __global__ __launch_bounds__(kBlock) void k_cut_centres(int G, double lx, double
 }
 
 // The entry cut, one thread per cell of a G^3 grid (cell (ix, iy, iz) = row (iz G + iy) G + ix), from the root, with
-// U(c) = the exact distance from the centre c to its closest face (hint[cell], from the centre's own query).
+// U(c) = the exact distance from the centre c to its closest point (pts[cell], the centre's own query; its face's leaf
+// is hint[cell]).
 // R = (U(c) + 2r) (1 + 1e-6), r the cell's half-diagonal + 0.1 %.  For q in the cell, d(q) <= U(c) + r, so a subtree
 // farther than R from c holds neither q's answer nor a tie.  Entries (internal nodes or ~leaves) are replaced by their
 // children whose bound from c is within R, in passes over the list, while it keeps at most kCutK entries; a child
 // outside R is dropped (the cull is the traversal's own: bound > fp32(R^2 (1 + 2^-40)) rounded up).  An entry's bound
 // from c: its box bound when its parent node was expanded, raised to the smaller of its children's bounds when its own
-// node is loaded, the exact squared distance for a leaf -- each a lower bound of the squared distance from c to what
-// it holds.
+// node is loaded -- each a lower bound of the squared distance from c to what it holds.  (Exact leaf distances as the
+// leaves' bounds, dropping leaves beyond R: 0.4 % fewer leaf tests per query for 10 ms more of build on C3,
+// profiles/r06_c3_cut_build_probe.jsonl.)  An entry that cannot be expanded is retried only once the list shrank.
 // Out (E4: 32-B records of 4-B entries, trees of <= 2^20 leaves; else 64-B records of (ref, bound bits)): word 0 the
 // hint leaf, then the entries nearest-first with max(s, 0)^2 rounded down to fp32, s = sqrt(bound) (1 - 1e-5) - r
 // (1 + 1e-5): a lower bound of the squared distance from any q of the cell.
@@ -1699,7 +1647,8 @@ template <bool E4>
 __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ nodes, const TriRec* __restrict__ tris,
                                                       double ox, double oy, double oz, double tm, int G, double lx,
                                                       double ly, double lz, double wx, double wy, double wz,
-                                                      const int* __restrict__ hint, uint32_t* __restrict__ rec) {
+                                                      const double* __restrict__ pts, const int* __restrict__ hint,
+                                                      uint32_t* __restrict__ rec) {
     constexpr int kw = E4 ? 8 : 16;  // record words
     const size_t n = (size_t)G * G * G;
     const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1708,25 +1657,19 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
     const D3 c = D3{lx + ((double)ix + 0.5) * wx, ly + ((double)iy + 0.5) * wy, lz + ((double)iz + 0.5) * wz};
     const double r = 0.5 * sqrt(wx * wx + wy * wy + wz * wz) * 1.001;
     int ref[kCutK];
-    float bd[kCutK];  // bound from c; -1: not formed yet (the root; a leaf until its exact test)
+    float bd[kCutK];  // bound from c; -1: not formed yet (the root)
     int stuck[kCutK];  // list size at which the entry could not be expanded (0: not stuck): retried only once smaller
     const int best_leaf = hint[cell];
     ref[0] = 0;
     bd[0] = -1.f;
     stuck[0] = 0;
     int m = 1;
-    uint32_t fdummy;
-    double U2 = INFINITY;  // squared distance from c to its closest face
-    if (best_leaf >= 0) {
-        D3 ta, tb, tc, o;
-        int part;
-        load_tri(tris, best_leaf, ta, tb, tc, fdummy);
-        U2 = closest_on_triangle(c, ta, tb, tc, o, part);
-    }
+    // U(c): the distance from c to its answer's point (pts: the centre walks' closest points; NaN without an answer)
+    const D3 pc = D3{pts[3 * cell], pts[3 * cell + 1], pts[3 * cell + 2]};
     float limf = INFINITY;
     {
-        const double R = (sqrt(U2) + 2.0 * r) * (1.0 + 1e-6);
-        if (R < INFINITY) limf = __double2float_ru(R * R * kSlack);
+        const double R = (sqrt(sqdist(c, pc)) + 2.0 * r) * (1.0 + 1e-6);
+        if (R < INFINITY) limf = __double2float_ru(R * R * kSlack);  // NaN / inf (no answer): the root only
     }
     const double o3[3] = {ox, oy, oz};
     const QF qf = make_qf(c, o3, tm);
@@ -1735,23 +1678,7 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
             bool changed = false;
             const int m0 = m;
             for (int k = 0; k < m0 && k < m; ++k) {
-                if (ref[k] < 0) {  // a leaf: its exact distance, once; a leaf beyond R is dropped (its slot is free)
-                    if (bd[k] < 0.f) {
-                        D3 ta, tb, tc, o;
-                        int part;
-                        load_tri(tris, ~ref[k], ta, tb, tc, fdummy);
-                        bd[k] = __double2float_rd(closest_on_triangle(c, ta, tb, tc, o, part));
-                        changed = true;
-                        if (bd[k] > limf) {
-                            ref[k] = ref[m - 1];
-                            bd[k] = bd[m - 1];
-                            stuck[k] = stuck[m - 1];
-                            --m;
-                            --k;  // the entry moved into slot k is looked at next
-                        }
-                    }
-                    continue;
-                }
+                if (ref[k] < 0) continue;  // a leaf: final, with its box bound
                 if (stuck[k] && m >= stuck[k]) continue;  // no room has been freed since it was stuck: no reload
                 const NodeV nd = load_node(nodes, ref[k]);
                 float d0, d1;
@@ -1775,16 +1702,16 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
                 stuck[k] = 0;
                 if (h0) {
                     ref[k] = c0;
-                    bd[k] = c0 < 0 ? -1.f : d0;  // a leaf gets its exact distance in the next pass
+                    bd[k] = d0;
                     if (h1) {
                         ref[m] = c1;
-                        bd[m] = c1 < 0 ? -1.f : d1;
+                        bd[m] = d1;
                         stuck[m] = 0;
                         ++m;
                     }
                 } else {
                     ref[k] = c1;
-                    bd[k] = c1 < 0 ? -1.f : d1;
+                    bd[k] = d1;
                 }
             }
             if (!changed || m == 0) break;
@@ -1902,18 +1829,19 @@ int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream
     return MSH_OK;
 }
 
-int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const int* d_hint, uint32_t* d_rec, bool e4,
-              hipStream_t s) {
+int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, const int* d_hint,
+              uint32_t* d_rec, bool e4, hipStream_t s) {
     const size_t n = (size_t)G * G * G;
     const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
     const TriRec* tris = static_cast<const TriRec*>(tree->d_leaves);
     const double tm = tree_margin(tree->half_diag);
+    TimedLaunch tl("cut_level", s);
     if (e4)
         k_cut_level<true><<<nb, kBlock, 0, s>>>(tree->d_nodes, tris, tree->origin[0], tree->origin[1], tree->origin[2], tm,
-                                               G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_hint, d_rec);
+                                               G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_pts, d_hint, d_rec);
     else
         k_cut_level<false><<<nb, kBlock, 0, s>>>(tree->d_nodes, tris, tree->origin[0], tree->origin[1], tree->origin[2], tm,
-                                                G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_hint, d_rec);
+                                                G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_pts, d_hint, d_rec);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }

@@ -147,8 +147,8 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
     }
 }
 
-// nearest hit along +-n (the line through p); key = lower bound of the squared distance from p to the
-// child's box (K2's packed fp32 bound, node_child_bounds), which also prunes against the best hit so far
+// nearest hit along +-n (the line through p); key = a lower bound of the squared distance from p to a hit inside the
+// child (the line's interval in it, ray_child_line_dist2), which also prunes against the best hit so far
 struct AlongPol {
     const TriRec* __restrict__ tris;
     D3 p, n;      // the rays (p, n) and (p, -n); directions ray_dir(p, +-n) are formed per leaf test
@@ -156,14 +156,14 @@ struct AlongPol {
     double best;  // distance
     uint32_t best_face;
     int best_leaf;  // the hit point is rebuilt from it at the end (hit()), not carried through the walk
-    __device__ double lim2() const { return best == INFINITY ? INFINITY : best * best * kSlack; }
+    float limf;     // best^2 (1 + 2^-40) rounded up to fp32 (the unit of the keys), refreshed when best improves
+    __device__ void relim() { limf = best == INFINITY ? INFINITY : __double2float_ru(best * best * kSlack); }
     __device__ void children(const NodeV& nd, bool& h0, bool& h1, float& k0, float& k1) const {
         ray_child_line_dist2(nd, rf, h0, h1, k0, k1);
-        const double l = lim2();
-        h0 = h0 && (double)k0 <= l;
-        h1 = h1 && (double)k1 <= l;
+        h0 = h0 && k0 <= limf;
+        h1 = h1 && k1 <= limf;
     }
-    __device__ bool keep(float key) const { return (double)key <= lim2(); }
+    __device__ bool keep(float key) const { return key <= limf; }
     __device__ bool done() const { return false; }
     // hit point and distance of the ray along +n (k = 0) or -n (k = 1); false: no hit
     __device__ bool along(int k, const D3& a, const D3& b, const D3& c, D3& hit, double& dist) const {
@@ -194,6 +194,7 @@ struct AlongPol {
                 best_leaf = leaf;
             }
         }
+        relim();
     }
     // the winning hit: the first direction of the best leaf at the best distance (the one test() kept)
     __device__ D3 hit() const {
@@ -278,6 +279,7 @@ __device__ inline void traverse_along_list(const BNode* __restrict__ nodes, size
                 pol.best = nd;
                 pol.best_face = nface;
                 pol.best_leaf = (int)(uint32_t)nf;
+                pol.relim();
             }
             asm volatile("" ::: "memory");
             if (STATS && valid) ++n_leaves;
@@ -378,10 +380,22 @@ __device__ inline void traverse_along_list(const BNode* __restrict__ nodes, size
 // kAlongPend leaves waiting, walked 34.4 nodes per ray instead of 29.5 at kAlongPend >= 4; at 1 it ran 4.75 ms against
 // 5.02 for per-lane tests, profiles/r06_c5_along_list_pend_ab.jsonl, and this form needs neither its LDS ring nor the
 // owners' rows fetched by ds_bpermute).
+// The alongnormal kernel's LDS stack depth.  12 entries (24 KB per block) + the node slots (16 KB) would keep a block
+// at 40 KB, 4 blocks per CU: at 4 waves per SIMD (128 VGPRs, two reloads in the walk) C5 ran 4.53-4.61 ms against
+// 4.50-4.56 at 3 waves with 16 entries (profiles/r06_c5_along_waves_ab.jsonl).
+#ifndef MSH_ALONG_STACK
+#define MSH_ALONG_STACK 16
+#endif
+constexpr int kAlongStack = MSH_ALONG_STACK;
+// PF: the lane's next node is loaded into its LDS slot as soon as it is chosen (node_prefetch, as k_knn's list
+// path), so its latency overlaps the wave's leaf phases and the loop's bookkeeping
+#ifndef MSH_ALONG_PF
+#define MSH_ALONG_PF 1
+#endif
 template <bool STATS>
 __device__ inline void traverse_along_pend(const BNode* __restrict__ nodes, size_t T, AlongPol& pol, bool active,
                                            uint2* __restrict__ lds, uint2* __restrict__ spill, unsigned& n_nodes,
-                                           unsigned& n_leaves) {
+                                           unsigned& n_leaves, const float4* nb, uint32_t wsl) {
     int node = 0, sp = 0;
     int pend = -1;  // this lane's leaf waiting for the wave's leaf phase
     size_t guard = 0;
@@ -389,6 +403,10 @@ __device__ inline void traverse_along_pend(const BNode* __restrict__ nodes, size
         pend = 0;
         active = false;
     }
+    auto fetch = [&]() {
+        if (MSH_ALONG_PF && node >= 0) node_prefetch(nodes, node, wsl);
+    };
+    if (active) fetch();
     for (;;) {
         const bool can = active && pend < 0;
         if (__ballot(can) == 0ull) {
@@ -405,7 +423,7 @@ __device__ inline void traverse_along_pend(const BNode* __restrict__ nodes, size
             pend = ~node;
             node = 0;
         } else {
-            const NodeV nd = load_node(nodes, node);
+            const NodeV nd = MSH_ALONG_PF ? node_from_lds(nb) : load_node(nodes, node);
             if (STATS) ++n_nodes;
             bool h0, h1;
             float k0, k1;
@@ -426,14 +444,16 @@ __device__ inline void traverse_along_pend(const BNode* __restrict__ nodes, size
                 int nearc = c0, farc = c1;
                 float kf = k1;
                 if (k1 < k0) { nearc = c1; farc = c0; kf = k0; }
-                stack_put(lds, spill, sp, make_uint2((unsigned)farc, __float_as_uint(kf)));
+                stack_put<kAlongStack>(lds, spill, sp, make_uint2((unsigned)farc, __float_as_uint(kf)));
                 ++sp;
                 node = nearc;
+                fetch();
                 if (++guard >= T) active = false;
                 continue;
             }
             if (in0 || in1) {
                 node = in0 ? c0 : c1;
+                fetch();
                 if (++guard >= T) active = false;
                 continue;
             }
@@ -447,7 +467,7 @@ __device__ inline void traverse_along_pend(const BNode* __restrict__ nodes, size
         bool more = false;
         while (sp > 0) {
             --sp;
-            const uint2 e = stack_get(lds, spill, sp);
+            const uint2 e = stack_get<kAlongStack>(lds, spill, sp);
             if (pol.keep(__uint_as_float(e.y))) {
                 node = (int)e.x;
                 more = true;
@@ -455,6 +475,7 @@ __device__ inline void traverse_along_pend(const BNode* __restrict__ nodes, size
             }
         }
         active = more;
+        if (more) fetch();
     }
 }
 
@@ -525,16 +546,16 @@ __device__ inline unsigned dequeue_tile_r(unsigned* counters, unsigned ntiles, u
 
 __device__ inline bool finite_d3(const D3& x) { return isfinite(x.x) && isfinite(x.y) && isfinite(x.z); }
 
-// waves per SIMD: visibility 4 (127 VGPRs, no spills); alongnormal 3 (164 VGPRs; at 4 the fp64 leaf test spills 37
-// VGPRs: C5 7.41 vs 6.62 ms in round 2, 5.74 vs 4.98 ms in round 6; one call site of the leaf test for both children
-// and both directions -- a loop -- spilled at 3 waves too: 5.99 ms, profiles/r06_c5_along_ab.jsonl)
+// waves per SIMD: visibility 4 (127 VGPRs, no spills); alongnormal 3 (168 VGPRs, 48 KB of LDS per block with the node
+// slots; at 4 the per-lane fp64 leaf test spilled 37 VGPRs: C5 7.41 vs 6.62 ms in round 2, 5.74 vs 4.98 ms in round 6
+// before the postponed leaf tests, profiles/r06_c5_along_ab.jsonl)
 #ifndef MSH_ALONG_WAVES
 #define MSH_ALONG_WAVES 3
 #endif
 template <int MODE, bool STATS>  // MODE 0 alongnormal, 1 visibility
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? MSH_ALONG_WAVES : 4))) void k_rays(RayArgs a) {
     unsigned n_nodes = 0, n_leaves = 0;
-    __shared__ uint2 stk[kStack * kBlock];
+    __shared__ uint2 stk[(MODE == 0 ? kAlongStack : kStack) * kBlock];
     // alongnormal: each wave's leaf ring + per-owner (distance bits, face << 32 | leaf) slots
     __shared__ uint32_t rsh[MODE == 0 && MSH_ALONG_LIST ? 4 * (kARing + 64 * 4) : 1];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -542,6 +563,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
     uint32_t* ring = rsh + (MODE == 0 && MSH_ALONG_LIST ? (tid >> 6) * (kARing + 64 * 4) : 0);
     [[maybe_unused]] unsigned long long* rbd = reinterpret_cast<unsigned long long*>(ring + kARing);
     [[maybe_unused]] unsigned long long* rbfl = rbd + 64;
+    // alongnormal: each wave's node slots (node_prefetch: LDS address from a wave-uniform index, so M0 is scalar)
+    __shared__ float4 nbuf[MODE == 0 && MSH_ALONG_PF ? 4 * kBlock : 1];
+    const int wv_u = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t wsl = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)(nbuf + (MODE == 0 && MSH_ALONG_PF ? wv_u * 256 : 0));
+    const float4* nb = nbuf + (MODE == 0 && MSH_ALONG_PF ? (tid >> 6) * 256 + lane : 0);
     uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
     const unsigned group = blockIdx.x & 7u;
     const D3 org = D3{a.org[0], a.org[1], a.org[2]};
@@ -557,13 +583,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
             const D3 p = live ? D3{a.p[3 * i], a.p[3 * i + 1], a.p[3 * i + 2]} : D3{0.0, 0.0, 0.0};
             const D3 n = live ? D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]} : D3{0.0, 0.0, 1.0};
             const D3 dp = ray_dir(p, n), pr = vsub(p, org);
-            AlongPol pol{a.tris, p, n, make_rayf(pr, dp, a.M, true), INFINITY, MSH_NO_FACE, -1};
+            AlongPol pol{a.tris, p, n, make_rayf(pr, dp, a.M, true), INFINITY, MSH_NO_FACE, -1, INFINITY};
 #if MSH_ALONG_LIST
             traverse_along_list<STATS>(a.nodes, a.T, pol, live && finite_d3(p) && finite_d3(dp), lds, spill, ring, rbd,
                                        rbfl, n_nodes, n_leaves);
 #else
             traverse_along_pend<STATS>(a.nodes, a.T, pol, live && finite_d3(p) && finite_d3(dp), lds, spill, n_nodes,
-                                       n_leaves);
+                                       n_leaves, nb, wsl);
 #endif
             if (STATS || !live) continue;
             const double dist = pol.best == INFINITY ? 1e100 : pol.best;
@@ -608,6 +634,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
             a.vis[o] = out;
         }
     }
+    // a lane that stopped may still have a node prefetch in flight: it lands before the block's LDS is released
+    if constexpr (MODE == 0 && MSH_ALONG_PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (STATS) {
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
         atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
@@ -637,8 +665,9 @@ static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, c
     MSH_HIP(hipMemsetAsync(a.counters, 0, 8 * 32 * sizeof(unsigned), s));
     a.spill = nullptr;
     a.spill_depth = 0;
-    if (tree->max_depth + 1 > kStack) {
-        a.spill_depth = tree->max_depth + 1 - kStack + 1;
+    const int lds_depth = MODE == 0 ? kAlongStack : kStack;
+    if (tree->max_depth + 1 > lds_depth) {
+        a.spill_depth = tree->max_depth + 1 - lds_depth + 1;
         MSH_TRY(tree->ws.spill.reserve((size_t)nblk * kBlock * (size_t)a.spill_depth * sizeof(uint2)));
         a.spill = tree->ws.spill.as<uint2>();
     }

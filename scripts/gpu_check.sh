@@ -28,6 +28,10 @@ for s in $STAGES; do
       for n in ${ORDER:?set ORDER}; do
         MESH_AMD_LIB=$PWD/build/variants/$n.so timeout -k 10 400 python bench.py --steps ${BSTEPS:-10} --warmup 2 --no-cpu >> gpurun_out/benchab.jsonl 2> gpurun_out/benchab_$n.err; ok benchab_$n $?
       done ;;
+    cutprobe)  # entry cut build phases over build/variants/*.so in the order ORDER
+      for n in ${ORDER:?set ORDER}; do
+        MESH_AMD_LIB=$PWD/build/variants/$n.so timeout -k 10 300 python scripts/cut_build_probe.py >> gpurun_out/cutprobe.jsonl 2> gpurun_out/cutprobe_$n.err; ok cutprobe_$n $?
+      done ;;
     smoke)  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; ok smoke $? ;;
     pytest) timeout -k 10 1200 python -u -m pytest tests -v -m gpu -x -p no:cacheprovider --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; ok pytest $? ;;
     bench_small) timeout -k 10 600 python bench.py --queries 10000000 --steps 5 --warmup 2 --no-cpu > gpurun_out/bench_small.log 2>&1; ok bench_small $? ;;
