@@ -291,10 +291,11 @@ def main():
         return (torch.empty(n, dtype=torch.int32, device=dev), torch.empty(n, dtype=torch.int32, device=dev),
                 torch.empty((n, 3), dtype=torch.float64, device=dev))
 
-    slabs = [slab(rows) for _ in range(2 if coll else 1)]
+    slabs = [slab(rows)]  # the steps without an exchange (N = 1, and the no-allgather line)
     ring = None
     if coll:
-        ring = ResultRing(slabs, [slab(world * rows) for _ in range(2)])
+        # in place: each batch is answered into its own rows of the gathered buffers, which are all-gathered in place
+        ring = ResultRing(None, [slab(world * rows) for _ in range(2)])
 
     def answer(sl):
         nearest_device(tree, q, sl[0][:S_loc], sl[1][:S_loc], sl[2][:S_loc], stream=stream)
@@ -393,11 +394,10 @@ def main():
             del rp, rpt
             torch.cuda.empty_cache()
         if not args.no_weak:
-            del ring, slabs
+            del ring
             torch.cuda.empty_cache()
-            wslabs = [slab(S) for _ in range(2)]
             wg = slab(world * S)  # one gathered buffer written by both batches in turn: only the timing matters
-            wring = ResultRing(wslabs, [wg, wg])
+            wring = ResultRing(None, [wg, wg])
 
             def weak_step():
                 wring.step(lambda sl: nearest_device(tree, q_all, sl[0], sl[1], sl[2], stream=stream))
@@ -405,7 +405,7 @@ def main():
             weak_step()
             wring.drain()
             elapsed_weak = timed(weak_step, args.steps, wring)
-            del wring, wslabs, wg
+            del wring, wg
             torch.cuda.empty_cache()
 
     # one-shot device caller (untimed for value): a fresh tree from the host mesh, its first 100M-row batch with the

@@ -123,13 +123,22 @@ class ResultRing(object):
     it; a slab and its gathered buffer are rewritten only after the gather that used them has completed (its
     handle is waited on, on the current stream, first).
 
-    slabs: two tuples of local result tensors (e.g. face, part, point); gathered: two tuples of the matching
-    (world n, ...) tensors (passing the same tuple twice is allowed when only the timing matters: the two
-    gathers then write one buffer in turn).  step(compute) calls compute(slab) to enqueue batch k's work on the
+    slabs: two tuples of local result tensors (e.g. face, part, point), or None for the in-place form (each slab the
+    view of this rank's rows of its gathered buffer); gathered: two tuples of the matching (world n, ...) tensors
+    (passing the same tuple twice is allowed when only the timing matters: the two gathers then write one buffer in
+    turn).  step(compute) calls compute(slab) to enqueue batch k's work on the
     current stream, starts its gathers and returns k % 2; result(b) waits for batch b's gathers and returns
     gathered[b] — the answer of the newest batch started in that buffer; drain() waits for every gather."""
 
     def __init__(self, slabs, gathered, group=None):
+        import torch.distributed as dist
+
+        if slabs is None:
+            # in place: this rank's slab of buffer b is the view of its own rows of gathered[b], and the all-gather
+            # runs in place (no copy of the local rows; at world size 1 nothing moves)
+            world, rank = dist.get_world_size(group), dist.get_rank(group)
+            n = gathered[0][0].shape[0] // world
+            slabs = [tuple(x[rank * n:(rank + 1) * n] for x in g) for g in gathered]
         if len(slabs) != 2 or len(gathered) != 2 or any(len(s) != len(gathered[0]) for s in slabs) or \
                 len(gathered[1]) != len(gathered[0]):
             raise ValueError("ResultRing: two slabs and two gathered buffers of the same tensors")

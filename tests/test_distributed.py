@@ -318,3 +318,48 @@ def test_narrow_ring_world2():
             assert (face == want_f).all()
             assert (part == want_f * 3 + 1).all()
             assert (pt == q_all * 2.0 + want_f[:, None]).all()
+
+
+def _worker_ring_inplace(rank, world, port, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from mesh_amd.distributed import ResultRing
+        n = 97
+        gathered = [(torch.full((world * n,), -1, dtype=torch.int32), torch.full((world * n, 3), -1.0, dtype=torch.float64))
+                    for _ in range(2)]
+        ring = ResultRing(None, gathered)  # in place: the slabs are this rank's rows of the gathered buffers
+        res = []
+        for k in range(3):
+            def run(slab, k=k):
+                face, pt = slab
+                face.copy_(torch.arange(n, dtype=torch.int32) + 1000 * rank + 100000 * k)
+                pt.copy_(face.to(torch.float64)[:, None] * torch.tensor([2.0, 0.5, -1.0], dtype=torch.float64))
+            b = ring.step(run)
+            g = ring.result(b)
+            res.append((k, g[0].numpy().copy(), g[1].numpy().copy()))
+        ring.drain()
+        out_q.put((rank, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_result_ring_in_place_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_ring_inplace, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    n = 97
+    for _, batches in res:
+        for k, face, pt in batches:
+            want = np.concatenate([np.arange(n) + 1000 * r + 100000 * k for r in range(world)]).astype(np.int32)
+            assert (face == want).all()
+            assert (pt == want[:, None].astype(np.float64) * np.array([2.0, 0.5, -1.0])).all()
