@@ -357,18 +357,22 @@ def main():
     # rank answers the whole stream; the world x S answers are all-gathered) ----
     elapsed_no_ag = elapsed_weak = elapsed_narrow = None
     probe = None
+    errors = {}
     if coll:
         elapsed_no_ag = timed(lambda: answer(slabs[0]), args.steps)
         if S % world == 0:
-            nring = NarrowRing(tree, q_all, S // world, [slab(S) for _ in range(2)])
+            try:  # a line beside value: a failure is reported, not fatal to the value line
+                nring = NarrowRing(tree, q_all, S // world, [slab(S) for _ in range(2)])
 
-            def narrow_step():
-                nring.step(lambda fc, pa, pt: nearest_device(tree, q, fc, pa, pt, stream=stream))
+                def narrow_step():
+                    nring.step(lambda fc, pa, pt: nearest_device(tree, q, fc, pa, pt, stream=stream))
 
-            narrow_step()
-            nring.drain()
-            elapsed_narrow = timed(narrow_step, args.steps, nring)
-            del nring
+                narrow_step()
+                nring.drain()
+                elapsed_narrow = timed(narrow_step, args.steps, nring)
+                del nring
+            except Exception as e:  # noqa: BLE001
+                errors["narrow_exchange"] = "%s: %s" % (type(e).__name__, e)
             torch.cuda.empty_cache()
         # the narrow exchange's rebuild on its own: the points and parts of 7/8 of the stream (what a rank of N = 8
         # rebuilds per step) from (row, face), against this rank's answers of the same rows (N = 1: all of them)
@@ -426,7 +430,13 @@ def main():
         t1.free()
         del t1
 
-        sec = secondary(timed, world, rank, dev, args.steps, coll)
+    sec = None
+    if args.secondary == "on" or (args.secondary == "auto" and coll):
+        try:  # lines beside value: a failure is reported, not fatal to the value line
+            sec = secondary(timed, world, rank, dev, args.steps, coll)
+        except Exception as e:  # noqa: BLE001
+            errors["secondary"] = "%s: %s" % (type(e).__name__, e)
+            torch.cuda.empty_cache()
 
     # ---- instrumented traversal (untimed): algorithmic bytes of this rank's shard ----
     nodes, leaves = _native.ctypes.c_uint64(0), _native.ctypes.c_uint64(0)
@@ -531,6 +541,8 @@ def main():
         out["narrow_rebuild_probe"] = probe
     if one_shot is not None:
         out["one_shot"] = one_shot
+    if errors:
+        out["errors"] = errors
     if elapsed_weak is not None:
         out["value_weak_100M_per_gpu"] = world * S * args.steps / elapsed_weak
         out["ms_per_step_weak"] = elapsed_weak / args.steps * 1e3
