@@ -152,22 +152,25 @@ int msh_tree_points_from_faces_device(msh_tree* tree, const double* d_q, size_t 
 int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* d_perm, void* stream);
 
 /* Entry cut of a triangle tree (no reference counterpart: derived acceleration data).  A grid
- * of G^3 cells over the scene box widened by 1/4, 68 B per cell (8 start entries + a hint leaf), from which
- * closest-point queries start their walks instead of the root; it changes where a walk starts, never an
- * answer.  It is built lazily by a closest-point call of the handle (msh_tree_nearest*, msh_tree_nearest_bary*,
- * msh_tree_nearest_stats): the automatic grid once the handle's calls have brought at least one row per 16 of its
- * cells (C3: 4.2M rows; a few small calls on a large mesh walk from the root instead of paying the build), a grid
- * asked for with msh_tree_set_entry_cut by the next call whatever its size.  Trees used only for rays, visibility
- * or the normals metric never hold it; trees of < 4096 faces never get one.  The call that builds it is
- * synchronous, also for the *_device entry points (the cut's build waits for its own cell-centre queries): a
- * caller that captures *_device calls in a graph or needs them asynchronous calls msh_tree_set_entry_cut and makes
- * one small query first (or sets G = 0).
- *   G < 0: automatic grid (about 64 cells per face, at most 2^26 cells: C3 G = 400, 4.4 GB) — the default;
+ * of G^3 cells over the scene box widened by 1/4, one record per cell -- its hint leaf and 7 start entries: 32 B for
+ * trees of up to 2^20 faces, 64 B beyond -- from which closest-point queries start their walks instead of the root;
+ * it changes where a walk starts, never an answer.  It is built lazily by a closest-point call of the handle
+ * (msh_tree_nearest*, msh_tree_nearest_bary*, msh_tree_nearest_stats).  The automatic grid comes in two sizes: the
+ * coarse one (about 8 cells per face, at most 2^23 cells: C3 G = 200, 256 MB, ~11 ms) once the handle's calls have
+ * brought at least one row per 16 of its cells (C3: 500k rows; a few small calls on a large mesh walk from the root
+ * instead of paying the build), the fine one (about 64 cells per face, at most 2^26: C3 G = 400, 2.05 GB, ~65 ms)
+ * once they have brought 16 rows per fine cell (C3: ~1G rows), or at the next call after msh_tree_set_entry_cut(t,
+ * -1) (a caller that keeps the tree for many batches).  A grid asked for with msh_tree_set_entry_cut is built by the
+ * next call whatever its size.  Trees used only for rays, visibility or the normals metric never hold it; trees of
+ * < 4096 faces never get one.  The call that builds it is synchronous, also for the *_device entry points (the cut's
+ * build waits for its own cell-centre queries): a caller that captures *_device calls in a graph or needs them
+ * asynchronous calls msh_tree_set_entry_cut and makes one small query first (or sets G = 0).
+ *   G < 0: the fine automatic grid at the next call (the default policy above until then);
  *   G = 0: no cut (frees one already built); queries start at the root;
  *   G > 0: G^3 cells.
  * Calling it (any G != 0, also the current one) makes the next closest-point call build the grid if it is not
- * built yet; changing G frees the current cut first.  A cut that cannot be
- * built (device memory) is not an error: its queries start at the root; an automatic grid is tried again after
+ * built yet; changing G frees the current cut first.  A cut that cannot be built (device memory) is not an error:
+ * its queries start at the root (a failed upgrade keeps the coarse grid); an automatic grid is tried again after
  * another threshold of rows (at most twice, state 0 meanwhile), then the handle records the failure (state 3), as
  * it does at once for a grid asked for with msh_tree_set_entry_cut. */
 int msh_tree_set_entry_cut(msh_tree* tree, int G);

@@ -237,9 +237,9 @@ class Handle(object):
         return inf
 
     def set_entry_cut(self, G=-1):
-        """msh_tree_set_entry_cut: G < 0 automatic grid (default), 0 none, > 0 G^3 cells; built by the next
-        closest-point query whatever its size (without this call, the automatic grid waits until the handle's
-        queries number at least 1/16 of its cells)."""
+        """msh_tree_set_entry_cut: G < 0 the fine automatic grid (~64 cells per face), 0 none, > 0 G^3 cells; built by
+        the next closest-point query whatever its size (without this call the handle gets the coarse automatic grid,
+        ~8 cells per face, once its queries number 1/16 of its cells, and the fine one after 16 rows per fine cell)."""
         check(lib().msh_tree_set_entry_cut(self.ptr, int(G)))
 
     CUT_STATES = {0: "pending", 1: "built", 2: "off", 3: "failed"}

@@ -7,7 +7,7 @@
 # preloaded:
 #   * the non-GPU tests of the loaders, the ABI / header / validation surface and the oracle against the reference's
 #     golden vectors (tests/test_loaders.py, tests/test_abi.py, tests/test_oracle.py);
-#     (less test_build_id_matches_sources: the sanitized build has its own id, and the bound-check test, run below);
+#     (less test_build_id_matches_sources -- the sanitized build has its own id -- and the bound-check test, run below);
 #   * tests/csrc/bound_check.cpp (the kernels' fp32 bound code on the host) built with the same sanitizers.
 # Leak checking is off (the Python interpreter keeps its allocations); any ASan report or UBSan error aborts.
 #
