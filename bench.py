@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--cpu-queries", type=int, default=24000,
                     help="CPU baseline: fixed sample of queries per host thread (1 thread: ~12 s)")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-one-shot", action="store_true",
+                    help="skip the one-shot line (profiling runs: its fresh tree's traversals would mix into the kernel "
+                         "statistics of the timed one)")
     ap.add_argument("--secondary", choices=("auto", "on", "off"), default="auto",
                     help="C5 visibility and C4 batch lines beside value (auto: when the collective path runs, the "
                          "configs north_star shards across GPUs)")
@@ -415,7 +418,7 @@ def main():
     # one-shot device caller (untimed for value): a fresh tree from the host mesh, its first 100M-row batch with the
     # automatic entry cut (the coarse grid, built by that call), results in HBM -- build + cut + batch
     one_shot = None
-    if world == 1:
+    if world == 1 and not args.no_one_shot:
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         t1 = spatialsearch.aabbtree_compute(v, f)

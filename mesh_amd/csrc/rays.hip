@@ -91,17 +91,20 @@ __device__ inline bool cgal_plane_line(const D3& p, const D3& d, const D3& a, co
 __device__ inline D3 ray_dir(const D3& p, const D3& v) { return vsub(vadd(p, v), p); }
 
 // ---- generic traversal: the policy decides box hits (and ordering key) and leaf tests ----
-template <class Pol, bool STATS>
+// PF: each next node is loaded into the lane's LDS slot (nb; node_prefetch) as soon as it is chosen; D: LDS stack depth
+template <class Pol, bool STATS, bool PF = false, int D = kStack>
 __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, Pol& pol, uint2* __restrict__ lds,
-                                     uint2* __restrict__ spill, unsigned& n_nodes, unsigned& n_leaves) {
+                                     uint2* __restrict__ spill, unsigned& n_nodes, unsigned& n_leaves,
+                                     const float4* nb = nullptr, uint32_t wsl = 0) {
     if (T == 1) {
         pol.test(0);
         if (STATS) ++n_leaves;
         return;
     }
     int node = 0, sp = 0;
+    if (PF) node_prefetch(nodes, 0, wsl);
     for (size_t guard = 0; guard < T; ++guard) {
-        const NodeV nd = load_node(nodes, node);
+        const NodeV nd = PF ? node_from_lds(nb) : load_node(nodes, node);
         if (STATS) ++n_nodes;
         bool h0, h1;
         float k0, k1;
@@ -126,17 +129,21 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
             float kf = k1;
             if (k1 < k0) { nearc = c1; farc = c0; kf = k0; }
             const uint2 e = make_uint2((unsigned)farc, __float_as_uint(kf));
-            stack_put(lds, spill, sp, e);
+            stack_put<D>(lds, spill, sp, e);
             ++sp;
             node = nearc;
+            if (PF) node_prefetch(nodes, node, wsl);
             continue;
         }
-        if (h0) { node = c0; continue; }
-        if (h1) { node = c1; continue; }
+        if (h0 || h1) {
+            node = h0 ? c0 : c1;
+            if (PF) node_prefetch(nodes, node, wsl);
+            continue;
+        }
         bool found = false;
         while (sp > 0) {
             --sp;
-            const uint2 e = stack_get(lds, spill, sp);
+            const uint2 e = stack_get<D>(lds, spill, sp);
             if (pol.keep(__uint_as_float(e.y))) {
                 node = (int)e.x;
                 found = true;
@@ -144,6 +151,7 @@ __device__ inline void traverse_rays(const BNode* __restrict__ nodes, size_t T, 
             }
         }
         if (!found) break;
+        if (PF) node_prefetch(nodes, node, wsl);
     }
 }
 
@@ -387,6 +395,13 @@ __device__ inline void traverse_along_list(const BNode* __restrict__ nodes, size
 #define MSH_ALONG_STACK 16
 #endif
 constexpr int kAlongStack = MSH_ALONG_STACK;
+// visibility: the node prefetch into LDS with a 12-entry stack (24 KB + 16 KB of node slots per block: 4 blocks per
+// CU, the kernel's 4 waves per SIMD) measured 58.8-59.8 against 50.9-51.4 ms for C5's 160M rays
+// (profiles/r06_c5_vis_pf_ab.jsonl): off
+#ifndef MSH_VIS_PF
+#define MSH_VIS_PF 0
+#endif
+constexpr int kVisStack = MSH_VIS_PF ? 12 : kStack;
 // PF: the lane's next node is loaded into its LDS slot as soon as it is chosen (node_prefetch, as k_knn's list
 // path), so its latency overlaps the wave's leaf phases and the loop's bookkeeping
 #ifndef MSH_ALONG_PF
@@ -555,7 +570,7 @@ __device__ inline bool finite_d3(const D3& x) { return isfinite(x.x) && isfinite
 template <int MODE, bool STATS>  // MODE 0 alongnormal, 1 visibility
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 0 ? MSH_ALONG_WAVES : 4))) void k_rays(RayArgs a) {
     unsigned n_nodes = 0, n_leaves = 0;
-    __shared__ uint2 stk[(MODE == 0 ? kAlongStack : kStack) * kBlock];
+    __shared__ uint2 stk[(MODE == 0 ? kAlongStack : kVisStack) * kBlock];
     // alongnormal: each wave's leaf ring + per-owner (distance bits, face << 32 | leaf) slots
     __shared__ uint32_t rsh[MODE == 0 && MSH_ALONG_LIST ? 4 * (kARing + 64 * 4) : 1];
     const int tid = threadIdx.x, lane = tid & 63;
@@ -564,10 +579,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
     [[maybe_unused]] unsigned long long* rbd = reinterpret_cast<unsigned long long*>(ring + kARing);
     [[maybe_unused]] unsigned long long* rbfl = rbd + 64;
     // alongnormal: each wave's node slots (node_prefetch: LDS address from a wave-uniform index, so M0 is scalar)
-    __shared__ float4 nbuf[MODE == 0 && MSH_ALONG_PF ? 4 * kBlock : 1];
+    constexpr bool kPF = MODE == 0 ? MSH_ALONG_PF : MSH_VIS_PF;
+    __shared__ float4 nbuf[kPF ? 4 * kBlock : 1];
     const int wv_u = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t wsl = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)(nbuf + (MODE == 0 && MSH_ALONG_PF ? wv_u * 256 : 0));
-    const float4* nb = nbuf + (MODE == 0 && MSH_ALONG_PF ? (tid >> 6) * 256 + lane : 0);
+    const uint32_t wsl = (uint32_t)(size_t)(__attribute__((address_space(3))) float4*)(nbuf + (kPF ? wv_u * 256 : 0));
+    const float4* nb = nbuf + (kPF ? (tid >> 6) * 256 + lane : 0);
     uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
     const unsigned group = blockIdx.x & 7u;
     const D3 org = D3{a.org[0], a.org[1], a.org[2]};
@@ -614,7 +630,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
             const D3 d = ray_dir(src, dir);
             AnyPol pol{a.tris, src, d, make_rayf(vsub(src, org), d, a.M, false), false};
             if (finite_d3(src) && finite_d3(d))
-                traverse_rays<AnyPol, STATS>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves);
+                traverse_rays<AnyPol, STATS, kPF, kVisStack>(a.nodes, a.T, pol, lds, spill, n_nodes, n_leaves, nb, wsl);
             if (STATS) continue;
             const uint32_t reach = pol.hit ? 0u : 1u;
             a.ndc[o] = a.normals ? vdot(D3{a.normals[3 * iv], a.normals[3 * iv + 1], a.normals[3 * iv + 2]}, dir) : 0.0;
@@ -635,7 +651,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
         }
     }
     // a lane that stopped may still have a node prefetch in flight: it lands before the block's LDS is released
-    if constexpr (MODE == 0 && MSH_ALONG_PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (kPF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (STATS) {
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
         atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
@@ -665,7 +681,7 @@ static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, c
     MSH_HIP(hipMemsetAsync(a.counters, 0, 8 * 32 * sizeof(unsigned), s));
     a.spill = nullptr;
     a.spill_depth = 0;
-    const int lds_depth = MODE == 0 ? kAlongStack : kStack;
+    const int lds_depth = MODE == 0 ? kAlongStack : kVisStack;
     if (tree->max_depth + 1 > lds_depth) {
         a.spill_depth = tree->max_depth + 1 - lds_depth + 1;
         MSH_TRY(tree->ws.spill.reserve((size_t)nblk * kBlock * (size_t)a.spill_depth * sizeof(uint2)));

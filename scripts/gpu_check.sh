@@ -56,13 +56,13 @@ for s in $STAGES; do
     configs) timeout -k 10 900 python scripts/bench_configs.py > gpurun_out/bench_configs.log 2>&1; ok configs $? ;;
     bench)  timeout -k 10 900 python bench.py > gpurun_out/bench.log 2>&1; ok bench $? ;;
     pmc)    PASSES="${PMC_PASSES:-stats fetch write tcc sq valu valu2 sq2}" TARGET=${PMC_TARGET:-c3} bash scripts/profile_pmc.sh > gpurun_out/pmc_${PMC_TARGET:-c3}.log 2>&1; ok pmc_${PMC_TARGET:-c3} $? ;;
-    pmc_cfg) for t in ${PMC_CFGS:-c5 c2}; do PASSES="stats fetch write tcc" TARGET=$t bash scripts/profile_pmc.sh > gpurun_out/pmc_$t.log 2>&1; ok pmc_$t $?; done ;;
+    pmc_cfg) for t in ${PMC_CFGS:-c5 c2}; do PASSES="${PMC_CFG_PASSES:-stats fetch write tcc}" TARGET=$t bash scripts/profile_pmc.sh > gpurun_out/pmc_$t.log 2>&1; ok pmc_$t $?; done ;;
     nptl)   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$OLDPWD/gpurun_out/nptl" -o run -- python3 "$OLDPWD/scripts/numpy_timeline.py" --calls 3 > "$OLDPWD/gpurun_out/nptl.log" 2>&1); ok nptl $? ;;
     facade) timeout -k 10 900 python scripts/bench_configs.py --configs facade --reps 2 > gpurun_out/facade.log 2>&1; ok facade $? ;;
     repl)   timeout -k 10 300 python scripts/replication_timing.py > gpurun_out/repl.log 2>&1; ok repl $? ;;
     bench_stats) MESH_AMD_STATS_DUMP=1 timeout -k 10 600 python bench.py --steps 2 --warmup 1 --no-cpu > gpurun_out/bench_stats.log 2>&1; ok bench_stats $? ;;
     prof_small) (cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof_small" -o run -- python3 "$OLDPWD/bench.py" --queries 10000000 --steps 2 --warmup 1 --no-cpu > "$OLDPWD/gpurun_out/prof_small.log" 2>&1); ok prof_small $? ;;
-    prof)   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 3 --warmup 1 --no-cpu > "$OLDPWD/gpurun_out/prof.log" 2>&1); ok prof $? ;;
+    prof)   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 900 rocprofv3 --kernel-trace --stats -d "$OLDPWD/gpurun_out/prof" -o run -- python3 "$OLDPWD/bench.py" --steps 3 --warmup 1 --no-cpu --no-one-shot > "$OLDPWD/gpurun_out/prof.log" 2>&1); ok prof $? ;;
   esac
 done
 echo done | tee -a $ST

@@ -15,7 +15,7 @@ Q=${Q:-100000000}
 run() {
   local name=$1; shift
   if [ "$TARGET" = c3 ]; then
-    timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 "$R/bench.py" --queries $Q --steps 2 --warmup 1 --no-cpu > "$OUT/$name.log" 2>&1
+    timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 "$R/bench.py" --queries $Q --steps 2 --warmup 1 --no-cpu --no-one-shot > "$OUT/$name.log" 2>&1
   else
     MESH_AMD_NO_CPU=1 timeout -k 10 600 rocprofv3 "$@" --output-format csv -d "$OUT/$name" -o run -- python3 "$R/scripts/bench_configs.py" --configs $TARGET --reps 1 > "$OUT/$name.log" 2>&1
   fi
