@@ -158,9 +158,11 @@ int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* 
  * (msh_tree_nearest*, msh_tree_nearest_bary*, msh_tree_nearest_stats).  The automatic grid comes in two sizes: the
  * coarse one (about 8 cells per face, at most 2^23 cells: C3 G = 200, 256 MB, ~11 ms) once the handle's calls have
  * brought at least one row per 16 of its cells (C3: 500k rows; a few small calls on a large mesh walk from the root
- * instead of paying the build), the fine one (about 64 cells per face, at most 2^26: C3 G = 400, 2.05 GB, ~65 ms)
- * once they have brought 16 rows per fine cell (C3: ~1G rows), or at the next call after msh_tree_set_entry_cut(t,
- * -1) (a caller that keeps the tree for many batches).  A grid asked for with msh_tree_set_entry_cut is built by the
+ * instead of paying the build), the fine one (twice the coarse resolution: about 64 cells per face, C3 G = 400,
+ * 2.05 GB) once they have brought 16 rows per fine cell (C3: ~1G rows), or at the next call after
+ * msh_tree_set_entry_cut(t, -1) (a caller that keeps the tree for many batches).  The fine grid is built from the
+ * coarse one (its cells' start lists and centre walks begin there); asked for with no grid installed, the coarse grid
+ * is built first and freed after (C3: ~57 ms for both).  build_ms counts both.  A grid asked for with msh_tree_set_entry_cut is built by the
  * next call whatever its size.  Trees used only for rays, visibility or the normals metric never hold it; trees of
  * < 4096 faces never get one.  The call that builds it is synchronous, also for the *_device entry points (the cut's
  * build waits for its own cell-centre queries): a caller that captures *_device calls in a graph or needs them

@@ -512,7 +512,7 @@ static void free_entry_cut(msh_tree* t) {
 // The automatic grid comes in two sizes (round 6).  A coarse grid, 8 cells per leaf (at most 2^23 cells; C3: G = 200,
 // 256 MB), is built by the call that brings the handle's rows to 1/16 of its cells (C3: 500k rows); it costs a
 // one-shot caller ~10 ms.  The fine grid, 64 cells per leaf (at most 2^26; C3: G = 400, 2.05 GB), replaces it once the
-// handle has answered kFineRowsPerCell rows per fine cell (C3: ~1G rows): its ~70-ms build pays back after that many
+// handle has answered kFineRowsPerCell rows per fine cell (C3: ~1G rows): its ~46-ms build pays back after that many
 // queries (C3 100M-query batches: ~3 ms faster each than with the coarse grid).  msh_tree_set_entry_cut(t, -1) asks
 // for the fine grid at the next call (a caller that keeps the tree for many batches, as bench.py does).
 // Round-5 figures (68-B cells of 8 entries and a separate hint), C3 in M q/s: 8 per leaf, 2^23 cells: G = 200, 46.9
@@ -527,6 +527,14 @@ static void free_entry_cut(msh_tree* t) {
 #ifndef MSH_CUT_MAX_LOG2
 #define MSH_CUT_MAX_LOG2 26
 #endif
+#ifndef MSH_CUT_FROM_HALF
+#define MSH_CUT_FROM_HALF 1
+#endif
+constexpr bool kCutFromHalf = MSH_CUT_FROM_HALF;
+#ifndef MSH_CUT_STAGED
+#define MSH_CUT_STAGED 1
+#endif
+constexpr bool kCutStaged = MSH_CUT_STAGED;
 constexpr size_t kCutCoarsePerLeaf = 8;
 constexpr int kCutCoarseMaxLog2 = 23;
 constexpr size_t kFineRowsPerCell = 16;
@@ -537,14 +545,20 @@ static size_t auto_cut_cells(const msh_tree* t, bool fine) {
 // record bytes per cell: 32 (4-B entries) for trees of <= 2^20 leaves, else 64
 static size_t cut_rec_bytes(const msh_tree* t) { return t->T <= kEnt4MaxLeaves ? 32 : 64; }
 
-// cells per axis of the grid to build: the caller's G, else the automatic fine or coarse grid
+// cells per axis of the grid to build: the caller's G, else the automatic coarse grid or the fine one at twice its
+// resolution (8 x its cells: the fine grid's cells nest in the coarse one's, whose records then start them)
 static int cut_grid(const msh_tree* t, bool fine) {
     if (t->cut_req > 0) return t->cut_req;
-    return std::max(16, (int)std::lround(std::cbrt((double)auto_cut_cells(t, fine))));
+    const int Gc = std::max(16, (int)std::lround(std::cbrt((double)auto_cut_cells(t, false))));
+    if (!fine) return Gc;
+    return kCutFromHalf ? 2 * Gc : std::max(16, (int)std::lround(std::cbrt((double)auto_cut_cells(t, true))));
 }
 
-// The grid's cell centres are answered exactly by the tree (walks from the root: no cut is installed while one is
-// built), then every cell is cut from the root (nearest.hip k_cut_level).  Round 6 also tried a pyramid -- the
+// The grid's cell centres are answered exactly by the tree (walks from the installed coarse grid when the fine one is
+// built, else from the root), then every cell is cut (nearest.hip k_cut_level): from the enclosing coarse cell's start
+// list when the coarse grid is installed and this grid is twice its resolution, else from the root.  C3 (round 6):
+// coarse grid 11 ms; fine grid from it 46 ms (centre walks 26, cut 18), 67 ms from the root
+// (profiles/r06_c3_cut_staged_ab.jsonl).  Round 6 also tried a pyramid -- the
 // coarsest grid answered exactly, each finer level cut from the coarser one's records with hints taken from the 8
 // coarse cells around it -- which built C3's grid in 41 ms instead of ~70 but started queries from worse hints:
 // 49.4 node visits per query against 42.5, 2.02-2.06 G q/s against 2.32-2.36 (profiles/r06_c3_cut_levels_ab.jsonl).
@@ -606,7 +620,13 @@ static int build_entry_cut(msh_tree* t, bool fine) {
                 st = MSH_ENOMEM;
                 break;
             }
-            if ((st = cut_level(t, G, lo, w, dp.as<double>(), dhint.as<int>(), cut, e4, s)) != MSH_OK) break;
+            // the installed grid, when it is this one at half resolution over the same box (the automatic coarse grid
+            // under the fine one), gives every cell its start list (k_cut_level)
+            const uint32_t* half = nullptr;
+            if (kCutFromHalf && t->d_cut && 2 * t->cut_G == G && t->cut_wide == (e4 ? 0 : 1) &&
+                t->cut_lo[0] == lo[0] && t->cut_lo[1] == lo[1] && t->cut_lo[2] == lo[2])
+                half = t->d_cut;
+            if ((st = cut_level(t, G, lo, w, dp.as<double>(), dhint.as<int>(), cut, e4, s, half)) != MSH_OK) break;
             (void)hipEventRecord(e1, s);
             if ((e = hipStreamSynchronize(s)) != hipSuccess) {
                 set_error("entry cut build: %s", hipGetErrorString(e));
@@ -663,6 +683,19 @@ static void ensure_entry_cut(msh_tree* t, size_t S) {
         return;
     }
     const std::string keep = g_err;
+    // a fine grid asked for with no grid installed (msh_tree_set_entry_cut(t, -1) before the first call) is built in
+    // two stages: the coarse grid first (its own centre walks from the root), then the fine one, whose centre walks and
+    // start lists begin from it (build_entry_cut); the coarse grid is then freed like an upgrade's
+    double staged_ms = 0.0;
+    if (kCutStaged && fine && !t->d_cut && t->cut_req < 0) {
+        t->cut_state = kCutOff;
+        if (build_entry_cut(t, false) == MSH_OK) {
+            staged_ms = t->cut_ms;
+        } else {
+            (void)hipGetLastError();  // the fine grid is then built from the root
+            t->d_cut = nullptr;
+        }
+    }
     // while a grid is built its cell-centre queries start from the coarse grid, when one is installed (an upgrade),
     // else from the root; the state is off meanwhile, so the build's own queries do not build again
     uint32_t* old = t->d_cut;
@@ -676,6 +709,7 @@ static void ensure_entry_cut(msh_tree* t, size_t S) {
     t->cut_state = kCutOff;
     const int st = build_entry_cut(t, fine);
     if (st == MSH_OK) {
+        t->cut_ms += staged_ms;
         if (old) {
             if (t->ws_done) (void)hipEventSynchronize(t->ws_done);
             (void)dfree(old);
@@ -756,6 +790,10 @@ static int build_triangles(msh_tree* t, const double* v, size_t Pall, const uint
 }
 
 static const size_t kSortMin = 4096;  // below this the query Morton sort costs more than it saves
+#ifndef MSH_ALONG_LAZY
+#define MSH_ALONG_LAZY 1
+#endif
+static constexpr bool kAlongLazy = MSH_ALONG_LAZY;  // alongnormal rays read at perm[slot] instead of gathered
 
 // Query order for S point rows (device): below kSortMin the caller's arrays are used as they are;
 // otherwise Morton codes + radix sort give the permutation (ws.vals).  With allow_lazy (closest-point
@@ -775,8 +813,8 @@ static int sort_queries(msh_tree* t, const double* d_q, const double* d_n, size_
     float lo[3], hi[3];
     query_box(t, lo, hi);
     MSH_TRY(query_sort(lo, hi, d_q, S, kQuerySortLo, ws, s));
-    if (allow_lazy && !d_n) {
-        *ord = QueryOrder{d_q, nullptr, ws.vals.as<uint32_t>(), ws.inv.as<uint32_t>(), false};
+    if (allow_lazy) {
+        *ord = QueryOrder{d_q, d_n, ws.vals.as<uint32_t>(), ws.inv.as<uint32_t>(), false};
         return MSH_OK;
     }
     MSH_TRY(ws.qs.reserve(3 * S * sizeof(double)));
@@ -1928,7 +1966,7 @@ int msh_tree_nearest_alongnormal_device(msh_tree* t, const double* d_p, const do
     hipStream_t s = pick(t, stream);
     WsOrder order(t, s);
     QueryOrder ord;
-    MSH_TRY(sort_queries(t, d_p, d_n, S, s, &ord));
+    MSH_TRY(sort_queries(t, d_p, d_n, S, s, &ord, kAlongLazy));
     return launch_alongnormal(t, ord, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_dist}, s);
 }
 
@@ -1952,7 +1990,7 @@ int msh_tree_nearest_alongnormal_stats(msh_tree* t, const double* d_p, const dou
     {
         WsOrder order(t, s);
         QueryOrder ord;
-        MSH_TRY(sort_queries(t, d_p, d_n, S, s, &ord));
+        MSH_TRY(sort_queries(t, d_p, d_n, S, s, &ord, kAlongLazy));
         MSH_TRY(t->ws.stats.reserve(8 * sizeof(unsigned long long)));
         MSH_HIP(hipMemsetAsync(t->ws.stats.ptr, 0, 8 * sizeof(unsigned long long), s));
         MSH_TRY(launch_alongnormal_stats(t, ord, S, t->ws.stats.as<unsigned long long>(), s));

@@ -244,8 +244,10 @@ int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32
 constexpr int kCutK = 7;
 constexpr size_t kEnt4MaxLeaves = (size_t)1 << 20;  // 4-B stack / cut entries: refs in [-2^20, 2^20), 21 bits
 int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s);
+// d_half: the records of the G/2 grid over the same box (same record size), each cell then starts from its enclosing
+// half-resolution cell's entries instead of the root; nullptr: from the root
 int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, const int* d_hint,
-              uint32_t* d_rec, bool e4, hipStream_t s);
+              uint32_t* d_rec, bool e4, hipStream_t s, const uint32_t* d_half = nullptr);
 // d_inv[face] = the leaf holding it (T words)
 int face_leaf_map(const msh_tree* tree, uint32_t* d_inv, hipStream_t s);
 // closest point (and part) of each row q[i] on face d_face[i] (the traversal's answer construction); d_inv from

@@ -1629,7 +1629,8 @@ __global__ __launch_bounds__(kBlock) void k_cut_centres(int G, double lx, double
     q[3 * cell + 2] = lz + ((double)iz + 0.5) * wz;
 }
 
-// The entry cut, one thread per cell of a G^3 grid (cell (ix, iy, iz) = row (iz G + iy) G + ix), from the root, with
+// The entry cut, one thread per cell of a G^3 grid (cell (ix, iy, iz) = row (iz G + iy) G + ix), from the root (or from
+// the records of the installed half-resolution grid, d_half below), with
 // U(c) = the exact distance from the centre c to its closest point (pts[cell], the centre's own query; its face's leaf
 // is hint[cell]).
 // R = (U(c) + 2r) (1 + 1e-6), r the cell's half-diagonal + 0.1 %.  For q in the cell, d(q) <= U(c) + r, so a subtree
@@ -1648,12 +1649,18 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
                                                       double ox, double oy, double oz, double tm, int G, double lx,
                                                       double ly, double lz, double wx, double wy, double wz,
                                                       const double* __restrict__ pts, const int* __restrict__ hint,
-                                                      uint32_t* __restrict__ rec) {
+                                                      uint32_t* __restrict__ rec, const uint32_t* __restrict__ crec) {
     constexpr int kw = E4 ? 8 : 16;  // record words
-    const size_t n = (size_t)G * G * G;
-    const size_t cell = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    if (cell >= n) return;
-    const size_t ix = cell % (size_t)G, iy = (cell / (size_t)G) % (size_t)G, iz = cell / ((size_t)G * G);
+    // a wave takes a 4 x 4 x 4 brick of cells (bricks in row order): its cells' start lists share their nodes, and
+    // under a half-resolution grid it reads 8 records
+    const size_t gid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t GB = ((size_t)G + 3) / 4, brick = gid >> 6;
+    const unsigned ln = (unsigned)(gid & 63);
+    if (brick >= GB * GB * GB) return;
+    const size_t ix = (brick % GB) * 4 + (ln & 3), iy = ((brick / GB) % GB) * 4 + ((ln >> 2) & 3),
+                 iz = (brick / (GB * GB)) * 4 + (ln >> 4);
+    if (ix >= (size_t)G || iy >= (size_t)G || iz >= (size_t)G) return;
+    const size_t cell = (iz * G + iy) * G + ix;
     const D3 c = D3{lx + ((double)ix + 0.5) * wx, ly + ((double)iy + 0.5) * wy, lz + ((double)iz + 0.5) * wz};
     const double r = 0.5 * sqrt(wx * wx + wy * wy + wz * wz) * 1.001;
     int ref[kCutK];
@@ -1670,6 +1677,39 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
     {
         const double R = (sqrt(sqdist(c, pc)) + 2.0 * r) * (1.0 + 1e-6);
         if (R < INFINITY) limf = __double2float_ru(R * R * kSlack);  // NaN / inf (no answer): the root only
+    }
+    if (crec) {
+        // start from the enclosing cell of the half-resolution grid (G = 2 Gc, the same box): a subtree its record left
+        // out lies farther than d(q) from every q of that cell, this one's included.  Its entries keep their records'
+        // bounds -- already lower bounds for every q of the larger cell -- as (sqrt(b) + r)^2, which the store below
+        // maps back to <= sqrt(b); a node's bound is raised when it is loaded
+        const size_t Gc = (size_t)G / 2;
+        const uint32_t* cr = crec + (((iz >> 1) * Gc + (iy >> 1)) * Gc + (ix >> 1)) * kw;
+        m = 0;
+        for (int k = 0; k < kCutK; ++k) {
+            uint32_t rv, bb;
+            if (E4) {
+                const uint32_t e = cr[1 + k];
+                if (e & 0x80000000u) break;  // empty: the list ends
+                rv = (uint32_t)Ent4::ref(e);
+                bb = __float_as_uint(Ent4::bound(e));
+            } else {
+                rv = cr[2 + 2 * k];
+                if (rv == kCutEmpty) break;
+                bb = cr[3 + 2 * k];
+            }
+            if (__uint_as_float(bb) > limf) continue;  // farther than R from c (its bound holds from c too)
+            const float sb = sqrtf(__uint_as_float(bb)) + (float)r;
+            ref[m] = (int)rv;
+            bd[m] = sb * sb;  // its rounding is far inside the store's 1e-5 shrink
+            stuck[m] = 0;
+            ++m;
+        }
+        if (m == 0) {
+            ref[0] = 0;
+            bd[0] = -1.f;
+            m = 1;
+        }
     }
     const double o3[3] = {ox, oy, oz};
     const QF qf = make_qf(c, o3, tm);
@@ -1830,18 +1870,18 @@ int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream
 }
 
 int cut_level(const msh_tree* tree, int G, const double* lo, const double* w, const double* d_pts, const int* d_hint,
-              uint32_t* d_rec, bool e4, hipStream_t s) {
-    const size_t n = (size_t)G * G * G;
-    const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
+              uint32_t* d_rec, bool e4, hipStream_t s, const uint32_t* d_half) {
+    const size_t GB = ((size_t)G + 3) / 4;  // 4^3-cell bricks, one per wave
+    const unsigned nb = (unsigned)((GB * GB * GB * 64 + kBlock - 1) / kBlock);
     const TriRec* tris = static_cast<const TriRec*>(tree->d_leaves);
     const double tm = tree_margin(tree->half_diag);
     TimedLaunch tl("cut_level", s);
     if (e4)
         k_cut_level<true><<<nb, kBlock, 0, s>>>(tree->d_nodes, tris, tree->origin[0], tree->origin[1], tree->origin[2], tm,
-                                               G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_pts, d_hint, d_rec);
+                                               G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_pts, d_hint, d_rec, d_half);
     else
         k_cut_level<false><<<nb, kBlock, 0, s>>>(tree->d_nodes, tris, tree->origin[0], tree->origin[1], tree->origin[2], tm,
-                                                G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_pts, d_hint, d_rec);
+                                                G, lo[0], lo[1], lo[2], w[0], w[1], w[2], d_pts, d_hint, d_rec, d_half);
     MSH_HIP(hipGetLastError());
     return MSH_OK;
 }

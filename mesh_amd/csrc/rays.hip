@@ -523,6 +523,7 @@ struct RayArgs {
     const double* n;
     size_t S;
     const uint32_t* perm;  // slot -> caller's row (sorted rays), nullptr: identity
+    bool lazy;             // p / n are the caller's rows, read at perm[slot] (not gathered into slot order)
     double* out_dist;
     uint32_t* out_face;
     double* out_pt;
@@ -596,8 +597,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
         if (MODE == 0) {
             // every lane stays in the wave's loop (the leaf rounds use all 64); a lane past the rays only helps
             const bool live = i < a.S;
-            const D3 p = live ? D3{a.p[3 * i], a.p[3 * i + 1], a.p[3 * i + 2]} : D3{0.0, 0.0, 0.0};
-            const D3 n = live ? D3{a.n[3 * i], a.n[3 * i + 1], a.n[3 * i + 2]} : D3{0.0, 0.0, 1.0};
+            const size_t r = live && a.perm ? (size_t)a.perm[i] : i;  // the caller's row
+            const size_t ri = a.lazy ? r : i;
+            const D3 p = live ? D3{a.p[3 * ri], a.p[3 * ri + 1], a.p[3 * ri + 2]} : D3{0.0, 0.0, 0.0};
+            const D3 n = live ? D3{a.n[3 * ri], a.n[3 * ri + 1], a.n[3 * ri + 2]} : D3{0.0, 0.0, 1.0};
             const D3 dp = ray_dir(p, n), pr = vsub(p, org);
             AlongPol pol{a.tris, p, n, make_rayf(pr, dp, a.M, true), INFINITY, MSH_NO_FACE, -1, INFINITY};
 #if MSH_ALONG_LIST
@@ -609,8 +612,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
 #endif
             if (STATS || !live) continue;
             const double dist = pol.best == INFINITY ? 1e100 : pol.best;
-            const size_t r = a.perm ? (size_t)a.perm[i] : i;  // the caller's row (scattered store)
-            a.out_dist[r] = dist;
+            a.out_dist[r] = dist;  // scattered stores to the caller's row
             a.out_face[r] = pol.best_face;
             const D3 h = pol.hit();
             a.out_pt[3 * r] = h.x;
@@ -699,6 +701,7 @@ int launch_alongnormal(const msh_tree* tree, const QueryOrder& ord, size_t S, co
     a.nodes = tree->d_nodes; a.tris = static_cast<const TriRec*>(tree->d_leaves); a.T = tree->T;
     a.p = ord.q; a.n = ord.n;
     a.perm = ord.perm;  // rays run in slot order and store their answers to the caller's rows
+    a.lazy = !ord.gathered;
     a.out_dist = o.w; a.out_face = o.face; a.out_pt = o.pt;
     return launch_rays<0, false>(t, a, S, s, "alongnormal");
 }
@@ -798,6 +801,8 @@ int launch_alongnormal_stats(const msh_tree* tree, const QueryOrder& ord, size_t
     RayArgs a{};
     a.nodes = tree->d_nodes; a.tris = static_cast<const TriRec*>(tree->d_leaves); a.T = tree->T;
     a.p = ord.q; a.n = ord.n;
+    a.perm = ord.gathered ? nullptr : ord.perm;
+    a.lazy = !ord.gathered;
     a.stats = d_counts;
     return launch_rays<0, true>(t, a, S, s, "alongnormal_stats");
 }

@@ -43,16 +43,22 @@ def main():
     pt = torch.empty((S, 3), dtype=torch.float64, device="cuda")
     out = {"lib": os.path.basename(_native.LIB_PATH), "build_id": _native.build_id()}
 
+    import time
+    walls = {}
+
     def run(name, fn):
         fn()
         torch.cuda.synchronize()
         _native.timing_reset()
         _native.timing_enable(True)
+        t0 = time.perf_counter()
         for _ in range(args.reps):
             fn()
         torch.cuda.synchronize()
+        walls[name] = (time.perf_counter() - t0) / args.reps * 1e3
         _native.timing_enable(False)
         ms, cnt = _native.timing_get(name)
+        walls[name + "_parts"] = {k: _native.timing_get(k)[0] / args.reps for k in ("morton", "sort", "gather")}
         return ms / max(cnt, 1)
 
     k_a = run("alongnormal", lambda: alongnormal_device(tree, dp, dn, d, fc, pt))
@@ -60,7 +66,9 @@ def main():
     _native.check(_native.lib().msh_tree_nearest_alongnormal_stats(tree.ptr, dp.data_ptr(), dn.data_ptr(), S,
                                                                     _native.ctypes.byref(nodes),
                                                                     _native.ctypes.byref(leaves)))
-    out["alongnormal"] = {"kernel_ms": k_a, "rays_per_s_kernel": S / k_a * 1e3, "nodes_per_ray": nodes.value / S,
+    out["alongnormal"] = {"kernel_ms": k_a, "rays_per_s_kernel": S / k_a * 1e3, "wall_ms": walls["alongnormal"],
+                          "rays_per_s_device": S / walls["alongnormal"] * 1e3,
+                          "order_ms": walls["alongnormal_parts"], "nodes_per_ray": nodes.value / S,
                           "leaves_per_ray": leaves.value / S,
                           "sha": [sha(d), sha(fc), sha(pt)]}
     if args.brute:
@@ -83,7 +91,7 @@ def main():
     k_v = run("visibility", lambda: visibility_device(tree, dc, vis, ndc, dvn))
     _native.check(_native.lib().msh_visibility_stats(tree.ptr, dc.data_ptr(), C, 1e-3, _native.ctypes.byref(nodes),
                                                       _native.ctypes.byref(leaves)))
-    out["visibility"] = {"kernel_ms": k_v, "rays_per_s_kernel": C * P / k_v * 1e3, "nodes_per_ray": nodes.value / (C * P),
+    out["visibility"] = {"kernel_ms": k_v, "wall_ms": walls["visibility"], "rays_per_s_kernel": C * P / k_v * 1e3, "nodes_per_ray": nodes.value / (C * P),
                          "leaves_per_ray": leaves.value / (C * P), "sha": [sha(vis), sha(ndc)]}
     print(json.dumps(out), flush=True)
 
