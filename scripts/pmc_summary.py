@@ -119,8 +119,9 @@ def main():
                          "the box by profile_pmc.sh)")
     ap.add_argument("--queries", type=float, default=1e8)
     ap.add_argument("--freq", type=int, default=224)
-    ap.add_argument("--build-traversals", type=int, default=1,
-                    help="traversals per run that belong to the tree build (the entry cut's cell centres), dropped")
+    ap.add_argument("--build-traversals", type=int, default=2,
+                    help="traversals per run that belong to the tree build (the entry cut's cell centres: since round 6 "
+                         "the coarse grid's, then the fine grid's), dropped")
     args = ap.parse_args()
     S = int(args.queries)
     allc = {}
