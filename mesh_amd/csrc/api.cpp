@@ -221,13 +221,13 @@ void DevBuf::release() {
 
 void Workspace::release() {
     DevBuf* all[] = {&keys, &vals, &keys_alt, &vals_alt, &hist, &scan, &q, &n, &out_a, &out_b, &out_c, &out_d,
-                     &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w, &resume};
+                     &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w, &resume, &p2cand};
     for (DevBuf* b : all) b->release();
 }
 
 size_t Workspace::bytes() const {
     const DevBuf* all[] = {&keys, &vals, &keys_alt, &vals_alt, &hist, &scan, &q, &n, &out_a, &out_b, &out_c, &out_d,
-                           &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w, &resume};
+                           &flags, &counters, &spill, &stats, &ranges, &qs, &ns, &inv, &res, &res_w, &resume, &p2cand};
     size_t t = 0;
     for (const DevBuf* b : all) t += b->bytes;
     return t;

@@ -74,7 +74,7 @@ struct DevBuf {
 // results / staging).
 struct Workspace {
     DevBuf keys, vals, keys_alt, vals_alt, hist, scan, q, n, out_a, out_b, out_c, out_d, flags, counters, spill, stats,
-        ranges, qs, ns, inv, res, res_w, resume;
+        ranges, qs, ns, inv, res, res_w, resume, p2cand;
     void release();
     size_t bytes() const;
 };

@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <vector>
 #include <type_traits>
 
 #include "internal.h"
@@ -51,9 +52,33 @@ struct DeferRec {
     int32_t leaf;
     uint32_t roff;   // first of the query's resume entries (KnnArgs::resume)
     double best;
-    uint64_t rcnt;   // resume entries: pass 1's unexplored work (0: pass 2 starts at the root)
+    uint32_t rcnt;   // resume entries: pass 1's unexplored work (0: pass 2 starts at the root)
+    uint32_t sbound; // pass 2, an item split over waves: their shared bound, fp32 bits rounded up (atomicMin)
 };
 static_assert(sizeof(DeferRec) == 32, "DeferRec must be 32 B");
+
+// Pass 2 ends with its longest item: on C3 every deferred query lies near the sphere's centre, and their walks grow
+// steeply as they approach it (12.5M shard: 8,239 items of 250 node visits on average, the longest 19,688;
+// profiles/r06_c3_shard_pass2_r5_vs_r6.jsonl, r06_c3_p2_items.json).  So the items whose pass-1 distance is within
+// kP2Heavy of the largest one (k_p2_plan) are split over kP2Split waves, dealt before the others: part p takes every
+// kP2Split-th of the item's resume entries, the parts share their bound through DeferRec::sbound, and k_knn_combine
+// merges their candidates.  (Splitting every item: 12.5M shard pass 2 0.63 -> 0.50 ms at 2 parts, 0.68 at 4; 100M
+// 1.14 -> 3.2 ms at 4: the parts' fixed costs.)
+#ifndef MSH_P2_SPLIT
+#define MSH_P2_SPLIT 8
+#endif
+#ifndef MSH_P2_HEAVY
+#define MSH_P2_HEAVY 0.97
+#endif
+constexpr unsigned kP2Split = MSH_P2_SPLIT;
+constexpr double kP2Heavy = MSH_P2_HEAVY;      // split items with sqrt(best) >= kP2Heavy sqrt(the largest best)
+constexpr unsigned kP2SplitItems = 1u << 16;  // at most this many items split: 8 MB of candidates
+constexpr uint32_t kP2Whole = 0xFFFFFFFFu;    // DeferRec::sbound of an item run whole (k_p2_plan)
+struct P2Cand {
+    double best;
+    uint32_t face;
+    int32_t leaf;
+};
 
 // MODE: 0 closest point (face, part, point), 1 normals metric (face, point), 2 vertex NN (index,
 // distance), 3 closest point + barycentric weights (face, point, weights)
@@ -116,6 +141,12 @@ struct KnnArgs {
     uint2* resume;
     unsigned* n_resume;
     unsigned resume_cap;
+    // pass 2: the heavy items (k_p2_plan: heavy[0, *n_heavy)) run as kP2Split parts whose candidates go to cand
+    // (k_knn_combine); max_best: pass 1's largest deferred best (d2 bits)
+    P2Cand* cand;
+    unsigned* heavy;
+    unsigned* n_heavy;
+    unsigned long long* max_best;
 };
 
 // root node and fp32 query of slot i (batched trees: its mesh's root and origin)
@@ -871,6 +902,8 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                 r.roff = 0;
                 r.best = pol.best;
                 r.rcnt = 0;
+                r.sbound = 0x7F800000u;  // +inf
+                if (a.max_best) atomicMax(a.max_best, (unsigned long long)__double_as_longlong(pol.best));
                 if (a.resume) {
                     // what is left of this walk: the pending entry (w.node, not yet visited: bound 0) above the stack
                     const unsigned cnt = (unsigned)w.sp + 1;
@@ -1058,6 +1091,8 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
                             r.roff = 0;
                             r.best = pol.best;
                             r.rcnt = 0;
+                            r.sbound = 0x7F800000u;  // +inf
+                            if (a.max_best) atomicMax(a.max_best, (unsigned long long)__double_as_longlong(pol.best));
                             a.deferred[slot] = r;
                             active = false;
                             deferred = true;  // pass 2 owns this query
@@ -1143,11 +1178,21 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
     const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     unsigned n_nodes = 0, n_leaves = 0;
     unsigned* next_item = a.n_deferred + 32;  // items are dealt dynamically: their costs vary widely
+    // work units: the heavy items' K parts first (consecutive units: the parts run side by side), then every item in
+    // order, the heavy ones skipped
+    constexpr unsigned K = (MODE == 0 || MODE == 3) ? kP2Split : 1u;
+    const unsigned nsplit = (K > 1 && a.cand) ? min(*a.n_heavy, kP2SplitItems) : 0u;
+    const unsigned nunit = nsplit * K + total;
     for (;;) {
-        unsigned item = 0;
-        if (lane == 0) item = atomicAdd(next_item, 1u);
-        item = __shfl(item, 0);
-        if (item >= total) break;
+        unsigned unit = 0;
+        if (lane == 0) unit = atomicAdd(next_item, 1u);
+        unit = __shfl(unit, 0);
+        if (unit >= nunit) break;
+        const bool split = unit < nsplit * K;
+        const unsigned hidx = split ? unit / K : 0u;
+        const unsigned item = split ? a.heavy[hidx] : unit - nsplit * K;
+        const unsigned part = split ? unit % K : 0u, kk = split ? K : 1u;
+        if (!split && nsplit && a.deferred[item].sbound != kP2Whole) continue;  // a heavy item: its parts ran above
         const unsigned item_nodes0 = n_nodes, item_leaves0 = n_leaves;
         const DeferRec r = a.deferred[item];
         const size_t i = r.slot;
@@ -1156,6 +1201,15 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         const int root = query_root(a, i, q, qf);
         auto pol = make_pol<MODE>(a, i, q);
         pol.shared = r.best;  // pass-1 best: an upper bound of the final best
+        unsigned rounds = 0;
+        // an item's parts share their bound: every 8th round a part publishes its own and takes the others'
+        auto share = [&]() {
+            if (!split || (++rounds & 7u) != 0u) return;
+            unsigned old = 0;
+            if (lane == 0) old = atomicMin(&a.deferred[item].sbound, __float_as_uint(__double2float_ru(pol.shared)));
+            old = (unsigned)__shfl((int)old, 0);
+            pol.shared = fmin(pol.shared, (double)__uint_as_float(old));
+        };
         if (lane == 0) {
             pol.best = r.best;
             pol.best_face = r.face;
@@ -1170,11 +1224,15 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         uint2* W = &front[wv][0][0];  // kWork contiguous entries
         constexpr int kWork = 2 * kFront;
         // pass 1's unexplored entries (oldest first, its pending node on top), or the root
+        // (a split item's part p: entries p, p + K, p + 2K, ... in their order; the root, when pass 1 left none, to part 0)
         const int rc = (int)r.rcnt;
         int top = 1;
         if (rc > 0 && rc <= kWork - 128) {
-            for (int j = lane; j < rc; j += 64) W[j] = a.resume[r.roff + j];
-            top = rc;
+            const int cnt = rc > (int)part ? (rc - (int)part + (int)kk - 1) / (int)kk : 0;
+            for (int m = lane; m < cnt; m += 64) W[m] = a.resume[r.roff + part + (unsigned)m * kk];
+            top = cnt;
+        } else if (part != 0) {
+            top = 0;
         } else if (lane == 0) {
             W[0] = make_uint2((unsigned)root, 0u);
         }
@@ -1223,6 +1281,7 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
             top = base + __popcll(b0) + __popcll(b1);
             __builtin_amdgcn_wave_barrier();
             pol.shared = fmin(pol.shared, wave_min(pol.best));
+            share();
             pol.relim();
         }
         // overflow: deal the list to the lanes (entry j -> lane j % 64), then depth-first walks
@@ -1234,13 +1293,16 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         while (__any(active)) {
             if (active) active = w.step<decltype(pol), false>(a.nodes, qf, pol, lds, spill, n_nodes, n_leaves);
             pol.shared = fmin(pol.shared, wave_min(pol.best));
+            share();
             pol.relim();
         }
         double best = pol.best;
         uint32_t face = pol.best_face;
         int leaf = pol.best_leaf;
         wave_lexmin(best, face, leaf);
-        if (lane == 0 && !STATS) {
+        if (split) {  // the part's candidate; k_knn_combine merges the item's parts and writes the answer
+            if (lane == 0 && !STATS) a.cand[(size_t)hidx * K + part] = P2Cand{best, face, leaf};
+        } else if (lane == 0 && !STATS) {
             pol.best = best;
             pol.best_face = face;
             pol.best_leaf = leaf;
@@ -1253,6 +1315,7 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
                 atomicAdd(&a.stats[44], (unsigned long long)w);
                 atomicMax(&a.stats[45], (unsigned long long)w);
                 atomicAdd(&a.stats[46], 1ull);
+                a.deferred[item].sbound = w;  // development dump (MESH_AMD_P2_DUMP): the item's visits
             }
         }
         __builtin_amdgcn_wave_barrier();
@@ -1261,6 +1324,49 @@ __global__ __launch_bounds__(kBlock) void k_knn_coop(KnnArgs a) {
         atomicAdd(&a.stats[0], (unsigned long long)n_nodes);
         atomicAdd(&a.stats[1], (unsigned long long)n_leaves);
         if (lane == 0) atomicAdd(&a.stats[6], 1ull);  // waves x deferred items (pass-2 work units)
+    }
+}
+
+// pass 2's plan: the deferred items whose pass-1 distance is within kP2Heavy of the largest are listed in heavy[]
+// (sbound +inf, the parts' shared bound); every other item is marked to run whole (sbound kP2Whole)
+__global__ __launch_bounds__(kBlock) void k_p2_plan(KnnArgs a) {
+    const unsigned total = min(*a.n_deferred, a.max_deferred);
+    const double mb = __longlong_as_double((long long)*a.max_best);
+    const double thr = mb * (kP2Heavy * kP2Heavy);
+    for (unsigned k = blockIdx.x * kBlock + threadIdx.x; k < total; k += gridDim.x * kBlock) {
+        uint32_t mark = kP2Whole;
+        if (a.deferred[k].best >= thr) {
+            const unsigned h = atomicAdd(a.n_heavy, 1u);
+            if (h < kP2SplitItems) {
+                a.heavy[h] = k;
+                mark = 0x7F800000u;
+            }
+        }
+        a.deferred[k].sbound = mark;
+    }
+}
+
+// the answers of the split pass-2 items: the lexicographic (d2, face) minimum of their parts' candidates (each
+// part starts from the pass-1 candidate, so every part holds a real one)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_knn_combine(KnnArgs a) {
+    if constexpr (MODE == 0 || MODE == 3) {
+        const unsigned nsplit = min(*a.n_heavy, kP2SplitItems);
+        const unsigned h = blockIdx.x * kBlock + threadIdx.x;
+        if (h >= nsplit) return;
+        const DeferRec r = a.deferred[a.heavy[h]];
+        const size_t i = r.slot;
+        const D3 q = load_q(a, i);
+        auto pol = make_pol<MODE>(a, i, q);
+        pol.best = r.best;
+        pol.best_face = r.face;
+        pol.best_leaf = r.leaf;
+#pragma unroll
+        for (unsigned p = 0; p < kP2Split; ++p) {
+            const P2Cand c = a.cand[(size_t)h * kP2Split + p];
+            if (c.leaf >= 0) pol.offer(c.best, c.face, c.leaf);
+        }
+        write_result<MODE>(a, i, q, pol);
     }
 }
 
@@ -1391,11 +1497,12 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     const unsigned ncu = (unsigned)device_cus(tree->device);
     Workspace& ws = tree->ws;
     // counters: 8 group counters (one 128-B line each) + the deferred count + pass 2's item counter + the resume arena's
-    MSH_TRY(ws.counters.reserve(11 * 32 * sizeof(unsigned)));
+    // + the largest deferred best + the heavy items' count
+    MSH_TRY(ws.counters.reserve(13 * 32 * sizeof(unsigned)));
     a.counters = ws.counters.as<unsigned>();
     a.n_deferred = a.counters + 8 * 32;
     a.n_resume = a.counters + 10 * 32;
-    MSH_HIP(hipMemsetAsync(a.counters, 0, 11 * 32 * sizeof(unsigned), s));  // + the pass-2 item counter
+    MSH_HIP(hipMemsetAsync(a.counters, 0, 13 * 32 * sizeof(unsigned), s));  // + the pass-2 item counter
     const size_t n_lead = (a.S + kLead - 1) / kLead;
     const unsigned max_tiles = (unsigned)((a.S + 63) / 64);
     const unsigned nblk_max = std::min<unsigned>((max_tiles + 3) / 4, ncu * kKnnBlocksPerCU);
@@ -1433,6 +1540,16 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
     a.deferred = dbuf.as<DeferRec>();
     a.resume = nullptr;
     a.resume_cap = 0;
+    a.cand = nullptr;
+    a.heavy = nullptr;
+    a.n_heavy = a.counters + 12 * 32;
+    a.max_best = reinterpret_cast<unsigned long long*>(a.counters + 11 * 32);
+    const unsigned split_cap = std::min<unsigned>(a.max_deferred, kP2SplitItems);
+    if (kP2Split > 1 && (MODE == 0 || MODE == 3) && !STATS) {
+        MSH_TRY(ws.p2cand.reserve((size_t)split_cap * (kP2Split * sizeof(P2Cand) + sizeof(unsigned))));
+        a.cand = ws.p2cand.as<P2Cand>();
+        a.heavy = reinterpret_cast<unsigned*>(a.cand + (size_t)split_cap * kP2Split);
+    }
 #if MSH_RESUME
     if (a.list) {  // resume arena: ~48 entries per expected deferral (C3: 75k deferred of 100M queries), >= 1M entries
         const size_t cap = std::min<size_t>((size_t)1 << 26, std::max<size_t>((size_t)1 << 20, 48 * (a.S / 1024 + 1024)));
@@ -1490,8 +1607,28 @@ static int launch_knn(msh_tree* tree, KnnArgs a, hipStream_t s, const char* time
         }
         {
             TimedLaunch t2(STATS ? "knn_pass2_stats" : "knn_pass2", s);
+            if (a.cand) {
+                k_p2_plan<<<64, kBlock, 0, s>>>(a);
+                MSH_HIP(hipGetLastError());
+            }
             k_knn_coop<MODE, STATS><<<nblk2, kBlock, 0, s>>>(a);
             MSH_HIP(hipGetLastError());
+            if (a.cand) {
+                k_knn_combine<MODE><<<(split_cap + kBlock - 1) / kBlock, kBlock, 0, s>>>(a);
+                MSH_HIP(hipGetLastError());
+            }
+        }
+        if (STATS && getenv("MESH_AMD_P2_DUMP")) {  // development: the deferred items with their pass-2 visits
+            unsigned nd = 0;
+            MSH_HIP(hipMemcpyAsync(&nd, a.n_deferred, sizeof(unsigned), hipMemcpyDeviceToHost, s));
+            MSH_HIP(hipStreamSynchronize(s));
+            nd = std::min(nd, a.max_deferred);
+            std::vector<DeferRec> h(nd);
+            if (nd) MSH_HIP(hipMemcpy(h.data(), a.deferred, nd * sizeof(DeferRec), hipMemcpyDeviceToHost));
+            if (FILE* f = fopen(getenv("MESH_AMD_P2_DUMP"), "wb")) {
+                fwrite(h.data(), sizeof(DeferRec), nd, f);
+                fclose(f);
+            }
         }
     }
     return MSH_OK;
