@@ -1958,16 +1958,22 @@ int msh_tree_nearest_stats(msh_tree* t, const double* d_q, size_t S, uint64_t* n
     return MSH_OK;
 }
 
+// the rays' walks start from the tree's entry cut (built by the automatic policy on these rows too: rays_cut)
+static int along_run(msh_tree* t, const double* d_p, const double* d_n, size_t S, double* d_dist, uint32_t* d_face,
+                     double* d_pt, hipStream_t s) {
+    WsOrder order(t, s);
+    QueryOrder ord;
+    MSH_TRY(sort_queries(t, d_p, d_n, S, s, &ord, kAlongLazy));
+    return launch_alongnormal(t, ord, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_dist}, s);
+}
+
 int msh_tree_nearest_alongnormal_device(msh_tree* t, const double* d_p, const double* d_n, size_t S, double* d_dist,
                                         uint32_t* d_face, double* d_pt, void* stream) {
     MSH_TRY(check_tree(t, kTriangles, "msh_tree_nearest_alongnormal_device"));
     MSH_TRY(check_count(S, "msh_tree_nearest_alongnormal_device"));
     if (S == 0) return MSH_OK;
-    hipStream_t s = pick(t, stream);
-    WsOrder order(t, s);
-    QueryOrder ord;
-    MSH_TRY(sort_queries(t, d_p, d_n, S, s, &ord, kAlongLazy));
-    return launch_alongnormal(t, ord, S, SlotOut{d_face, nullptr, d_pt, nullptr, d_dist}, s);
+    ensure_entry_cut(t, S);
+    return along_run(t, d_p, d_n, S, d_dist, d_face, d_pt, pick(t, stream));
 }
 
 static int read_stats(msh_tree* t, hipStream_t s, uint64_t* nodes, uint64_t* leaves) {
@@ -1986,6 +1992,7 @@ int msh_tree_nearest_alongnormal_stats(msh_tree* t, const double* d_p, const dou
     if (!nodes || !leaves) { set_error("msh_tree_nearest_alongnormal_stats: null argument"); return MSH_EINVAL; }
     *nodes = *leaves = 0;
     if (S == 0) return MSH_OK;
+    ensure_entry_cut(t, S);
     hipStream_t s = t->stream;
     {
         WsOrder order(t, s);
@@ -2022,13 +2029,13 @@ int msh_tree_nearest_alongnormal(msh_tree* t, const double* p, const double* n, 
     if (!p || !n || !dist || !face || !pt) { set_error("msh_tree_nearest_alongnormal: null argument"); return MSH_EINVAL; }
     return fan_out(t, S, 84, [&](msh_tree* h, size_t r0, size_t S_h) {
         MSH_TRY(use_device(h->device));
+        ensure_entry_cut(h, S);  // the whole call's rows, once (as nearest_host)
         const std::vector<HostArr> arrs = {{p + 3 * r0, nullptr, 24}, {n + 3 * r0, nullptr, 24}, {nullptr, dist + r0, 8},
                                            {nullptr, face + r0, 4}, {nullptr, pt + 3 * r0, 24}};
         return pipelined(h, S_h, arrs, [&](size_t, size_t c, const std::vector<char*>& d) {
-            return msh_tree_nearest_alongnormal_device(h, reinterpret_cast<const double*>(d[0]),
-                                                       reinterpret_cast<const double*>(d[1]), c,
-                                                       reinterpret_cast<double*>(d[2]), reinterpret_cast<uint32_t*>(d[3]),
-                                                       reinterpret_cast<double*>(d[4]), h->stream);
+            return along_run(h, reinterpret_cast<const double*>(d[0]), reinterpret_cast<const double*>(d[1]), c,
+                             reinterpret_cast<double*>(d[2]), reinterpret_cast<uint32_t*>(d[3]),
+                             reinterpret_cast<double*>(d[4]), h->stream);
         });
     });
 }

@@ -242,6 +242,7 @@ int unpermute_results(const QRes* d_res, const double* d_w, int nw, const uint32
 // kCutK start entries per cell (the hint takes the record's eighth word; round 5: 8 entries of 8 B + a separate hint;
 // 4 entries: 1773-1800 M q/s against 8, 16: 1285, C3, profiles/r03_c3_entry_cut_ab.jsonl)
 constexpr int kCutK = 7;
+constexpr uint32_t kCutEmpty = 0x7FFFFFFFu;  // empty 64-B record entry: not a node id (ids < T - 1 <= 2^31 - 2) nor a ~leaf
 constexpr size_t kEnt4MaxLeaves = (size_t)1 << 20;  // 4-B stack / cut entries: refs in [-2^20, 2^20), 21 bits
 int cut_centres(int G, const double* lo, const double* w, double* d_q, hipStream_t s);
 // d_half: the records of the G/2 grid over the same box (same record size), each cell then starts from its enclosing

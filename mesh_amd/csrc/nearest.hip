@@ -621,7 +621,6 @@ constexpr size_t kLeadMinLeaves = 4096;  // smaller trees skip the leader phases
 // s = sqrt(bound from c) - r: a lower bound of the squared distance from q to its subtree.  The entries go
 // on the stack with it, nearest to c popped first, and the walk starts from the first entry within the
 // current limit.  false: no entry survives the hint's bound (the hint is the answer).
-constexpr uint32_t kCutEmpty = 0x7FFFFFFFu;  // not a node id (ids < T - 1 <= 2^31 - 2) nor a ~leaf
 constexpr size_t kNoCell = ~(size_t)0;
 // grid cell of q, or kNoCell outside the grid (or without a cut)
 __device__ inline size_t cut_cell(const KnnArgs& a, const D3& q) {
@@ -1910,7 +1909,9 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
         }
     uint32_t* out = rec + cell * kw;
     out[0] = (uint32_t)best_leaf;
-    if (!E4) out[1] = 0u;
+    // 64-B records: word 1 the radius R around c the list covers (every subtree left out lies farther from c), fp32
+    // rounded down (0: none) -- the alongnormal walks' first phase reads it (rays.hip)
+    if (!E4) out[1] = limf < INFINITY ? __float_as_uint(__double2float_rd(sqrt((double)limf / kSlack) * (1.0 - 1e-7))) : 0u;
     for (int k = 0; k < kCutK; ++k) {
         uint32_t ev = 0xFFFFFFFFu, rv = kCutEmpty, bb = 0u;
         if (k < m) {

@@ -165,7 +165,10 @@ struct AlongPol {
     uint32_t best_face;
     int best_leaf;  // the hit point is rebuilt from it at the end (hit()), not carried through the walk
     float limf;     // best^2 (1 + 2^-40) rounded up to fp32 (the unit of the keys), refreshed when best improves
-    __device__ void relim() { limf = best == INFINITY ? INFINITY : __double2float_ru(best * best * kSlack); }
+    float capf;     // the entry cut's first phase: the squared radius its start list covers (else +inf)
+    __device__ void relim() {
+        limf = best == INFINITY ? capf : fminf(__double2float_ru(best * best * kSlack), capf);
+    }
     __device__ void children(const NodeV& nd, bool& h0, bool& h1, float& k0, float& k1) const {
         ray_child_line_dist2(nd, rf, h0, h1, k0, k1);
         h0 = h0 && k0 <= limf;
@@ -407,10 +410,20 @@ constexpr int kVisStack = MSH_VIS_PF ? 12 : kStack;
 #ifndef MSH_ALONG_PF
 #define MSH_ALONG_PF 1
 #endif
+// alongnormal walks start from the closest-point entry cut when the tree holds one (traverse_along_pend)
+#ifndef MSH_ALONG_CUT
+#define MSH_ALONG_CUT 1
+#endif
+// rec / rho (round 6): the ray's cell of the closest-point entry cut and the radius around p its start list covers (every
+// subtree left out of it is farther than rho from p: k_rays).  The walk first runs from the list with the bound capped
+// at rho; a hit within rho is then the answer (every face with a hit that near lies in the list's subtrees, and they
+// were walked with the usual bound below the cap).  Otherwise the walk runs again from the root, keeping its best hit.
 template <bool STATS>
 __device__ inline void traverse_along_pend(const BNode* __restrict__ nodes, size_t T, AlongPol& pol, bool active,
                                            uint2* __restrict__ lds, uint2* __restrict__ spill, unsigned& n_nodes,
-                                           unsigned& n_leaves, const float4* nb, uint32_t wsl) {
+                                           unsigned& n_leaves, const float4* nb, uint32_t wsl,
+                                           const uint32_t* __restrict__ rec = nullptr, bool wide = false,
+                                           float rho = -1.f) {
     int node = 0, sp = 0;
     int pend = -1;  // this lane's leaf waiting for the wave's leaf phase
     size_t guard = 0;
@@ -421,8 +434,42 @@ __device__ inline void traverse_along_pend(const BNode* __restrict__ nodes, size
     auto fetch = [&]() {
         if (MSH_ALONG_PF && node >= 0) node_prefetch(nodes, node, wsl);
     };
+    bool phase_a = false;
+    if (active && rec) {  // the start list, nearest first: the first entry is the node, the others stacked (key 0)
+        int ent[kCutK];
+        int m = 0;
+#pragma unroll
+        for (int k = 0; k < kCutK; ++k) {
+            const uint32_t e = wide ? rec[2 + 2 * k] : rec[1 + k];
+            const bool ok = wide ? e != kCutEmpty : (int)e >= 0;
+            ent[k] = ok ? (wide ? (int)e : __builtin_amdgcn_sbfe((int)e, 0, 21)) : 0;
+            if (ok) m = k + 1;
+        }
+        if (m > 0) {
+#pragma unroll
+            for (int k = kCutK - 1; k >= 1; --k)
+                if (k < m) {
+                    stack_put<kAlongStack>(lds, spill, sp, make_uint2((unsigned)ent[k], 0u));
+                    ++sp;
+                }
+            node = ent[0];
+            phase_a = true;
+        }
+    }
     if (active) fetch();
     for (;;) {
+        if (phase_a && !active && pend < 0) {  // the start list is exhausted
+            phase_a = false;
+            if (!(pol.best <= (double)rho)) {  // no hit within rho: the whole tree, from the root
+                pol.capf = INFINITY;
+                pol.relim();
+                node = 0;
+                sp = 0;
+                guard = 0;
+                active = true;
+                fetch();
+            }
+        }
         const bool can = active && pend < 0;
         if (__ballot(can) == 0ull) {
             if (__ballot(pend >= 0) == 0ull) break;
@@ -545,6 +592,11 @@ struct RayArgs {
     int spill_depth;
     double org[3];  // tree origin
     double M;       // the tree's half-diagonal (hits lie within M of org)
+    // alongnormal: the tree's closest-point entry cut (traverse_along_pend's first phase); nullptr: from the root
+    const uint32_t* cut;
+    int cut_wide, cut_G;
+    double cut_lo[3], cut_iw[3];
+    double cut_r;  // the cells' half-diagonal as the cut's build took it, rounded down
 };
 
 __device__ inline unsigned dequeue_tile_r(unsigned* counters, unsigned ntiles, unsigned group) {
@@ -602,13 +654,51 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
             const D3 p = live ? D3{a.p[3 * ri], a.p[3 * ri + 1], a.p[3 * ri + 2]} : D3{0.0, 0.0, 0.0};
             const D3 n = live ? D3{a.n[3 * ri], a.n[3 * ri + 1], a.n[3 * ri + 2]} : D3{0.0, 0.0, 1.0};
             const D3 dp = ray_dir(p, n), pr = vsub(p, org);
-            AlongPol pol{a.tris, p, n, make_rayf(pr, dp, a.M, true), INFINITY, MSH_NO_FACE, -1, INFINITY};
+            AlongPol pol{a.tris, p, n, make_rayf(pr, dp, a.M, true), INFINITY, MSH_NO_FACE, -1, INFINITY, INFINITY};
+            const bool go = live && finite_d3(p) && finite_d3(dp);
+            // the entry cut's cell of p: its start list covers every face within rho of p, rho = R - |p - c| with R
+            // the radius the build kept around the centre c (64-B records hold it; else d(c) + 2r, d(c): c's distance
+            // to its hint face, the face the build found closest to c); both rounded down
+            const uint32_t* rec = nullptr;
+            float rho = -1.f;
+            if (a.cut && go) {
+                const double G = (double)a.cut_G;
+                const double ux = (p.x - a.cut_lo[0]) * a.cut_iw[0], uy = (p.y - a.cut_lo[1]) * a.cut_iw[1],
+                             uz = (p.z - a.cut_lo[2]) * a.cut_iw[2];
+                if (ux >= 0.0 && ux < G && uy >= 0.0 && uy < G && uz >= 0.0 && uz < G) {
+                    const unsigned ix = (unsigned)ux, iy = (unsigned)uy, iz = (unsigned)uz;
+                    const uint32_t* r = a.cut + (((size_t)iz * a.cut_G + iy) * a.cut_G + ix) * (a.cut_wide ? 16 : 8);
+                    const int hint = (int)r[0];
+                    if (hint >= 0) {
+                        const D3 c = D3{a.cut_lo[0] + ((double)ix + 0.5) / a.cut_iw[0],
+                                        a.cut_lo[1] + ((double)iy + 0.5) / a.cut_iw[1],
+                                        a.cut_lo[2] + ((double)iz + 0.5) / a.cut_iw[2]};
+                        double R;
+                        if (a.cut_wide) {
+                            R = (double)__uint_as_float(r[1]);  // the build's radius (k_cut_level)
+                        } else {  // 32-B records have no room for it: d(c) from the hint face
+                            D3 ta, tb, tc, o;
+                            uint32_t f;
+                            int part;
+                            load_tri(a.tris, hint, ta, tb, tc, f);
+                            R = (sqrt(closest_on_triangle(c, ta, tb, tc, o, part)) + 2.0 * a.cut_r) * (1.0 - 1e-9);
+                        }
+                        const double rr = (R - sqrt(sqdist(p, c))) * (1.0 - 1e-9);
+                        if (rr > 0.0) {
+                            rec = r;
+                            rho = __double2float_rd(rr);
+                            pol.capf = __double2float_ru((double)rho * (double)rho * kSlack);
+                            pol.relim();
+                        }
+                    }
+                }
+            }
 #if MSH_ALONG_LIST
             traverse_along_list<STATS>(a.nodes, a.T, pol, live && finite_d3(p) && finite_d3(dp), lds, spill, ring, rbd,
                                        rbfl, n_nodes, n_leaves);
 #else
-            traverse_along_pend<STATS>(a.nodes, a.T, pol, live && finite_d3(p) && finite_d3(dp), lds, spill, n_nodes,
-                                       n_leaves, nb, wsl);
+            traverse_along_pend<STATS>(a.nodes, a.T, pol, go, lds, spill, n_nodes, n_leaves, nb, wsl, rec,
+                                       a.cut_wide != 0, rho);
 #endif
             if (STATS || !live) continue;
             const double dist = pol.best == INFINITY ? 1e100 : pol.best;
@@ -684,8 +774,9 @@ static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, c
     a.spill = nullptr;
     a.spill_depth = 0;
     const int lds_depth = MODE == 0 ? kAlongStack : kVisStack;
-    if (tree->max_depth + 1 > lds_depth) {
-        a.spill_depth = tree->max_depth + 1 - lds_depth + 1;
+    const int need = tree->max_depth + 1 + (a.cut ? kCutK : 0);  // + the entry cut's start list
+    if (need > lds_depth) {
+        a.spill_depth = need - lds_depth + 1;
         MSH_TRY(tree->ws.spill.reserve((size_t)nblk * kBlock * (size_t)a.spill_depth * sizeof(uint2)));
         a.spill = tree->ws.spill.as<uint2>();
     }
@@ -695,9 +786,26 @@ static int launch_rays(msh_tree* tree, RayArgs a, size_t nrays, hipStream_t s, c
     return MSH_OK;
 }
 
+// the tree's closest-point entry cut for the alongnormal walks (traverse_along_pend's first phase)
+static void along_cut(const msh_tree* tree, RayArgs& a) {
+    if (!MSH_ALONG_CUT || !tree->d_cut || tree->B != 1 || tree->cut_G <= 0) return;
+    a.cut = tree->d_cut;
+    a.cut_wide = tree->cut_wide;
+    a.cut_G = tree->cut_G;
+    double w2 = 0.0;
+    for (int k = 0; k < 3; ++k) {
+        a.cut_lo[k] = tree->cut_lo[k];
+        a.cut_iw[k] = tree->cut_iw[k];
+        const double w = 1.0 / tree->cut_iw[k];
+        w2 += w * w;
+    }
+    a.cut_r = 0.5 * sqrt(w2) * 1.001 * (1.0 - 1e-9);  // k_cut_level's r, rounded down
+}
+
 int launch_alongnormal(const msh_tree* tree, const QueryOrder& ord, size_t S, const SlotOut& o, hipStream_t s) {
     msh_tree* t = const_cast<msh_tree*>(tree);
     RayArgs a{};
+    along_cut(tree, a);
     a.nodes = tree->d_nodes; a.tris = static_cast<const TriRec*>(tree->d_leaves); a.T = tree->T;
     a.p = ord.q; a.n = ord.n;
     a.perm = ord.perm;  // rays run in slot order and store their answers to the caller's rows
@@ -799,6 +907,7 @@ int launch_alongnormal_stats(const msh_tree* tree, const QueryOrder& ord, size_t
                              hipStream_t s) {
     msh_tree* t = const_cast<msh_tree*>(tree);
     RayArgs a{};
+    along_cut(tree, a);
     a.nodes = tree->d_nodes; a.tris = static_cast<const TriRec*>(tree->d_leaves); a.T = tree->T;
     a.p = ord.q; a.n = ord.n;
     a.perm = ord.gathered ? nullptr : ord.perm;

@@ -263,8 +263,8 @@ def test_entry_cut_wide_records():
 
 def test_entry_cut_lazy_and_failure_fallback(oracle):
     # The automatic cut comes in two sizes: the coarse grid (8 cells per face: C2 48^3) is built by the closest-point
-    # call that brings the handle's rows to one per 16 of its cells (6,888), never by the build, by rays or by the
-    # normals metric; the fine one (64 per face: 96^3) after 16 rows per fine cell, or at the next call after
+    # or alongnormal call that brings the handle's rows to one per 16 of its cells (6,888), never by the build, by
+    # visibility or by the normals metric; the fine one (64 per face: 96^3) after 16 rows per fine cell, or at the next call after
     # set_entry_cut(-1) (a kept tree); a requested grid is built by the next call whatever its size; a cut that cannot
     # be built (here 4096^3 cells: more than one query call holds) is not an error: the handle records the failure and
     # its queries start at the root with the same answers.
@@ -278,11 +278,11 @@ def test_entry_cut_lazy_and_failure_fallback(oracle):
     t = spatialsearch.aabbtree_compute(v, f)
     assert t.entry_cut_info()["state"] == "pending"
     nrm = np.tile([[0.0, 0.0, 1.0]], (q.shape[0], 1))
-    spatialsearch.aabbtree_nearest_alongnormal(t, q, nrm)
+    spatialsearch.aabbtree_nearest_alongnormal(t, q[:3000], nrm[:3000])  # alongnormal rows count too (round 6)
     assert t.entry_cut_info()["state"] == "pending" and t.entry_cut_info()["bytes"] == 0
-    _nearest_tree(t, q[:5000])  # 5,000 rows: below the coarse grid's volume, walks from the root
+    _nearest_tree(t, q[:3000])  # 6,000 rows: below the coarse grid's volume, walks from the root
     assert t.entry_cut_info()["state"] == "pending" and t.entry_cut_info()["bytes"] == 0
-    again = _nearest_tree(t, q)  # 45,000 rows in all: the coarse grid is built by this call
+    again = _nearest_tree(t, q)  # 46,000 rows in all: the coarse grid is built by this call
     info = t.entry_cut_info()
     assert info["state"] == "built" and info["G"] == 48 and info["bytes"] == 48 ** 3 * 32 and info["build_ms"] > 0
     for a, b in zip(ref, again):
@@ -536,6 +536,50 @@ def test_alongnormal_bit_exact(oracle):
     hit = bd < 1e100
     assert np.array_equal(pt[hit], bpt[hit])
     assert (d[~hit] == 1e100).all() and (face[~hit] == 0xFFFFFFFF).all() and np.isnan(pt[~hit]).all()
+
+
+def test_alongnormal_entry_cut_bit_exact(oracle):
+    # alongnormal walks start from the closest-point entry cut's start list, the bound capped at the radius the list
+    # covers around p, and walk again from the root when no hit lies that near (rays.hip traverse_along_pend): the
+    # answers equal the walks from the root for the 48^3 (coarse), 96^3 (fine, built from the coarse one) and 8^3
+    # grids, on near-surface rays (mostly answered from the list), far and random rays (mostly walked again), rays on
+    # the grid's cell faces and outside it, and rays that miss; 6,000 of them against brute force
+    from mesh_amd import spatialsearch
+    v, f = W.c2_mesh()
+    rng = np.random.default_rng(71)
+    near, fi = W.surface_samples(v, f, 20_000, seed=72, sigma=0.01)
+    tri = v[f[fi].astype(np.int64)]
+    nn = np.cross(tri[:, 1] - tri[:, 0], tri[:, 2] - tri[:, 0])
+    nn /= np.linalg.norm(nn, axis=1)[:, None]
+    far, _ = W.surface_samples(v, f, 5_000, seed=73, sigma=0.3)
+    lo, hi = v.min(0), v.max(0)
+    box = rng.uniform(lo - 0.5 * (hi - lo), hi + 0.5 * (hi - lo), (10_000, 3))
+    onf = rng.uniform(lo, hi, (3_000, 3))
+    c, e = 0.5 * (lo + hi), 1.25 * 0.5 * (hi - lo)
+    ax = rng.integers(0, 3, 3_000)
+    onf[np.arange(3_000), ax] = (c - e)[ax] + rng.integers(0, 49, 3_000) * (2 * e / 48)[ax]
+    rd = rng.normal(size=(18_000, 3))
+    rd /= np.linalg.norm(rd, axis=1)[:, None]
+    p = np.vstack([near, far, box, onf, [[50.0, 50.0, 50.0]] * 4])
+    n = np.vstack([nn, rd[:5_000], rd[5_000:15_000], rd[15_000:18_000], [[1.0, 0.0, 0.0]] * 4])
+    t = spatialsearch.aabbtree_compute(v, f)
+    outs = []
+    for g in (0, 48, -1, 8):
+        t.set_entry_cut(g)
+        outs.append(spatialsearch.aabbtree_nearest_alongnormal(t, p, n))
+        info = t.entry_cut_info()
+        assert info["state"] == ("off" if g == 0 else "built"), info
+        assert info["G"] == (0 if g == 0 else (96 if g < 0 else g)), info
+    for o in outs[1:]:
+        assert np.array_equal(outs[0][0], o[0]) and np.array_equal(outs[0][1], o[1])
+        assert np.array_equal(outs[0][2].view(np.int64), o[2].view(np.int64))  # NaN points of misses too
+    rows = np.concatenate([rng.choice(20_000, 3_000, replace=False), 20_000 + rng.choice(18_004, 3_000, replace=False)])
+    bd, bf, bpt = oracle.brute_alongnormal(v, f, p[rows], n[rows])
+    d, face, pt = outs[2]
+    assert np.array_equal(d[rows], bd) and np.array_equal(face[rows], bf)
+    hit = bd < 1e100
+    assert hit.sum() > 3_000
+    assert np.array_equal(pt[rows][hit], bpt[hit])
 
 
 def test_visibility_random_exact(oracle):
