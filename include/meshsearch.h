@@ -153,9 +153,11 @@ int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* 
 
 /* Entry cut of a triangle tree (no reference counterpart: derived acceleration data).  A grid
  * of G^3 cells over the scene box widened by 1/4, one record per cell -- its hint leaf and 7 start entries: 32 B for
- * trees of up to 2^20 faces, 64 B beyond -- from which closest-point queries start their walks instead of the root;
- * it changes where a walk starts, never an answer.  It is built lazily by a closest-point call of the handle
- * (msh_tree_nearest*, msh_tree_nearest_bary*, msh_tree_nearest_stats).  The automatic grid comes in two sizes: the
+ * trees of up to 2^20 faces, 64 B beyond (which also hold the radius each list covers) -- from which closest-point
+ * queries start their walks instead of the root, and so do nearest_alongnormal rays (their walk first covers that
+ * radius around p, and starts again from the root only when no hit lies that near); it changes where a walk starts,
+ * never an answer.  It is built lazily by a closest-point or alongnormal call of the handle (msh_tree_nearest*,
+ * msh_tree_nearest_bary*, msh_tree_nearest_alongnormal*, and their _stats).  The automatic grid comes in two sizes: the
  * coarse one (about 8 cells per face, at most 2^23 cells: C3 G = 200, 256 MB, ~11 ms) once the handle's calls have
  * brought at least one row per 16 of its cells (C3: 500k rows; a few small calls on a large mesh walk from the root
  * instead of paying the build), the fine one (twice the coarse resolution: about 64 cells per face, C3 G = 400,
@@ -163,7 +165,7 @@ int msh_tree_query_order(msh_tree* tree, const double* d_q, size_t S, uint32_t* 
  * msh_tree_set_entry_cut(t, -1) (a caller that keeps the tree for many batches).  The fine grid is built from the
  * coarse one (its cells' start lists and centre walks begin there); asked for with no grid installed, the coarse grid
  * is built first and freed after (C3: ~57 ms for both).  build_ms counts both.  A grid asked for with msh_tree_set_entry_cut is built by the
- * next call whatever its size.  Trees used only for rays, visibility or the normals metric never hold it; trees of
+ * next call whatever its size.  Trees used only for visibility or the normals metric never hold it; trees of
  * < 4096 faces never get one.  The call that builds it is synchronous, also for the *_device entry points (the cut's
  * build waits for its own cell-centre queries): a caller that captures *_device calls in a graph or needs them
  * asynchronous calls msh_tree_set_entry_cut and makes one small query first (or sets G = 0).

@@ -488,9 +488,9 @@ struct WsOrder {
 // G = 64 / 126 / 160: 1718 / 1742-1765 / 1782 M q/s against 1789-1800 at G = 200); the cell centres are answered
 // by the tree itself, then every cell's start entries are cut from the root.  Trees under kCutMinLeaves
 // leaves start at the root (their top levels are few).  Built lazily (ensure_entry_cut): the automatic grid once the
-// handle's closest-point calls have brought kCutAutoRows rows per cell... in all, so ray-only, visibility and
+// handle's closest-point and alongnormal calls have brought enough rows (ensure_entry_cut), so visibility and
 // normals-metric trees and a few small calls never pay its memory or build time; msh_tree_set_entry_cut chooses the
-// grid (built by the next closest-point call) or turns it off.
+// grid (built by the next closest-point or alongnormal call) or turns it off.
 constexpr size_t kCutMinLeaves = 4096;
 enum { kCutPending = 0, kCutBuilt = 1, kCutOff = 2, kCutFailed = 3 };
 
