@@ -535,11 +535,6 @@ constexpr bool kCutFromHalf = MSH_CUT_FROM_HALF;
 #define MSH_CUT_STAGED 1
 #endif
 constexpr bool kCutStaged = MSH_CUT_STAGED;
-// the fine grid without centre walks: each cell's hint and bound from its coarse cell's hint face (k_cut_level)
-#ifndef MSH_CUT_FINE_NOWALK
-#define MSH_CUT_FINE_NOWALK 0
-#endif
-constexpr bool kCutFineNoWalk = MSH_CUT_FINE_NOWALK;
 constexpr size_t kCutCoarsePerLeaf = 8;
 constexpr int kCutCoarseMaxLog2 = 23;
 constexpr size_t kFineRowsPerCell = 16;
@@ -592,13 +587,6 @@ static int build_entry_cut(msh_tree* t, bool fine) {
     const bool e4 = t->T <= kEnt4MaxLeaves;
     const size_t rb = cut_rec_bytes(t);
     hipStream_t s = t->stream;
-    // the installed grid, when it is this one at half resolution over the same box (the automatic coarse grid under
-    // the fine one), gives every cell its start list (k_cut_level)
-    const uint32_t* hrec = nullptr;
-    if (kCutFromHalf && t->d_cut && 2 * t->cut_G == G && t->cut_wide == (e4 ? 0 : 1) && t->cut_lo[0] == lo[0] &&
-        t->cut_lo[1] == lo[1] && t->cut_lo[2] == lo[2])
-        hrec = t->d_cut;
-    const bool walks = !(kCutFineNoWalk && hrec);
     hipEvent_t e0 = nullptr, e1 = nullptr;
     MSH_HIP(hipEventCreate(&e0));
     hipError_t e = hipEventCreate(&e1);
@@ -612,7 +600,6 @@ static int build_entry_cut(msh_tree* t, bool fine) {
     {
         DevBuf dq, df, dp, dinv, dhint;
         do {
-            if (walks) {
             if ((st = dq.reserve(n * 3 * sizeof(double))) != MSH_OK) break;
             if ((st = df.reserve(n * sizeof(uint32_t))) != MSH_OK) break;
             if ((st = dp.reserve(n * 3 * sizeof(double))) != MSH_OK) break;
@@ -627,16 +614,19 @@ static int build_entry_cut(msh_tree* t, bool fine) {
                 break;
             if ((st = cut_hints(t, df.as<uint32_t>(), n, dinv.as<uint32_t>(), dhint.as<int>(), s)) != MSH_OK) break;
             dq.release();  // the centres' rows are not needed by the cut itself
-            }
             e = dmalloc(&cut, n * rb);
             if (e != hipSuccess) {
                 set_error("hipMalloc entry cut (%zu cells): %s", n, hipGetErrorString(e));
                 st = MSH_ENOMEM;
                 break;
             }
-            if ((st = cut_level(t, G, lo, w, walks ? dp.as<double>() : nullptr, walks ? dhint.as<int>() : nullptr, cut,
-                                e4, s, hrec)) != MSH_OK)
-                break;
+            // the installed grid, when it is this one at half resolution over the same box (the automatic coarse grid
+            // under the fine one), gives every cell its start list (k_cut_level)
+            const uint32_t* half = nullptr;
+            if (kCutFromHalf && t->d_cut && 2 * t->cut_G == G && t->cut_wide == (e4 ? 0 : 1) &&
+                t->cut_lo[0] == lo[0] && t->cut_lo[1] == lo[1] && t->cut_lo[2] == lo[2])
+                half = t->d_cut;
+            if ((st = cut_level(t, G, lo, w, dp.as<double>(), dhint.as<int>(), cut, e4, s, half)) != MSH_OK) break;
             (void)hipEventRecord(e1, s);
             if ((e = hipStreamSynchronize(s)) != hipSuccess) {
                 set_error("entry cut build: %s", hipGetErrorString(e));

@@ -1802,30 +1802,13 @@ __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ 
     int ref[kCutK];
     float bd[kCutK];  // bound from c; -1: not formed yet (the root)
     int stuck[kCutK];  // list size at which the entry could not be expanded (0: not stuck): retried only once smaller
-    // without centre walks (pts == nullptr, a half-resolution grid installed): the enclosing coarse cell's hint face
-    // stands in for c's answer -- its closest point to c bounds d(c) from above, so the list stays conservative
-    int best_leaf;
-    D3 pc;
-    if (pts) {
-        best_leaf = hint[cell];
-        pc = D3{pts[3 * cell], pts[3 * cell + 1], pts[3 * cell + 2]};
-    } else {
-        const size_t Gc = (size_t)G / 2;
-        best_leaf = (int)crec[(((iz >> 1) * Gc + (iy >> 1)) * Gc + (ix >> 1)) * kw];
-        pc = D3{NAN, NAN, NAN};
-        if (best_leaf >= 0) {
-            D3 ta, tb, tc;
-            uint32_t f;
-            int part;
-            load_tri(tris, best_leaf, ta, tb, tc, f);
-            closest_on_triangle(c, ta, tb, tc, pc, part);
-        }
-    }
+    const int best_leaf = hint[cell];
     ref[0] = 0;
     bd[0] = -1.f;
     stuck[0] = 0;
     int m = 1;
     // U(c): the distance from c to its answer's point (pts: the centre walks' closest points; NaN without an answer)
+    const D3 pc = D3{pts[3 * cell], pts[3 * cell + 1], pts[3 * cell + 2]};
     float limf = INFINITY;
     {
         const double R = (sqrt(sqdist(c, pc)) + 2.0 * r) * (1.0 + 1e-6);
