@@ -797,9 +797,10 @@ static constexpr bool kAlongLazy = MSH_ALONG_LAZY;  // alongnormal rays read at 
 
 // Query order for S point rows (device): below kSortMin the caller's arrays are used as they are;
 // otherwise Morton codes + radix sort give the permutation (ws.vals).  With allow_lazy (closest-point
-// launches without normals) the traversal reads row perm[i] itself and writes the inverse permutation
-// (ws.inv); otherwise the rows (and normals, when given) are gathered once into slot order
-// (ws.qs / ws.ns) with the inverse permutation (gathering the closest-point rows too measured 3 % slower on C3).
+// launches, and alongnormal rays with their normals: kAlongLazy) the traversal reads row perm[i] itself (and the
+// closest-point one writes the inverse permutation, ws.inv); otherwise (the normals-metric queries) the rows and
+// normals are gathered once into slot order (ws.qs / ws.ns) with the inverse permutation (gathering the
+// closest-point rows too measured 3 % slower on C3; the C5 rays 0.5 ms slower, profiles/r06_c5_along_lazy_ab.jsonl).
 // Queries are ordered by the Hilbert index of their cell of a 256^3 grid (the top 24 bits of their 30-bit Morton
 // code, mapped through sort.hip's Hilbert state table; 3 radix passes): C3's 100M queries put ~6 in a cell, and the
 // traversal runs the same node counts as with the full code.  The order within a cell is the caller's (stable sort).

@@ -18,10 +18,11 @@
 //
 // Execution shape: one lane per ray, persistent near-first traversal over the same 64-B nodes as K2:
 // box tests are conservative fp32 slab tests of the ray against both children's oriented boxes (the ray
-// projected once per node onto the node frame; make_rayf / ray_child_slabs), and alongnormal also bounds
-// the children's distance from p with K2's packed test.  alongnormal rays are Morton-sorted by
-// their source and gathered into slot order like K2's queries; visibility rays run vertex-major per
-// camera over a Morton order of the vertices (cached per tree), so neighbouring lanes cast
+// projected once per node onto the node frame; make_rayf / ray_child_slabs), and alongnormal bounds each
+// child's distance from p along the line (ray_child_line_dist2: the line's interval in it).  alongnormal rays
+// are sorted by their source like K2's queries, each lane reading its ray at perm[slot], and their walks start
+// from the closest-point entry cut when the tree holds one (traverse_along_pend); visibility rays run
+// vertex-major per camera over a Morton order of the vertices (cached per tree), so neighbouring lanes cast
 // neighbouring, nearly parallel rays.
 #include <algorithm>
 
