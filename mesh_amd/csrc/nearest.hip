@@ -1777,9 +1777,10 @@ __global__ __launch_bounds__(kBlock) void k_cut_centres(int G, double lx, double
 // node is loaded -- each a lower bound of the squared distance from c to what it holds.  (Exact leaf distances as the
 // leaves' bounds, dropping leaves beyond R: 0.4 % fewer leaf tests per query for 10 ms more of build on C3,
 // profiles/r06_c3_cut_build_probe.jsonl.)  An entry that cannot be expanded is retried only once the list shrank.
-// Out (E4: 32-B records of 4-B entries, trees of <= 2^20 leaves; else 64-B records of (ref, bound bits)): word 0 the
-// hint leaf, then the entries nearest-first with max(s, 0)^2 rounded down to fp32, s = sqrt(bound) (1 - 1e-5) - r
-// (1 + 1e-5): a lower bound of the squared distance from any q of the cell.
+// Out (E4: 32-B records of 4-B entries, trees of <= 2^20 leaves; else 64-B records: word 1 the radius R around c the
+// list covers, then (ref, bound bits) pairs): word 0 the hint leaf, then the entries nearest-first with max(s, 0)^2
+// rounded down to fp32, s = sqrt(bound) (1 - 1e-5) - r (1 + 1e-5): a lower bound of the squared distance from any q
+// of the cell.
 template <bool E4>
 __global__ __launch_bounds__(kBlock) void k_cut_level(const BNode* __restrict__ nodes, const TriRec* __restrict__ tris,
                                                       double ox, double oy, double oz, double tm, int G, double lx,
