@@ -601,6 +601,13 @@ __device__ inline unsigned lanes_below(unsigned long long m) {
 #define MSH_KPEND 32
 #endif
 constexpr int kPend = MSH_KPEND;
+// Tile prefetch (round 6): a wave claims its next tile while the current one's rows load.  dequeue_tile is two
+// dependent round trips to the group's counter (a load, then the atomic), paid at every tile start with the wave
+// idle: C3 100M pass 1 38.4-39.5 -> 36.3-36.4 ms, 2.35-2.41 -> 2.53-2.54 G q/s; the 12.5M shard 6.92-6.95 -> 6.76-6.78
+// ms (profiles/r06_c3_tile_prefetch_ab.jsonl)
+#ifndef MSH_TILE_PF
+#define MSH_TILE_PF 1
+#endif
 
 constexpr unsigned kRing = 256;     // ring entries per wave: < 64 left after full rounds + <= 128 per step
 constexpr size_t kListMaxLeaves = (size_t)1 << 26;  // leaf index bits of a ring entry
@@ -695,9 +702,20 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
     unsigned long long u_trav_it = 0, u_trav_lanes = 0, u_leaf_it = 0, u_leaf_lanes = 0;  // STATS: wave iterations
     unsigned n_nodes = 0, n_leaves = 0;
     unsigned n_impr = 0, n_hinted = 0, n_hint_won = 0;  // STATS: improving leaf tests, hinted queries, hint = answer
+#if MSH_TILE_PF
+    // lane 0 claims the wave's next tile of its own group while the current one's rows load (an atomic whose return
+    // is waited for with the tile's first loads), instead of at the next tile's start
+    const unsigned glo = (unsigned)(((unsigned long long)a.ntiles * group) >> 3);
+    const unsigned ghi = (unsigned)(((unsigned long long)a.ntiles * (group + 1)) >> 3);
+    unsigned nxt = ~0u;
+#endif
     for (;;) {
         unsigned tile = 0;
+#if MSH_TILE_PF
+        if (lane == 0) tile = (nxt != ~0u && glo + nxt < ghi) ? glo + nxt : dequeue_tile(a.counters, a.ntiles, group);
+#else
         if (lane == 0) tile = dequeue_tile(a.counters, a.ntiles, group);
+#endif
         tile = __shfl(tile, 0);
         if (tile >= a.ntiles) break;
         // every lane of the wave stays in the tile's loops (compacted leaf phases deal entries to all 64 lanes);
@@ -710,6 +728,9 @@ __global__ __launch_bounds__(kBlock) MSH_KNN_ATTR void k_knn(KnnArgs a) {
             live = i < a.S;
         }
         const D3 q = live ? load_q(a, i) : D3{0.0, 0.0, 0.0};
+#if MSH_TILE_PF
+        if (lane == 0) nxt = glo < ghi ? atomicAdd(&a.counters[group * 32], 1u) : ~0u;
+#endif
         if (live && a.inv_w && !a.direct) a.inv_w[a.qperm[i]] = (uint32_t)i;
         auto pol = make_pol<MODE>(a, i, q);
         const bool fin = live && finite3(q);

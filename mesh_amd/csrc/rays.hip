@@ -411,6 +411,9 @@ constexpr int kVisStack = MSH_VIS_PF ? 12 : kStack;
 #ifndef MSH_ALONG_PF
 #define MSH_ALONG_PF 1
 #endif
+#ifndef MSH_RAY_TILE_PF
+#define MSH_RAY_TILE_PF 1
+#endif
 // alongnormal walks start from the closest-point entry cut when the tree holds one (traverse_along_pend)
 #ifndef MSH_ALONG_CUT
 #define MSH_ALONG_CUT 1
@@ -641,12 +644,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(MODE == 
     uint2* spill = a.spill ? a.spill + (size_t)blockIdx.x * kBlock * (size_t)a.spill_depth + tid : nullptr;
     const unsigned group = blockIdx.x & 7u;
     const D3 org = D3{a.org[0], a.org[1], a.org[2]};
+#if MSH_RAY_TILE_PF
+    // the next tile of the wave's group is claimed while the current one's rays load (nearest.hip MSH_TILE_PF)
+    const unsigned glo = (unsigned)(((unsigned long long)a.ntiles * group) >> 3);
+    const unsigned ghi = (unsigned)(((unsigned long long)a.ntiles * (group + 1)) >> 3);
+    unsigned nxt = ~0u;
+#endif
     for (;;) {
         unsigned tile = 0;
+#if MSH_RAY_TILE_PF
+        if (lane == 0) tile = (nxt != ~0u && glo + nxt < ghi) ? glo + nxt : dequeue_tile_r(a.counters, a.ntiles, group);
+#else
         if (lane == 0) tile = dequeue_tile_r(a.counters, a.ntiles, group);
+#endif
         tile = __shfl(tile, 0);
         if (tile >= a.ntiles) break;
         const size_t i = (size_t)tile * 64 + lane;
+#if MSH_RAY_TILE_PF
+        if (lane == 0) nxt = glo < ghi ? atomicAdd(&a.counters[group * 32], 1u) : ~0u;
+#endif
         if (MODE == 0) {
             // every lane stays in the wave's loop (the leaf rounds use all 64); a lane past the rays only helps
             const bool live = i < a.S;
