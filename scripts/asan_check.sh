@@ -20,7 +20,7 @@ RT=$(ls /opt/rocm/lib/llvm/lib/clang/*/lib/linux/libclang_rt.asan-x86_64.so | he
   echo "# asan_check.sh at $(git rev-parse --short HEAD) ($(date -u +%Y-%m-%dT%H:%MZ)), runtime $RT"
   make -s -j8 -C mesh_amd/csrc asan && make -s -C oracle asan || { echo "BUILD FAILED"; exit 2; }
   echo "## pytest (loaders, ABI, oracle) with the sanitized libraries"
-  LD_PRELOAD=$RT ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:halt_on_error=1:detect_odr_violation=0 \
+  LD_PRELOAD="$RT${LD_PRELOAD:+:$LD_PRELOAD}" ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:halt_on_error=1:detect_odr_violation=0 \
     UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 \
     MESH_AMD_LIB=$PWD/build/asan/libmeshsearch.so ORACLE_LIB=$PWD/oracle/_build/asan/liboracle.so \
     MESH_AMD_ASAN_CHECK=1 \
