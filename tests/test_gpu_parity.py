@@ -172,6 +172,30 @@ def test_c3_sample_both_leaf_paths(oracle, monkeypatch):
     assert np.array_equal(outs[0][2][rows], bpt)
 
 
+def test_pass2_heavy_items_split(oracle):
+    # Deferred queries near the sphere's centre, where nearly every face is equidistant, are pass 2's longest walks:
+    # k_p2_plan lists those within 3 % of the largest deferred distance, pass 2 splits each over 8 waves that share
+    # their bound, and k_knn_combine merges the parts.  30k such rows among 300k uniform ones give the arrays of the
+    # same tree with the fine entry cut and without one (leader phases then), and 300 of them match brute force.
+    from mesh_amd import spatialsearch
+    v, f = W.c3_mesh()
+    rng = np.random.default_rng(81)
+    d = rng.normal(size=(30_000, 3))
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    q = np.concatenate([rng.uniform(-1.1, 1.1, (300_000, 3)), d * rng.uniform(0.0, 0.05, (30_000, 1))])
+    t = spatialsearch.aabbtree_compute(v, f)
+    t.set_entry_cut(-1)
+    with_cut = _nearest_tree(t, q)
+    t.set_entry_cut(0)
+    from_root = _nearest_tree(t, q)
+    for a, b in zip(with_cut, from_root):
+        assert np.array_equal(a, b)
+    rows = 300_000 + rng.choice(30_000, 300, replace=False)
+    bf, bp, bpt, _ = oracle.brute_nearest(v, f, q[rows])
+    assert np.array_equal(with_cut[0][rows], bf) and np.array_equal(with_cut[1][rows], bp)
+    assert np.array_equal(with_cut[2][rows], bpt)
+
+
 def test_workspace_handoff_between_trees(oracle, meshes):
     # a freed triangle tree hands its query workspace to the next tree built on the device (api.cpp WsPool), as
     # a tree per call (Mesh.closest_faces_and_points) does: trees built and freed in turn on two meshes answer
